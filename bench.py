@@ -1,0 +1,216 @@
+"""bench.py — Gkeys/s of the MI355X LSD radix sort (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5]
+  (N > 1: torchrun --nproc-per-node N ... bench.py --gpus N ...; one rank per GPU, RCCL)
+
+A step = one complete sort of one batch of synthetic keys already resident in HBM
+(key[i] = splitmix64(seed ^ global_i)).  Every step sorts its OWN unsorted
+buffer (generated before the timed region), so nothing is restored or skipped inside it.
+
+Default workload (config c4, the one the metric "Gkeys/s (uint32) at 1/2/4/8 MI355X" is
+quoted on): 2^27 uniform uint32 keys per GPU (weak scaling; at 8 GPUs this is BASELINE
+config 4, 2^30 keys), 8-bit digits.  At N = 1 it is a plain single-GPU sort; at N > 1 each
+rank range-partitions its shard, exchanges buckets with one RCCL all-to-all-v over xGMI and
+sorts what it received (gpuradixsort_amd/sharded.py).
+
+Rank 0 prints ONE JSON line with the driver contract plus:
+  roofline      dominant kernel (grs_onesweep_pass): algorithmic bytes per launch
+                (n_local x 2 x (key + value bytes)) / its mean duration from
+                hipEvents recorded on the sort's stream during the timed steps
+  cpu_baseline  the oracle's host std::sort on a bounded sample (rank 0, N = 1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "Gkeys/s (uint32) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
+HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+
+CONFIGS = {
+    # name: (config_id, keys per GPU, key_bits, pairs, radix_bits, description)
+    "c4": (4, 1 << 27, 32, False, 8, "C4: uint32 keys, 2^27 per GPU (2^30 at 8 GPUs), 8-bit LSD, "
+                                     "range partition + RCCL all-to-all-v"),
+    "c2": (2, 1 << 24, 32, False, 4, "C2: 16M uint32 keys, 4-bit-digit LSD"),
+    "c3": (3, 1 << 28, 32, True, 8, "C3: 256M uint32 key + uint32 payload, stable"),
+    "c5": (5, 1 << 28, 64, False, 8, "C5: 256M uint64 keys, 8 x 8-bit passes"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=0, help="override keys per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--pool-gib", type=float, default=96.0,
+                    help="HBM budget for the distinct per-step input buffers")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+
+    import oracle
+
+    keys = oracle.splitmix_keys(n_sample, key_bits, seed)
+    t = time.perf_counter()
+    if pairs:
+        vals = np.arange(n_sample, dtype=np.uint32)
+        oracle.cpu_stable_sort_pairs(keys, vals, 1)
+        what = "std::sort of (key, index) words = stable pair sort"
+    else:
+        oracle.cpu_sort(keys, 1)
+        what = "std::sort"
+    dt = time.perf_counter() - t
+    return {"value": round(n_sample / dt / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
+            "sample": f"{n_sample} keys of the same splitmix64 uniform workload, {what}, "
+                      f"1 thread, {dt:.2f} s (oracle/cpu_sort.cpp)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and not (world == 1 and a.gpus == 1):
+        if world == 1:
+            raise SystemExit("--gpus N > 1 must be launched with torchrun (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import gpuradixsort_amd as grs
+
+    cid, n_local, kb, pairs, rb, desc = CONFIGS[a.config]
+    if a.n:
+        n_local = a.n
+    seed = (0x6A09E667F3BCC908 + cid) & ((1 << 64) - 1)
+    kdt = torch.uint32 if kb == 32 else torch.uint64
+    step_bytes = n_local * (kb // 8 + (4 if pairs else 0))
+    pool = max(1, min(a.warmup + a.steps, int(a.pool_gib * 2**30 // step_bytes)))
+
+    # distinct unsorted inputs, one per step (step s uses global indices offset by s * N_total)
+    n_total = n_local * world
+    keys_pool, vals_pool = [], []
+    for i in range(pool):
+        k = torch.empty(n_local, dtype=kdt, device=dev)
+        grs.fill_splitmix(k, seed, first_index=i * n_total + rank * n_local)
+        keys_pool.append(k)
+        if pairs:
+            v = torch.empty(n_local, dtype=torch.uint32, device=dev)
+            grs.iota_u32(v, rank * n_local)
+            vals_pool.append(v)
+
+    if world == 1:
+        sorter = grs.RadixSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb)
+        sorter.set_profiling(max(1, a.steps))
+
+        def step(i):
+            k = keys_pool[i % pool]
+            if i >= pool:   # pool exhausted: regenerate inside the step (counted, honest)
+                grs.fill_splitmix(k, seed, first_index=i * n_total)
+            sorter.sort(k, vals_pool[i % pool] if pairs else None)
+    else:
+        from gpuradixsort_amd.sharded import ShardedSorter
+
+        sorter = ShardedSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb)
+        sorter.set_profiling(max(1, a.steps))
+
+        def step(i):
+            k = keys_pool[i % pool]
+            if i >= pool:
+                grs.fill_splitmix(k, seed, first_index=i * n_total + rank * n_local)
+            sorter.sort(k, vals_pool[i % pool] if pairs else None)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    for i in range(a.warmup):
+        step(i)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(a.warmup, a.warmup + a.steps):
+        step(i)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of the last timed step (cheap property: sortedness on device)
+    last = (a.warmup + a.steps - 1) % pool
+    inversions = sorter.count_inversions(keys_pool[last]) if world > 1 else \
+        grs.count_inversions(keys_pool[last])
+
+    # per-phase GPU times over the timed steps (hipEvents on the sort's stream)
+    tims = [sorter.timing(k) for k in range(min(a.steps, pool))]
+    pass_ms = [p for t in tims for p in t["pass_ms"]]
+    mean_pass_ms = sum(pass_ms) / len(pass_ms)
+    hist_ms = sum(t["hist_ms"] for t in tims) / len(tims)
+    sort_ms = sum(t["total_ms"] for t in tims) / len(tims)
+    n_sorted_local = sorter.last_local_n if world > 1 else n_local
+    alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
+    achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(min(a.cpu_sample, n_local), kb, pairs, seed)
+
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        rec = json.load(open(pmc_path)).get(f"{a.config}:{n_sorted_local}")
+        if rec:
+            traffic = rec.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        value = n_total * a.steps / elapsed / 1e9
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Gkeys/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32" if kb == 32 else "u64",
+            "data": "synthetic: splitmix64(seed ^ global_index) uniform keys, a distinct unsorted "
+                    "buffer per step resident in HBM" + ("; payload = global index" if pairs else ""),
+            "config": {"workload": desc, "keys_per_gpu": n_local, "total_keys": n_total,
+                       "key_bits": kb, "payload": "u32" if pairs else None, "radix_bits": rb,
+                       "passes": tims[0]["passes"], "parallelism": f"range-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic, "kernel": "grs_onesweep_pass",
+                         "kernel_mean_ms": round(mean_pass_ms, 5),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
+                          "sort_total_gpu": round(sort_ms, 5)},
+            "check": {"inversions_last_step": inversions},
+        }
+        if world > 1:
+            out["phases_ms"].update(sorter.phase_summary())
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,17 @@
+"""gpuradixsort_amd — MI355X-native (gfx950) stable LSD radix sort behind the reference's
+ParallelSort controller surface (amdreallyfast/GpuRadixSort).
+
+  RadixSorter          the C-ABI sorter (include/grs.h) over torch device tensors
+  OriginalDataSsbo,
+  ParallelSort         the reference's names and call pattern (ParallelSort.h:46-48)
+  RecordSort           sort whole records by a key (K1 key hook + pair sort + K5 gather)
+  sharded_sort         multi-GPU key-range sort: one RCCL all-to-all-v over xGMI
+
+All compute runs in libgrs.so's HIP kernels; there is no CPU fallback.
+"""
+from ._lib import GRS_MAX_N, GrsError, lib
+from .parallel_sort import OriginalDataSsbo, ParallelSort, RecordSort
+from .sorter import RadixSorter, count_inversions, fill_splitmix, gather_records, iota_u32
+
+__all__ = ["GRS_MAX_N", "GrsError", "lib", "OriginalDataSsbo", "ParallelSort", "RecordSort",
+           "RadixSorter", "count_inversions", "fill_splitmix", "gather_records", "iota_u32"]

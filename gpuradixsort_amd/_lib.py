@@ -1,0 +1,86 @@
+"""ctypes binding of libgrs.so (the C-ABI declared in include/grs.h).
+
+The library is built in-tree (`make -C gpuradixsort_amd/csrc`, or `__graft_entry__.build()`)
+and is the ONLY compute path of this package: there is no CPU fallback.  If the shared
+object is missing, `lib()` raises; on a machine without a GPU the library still loads (so the
+exported-symbol checks run on CPU) and every compute call returns GRS_ENODEV.
+
+torch is imported before the library is loaded on purpose: torch ships its own
+libamdhip64.so.7, and loading it first makes libgrs bind to that same HIP runtime (same
+soname), so device pointers and streams from torch are valid inside libgrs.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint64, c_void_p
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libgrs.so")
+
+GRS_OK, GRS_EINVAL, GRS_ENOMEM, GRS_EHIP, GRS_ECAPACITY, GRS_ENODEV, GRS_ETIMEOUT = range(7)
+GRS_KEY_U32, GRS_KEY_U64 = 0, 1
+GRS_MAX_N = (1 << 30) - 1
+
+
+class GrsError(RuntimeError):
+    def __init__(self, status: int, what: str, detail: str = ""):
+        self.status = status
+        names = ["GRS_OK", "GRS_EINVAL", "GRS_ENOMEM", "GRS_EHIP", "GRS_ECAPACITY", "GRS_ENODEV",
+                 "GRS_ETIMEOUT"]
+        name = names[status] if 0 <= status < len(names) else str(status)
+        super().__init__(f"{what}: {name}" + (f" ({detail})" if detail else ""))
+
+
+class grs_timing(ctypes.Structure):
+    _fields_ = [("passes", c_int), ("total_ms", c_float), ("hist_ms", c_float),
+                ("pass_ms", c_float * 16), ("copy_ms", c_float)]
+
+
+# (name, restype, argtypes) of every symbol include/grs.h declares
+SIGNATURES = [
+    ("grs_version", c_int, []),
+    ("grs_status_string", c_char_p, [c_int]),
+    ("grs_last_error", c_char_p, []),
+    ("grs_create", c_int, [POINTER(c_void_p), c_size_t, c_int, c_int, c_int, c_int]),
+    ("grs_destroy", None, [c_void_p]),
+    ("grs_scratch_bytes", c_size_t, [c_void_p]),
+    ("grs_sort", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    ("grs_sort_bits", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
+    ("grs_set_profiling", c_int, [c_void_p, c_int]),
+    ("grs_last_timing", c_int, [c_void_p, POINTER(grs_timing)]),
+    ("grs_timing_history", c_int, [c_void_p, c_int, POINTER(grs_timing)]),
+    ("grs_check_error", c_int, [c_void_p]),
+    ("grs_iota_u32", c_int, [c_void_p, c_size_t, c_uint32, c_void_p]),
+    ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
+    ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),
+    ("grs_count_inversions", c_int, [c_void_p, c_size_t, c_int, POINTER(c_uint64), c_void_p]),
+]
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgrs.so once (after torch, see module doc) and declare its signatures."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (binds libgrs to torch's HIP runtime; see module doc)
+
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C gpuradixsort_amd/csrc` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(status: int, what: str) -> None:
+    if status != GRS_OK:
+        detail = lib().grs_last_error()
+        raise GrsError(status, what, detail.decode() if detail else "")

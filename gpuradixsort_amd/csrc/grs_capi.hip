@@ -1,0 +1,419 @@
+// grs_capi.hip — C-ABI of libgrs (include/grs.h): sorter lifecycle, pass driver, helpers.
+//
+// The pass driver replaces ParallelSort::Sort (Source/ComputeControllers/ParallelSort.cpp:168-298):
+// where the reference issues 1 + 32 x 4 GLSL dispatches with a glMemoryBarrier after each,
+// one grs_sort call issues
+//     hipMemsetAsync(control block)  -> grs_upfront_hist  -> P x grs_onesweep_pass
+// on one stream (P = ceil((end_bit - begin_bit) / radix_bits); 4 launches for u32 at 8-bit
+// digits), plus one D2D copy when P is odd so the result lands back in the caller's buffer
+// (the reference's glCopyBufferSubData, ParallelSort.cpp:312-318).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/grs.h"
+#include "grs_config.h"
+#include "grs_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+grs_status set_err(grs_status s, const std::string& msg) {
+  g_last_error = msg;
+  return s;
+}
+
+#define GRS_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return set_err(GRS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+// Tile geometry per (key type, payload, radix).  ITEMS keys per thread, GRS_BLOCK threads.
+template <typename K, bool PAIRS, int RB>
+struct TileCfg {
+  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 12 : 16) : (PAIRS ? 16 : 16);
+  static constexpr int TILE = GRS_BLOCK * ITEMS;
+};
+
+constexpr int max_tile_min() { return GRS_BLOCK * 12; }  // smallest TILE over configs
+
+}  // namespace
+
+struct grs_sorter {
+  int device = 0;
+  grs_key_type key_type = GRS_KEY_U32;
+  int pairs = 0;
+  int radix_bits = 8;
+  size_t capacity = 0;
+  void* alt_keys = nullptr;
+  uint32_t* alt_vals = nullptr;
+  uint32_t* status = nullptr;      // 2 x status_words
+  size_t status_words = 0;         // per buffer
+  uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
+  size_t scratch_bytes = 0;
+  // Profiling ring: the last `ring` calls keep their per-phase hipEvents.
+  static constexpr int EV_PER_CALL = GRS_MAX_PASSES + 3;
+  int ring = 0;
+  long long calls = 0;             // profiled calls recorded so far
+  hipEvent_t* ev = nullptr;        // ring * EV_PER_CALL events
+  struct CallInfo { int ev_used; int passes; bool copy; };
+  CallInfo* info = nullptr;        // ring entries
+};
+
+extern "C" {
+
+int grs_version(void) { return GRS_VERSION; }
+
+const char* grs_status_string(grs_status s) {
+  switch (s) {
+    case GRS_OK: return "GRS_OK";
+    case GRS_EINVAL: return "GRS_EINVAL";
+    case GRS_ENOMEM: return "GRS_ENOMEM";
+    case GRS_EHIP: return "GRS_EHIP";
+    case GRS_ECAPACITY: return "GRS_ECAPACITY";
+    case GRS_ENODEV: return "GRS_ENODEV";
+    case GRS_ETIMEOUT: return "GRS_ETIMEOUT";
+  }
+  return "GRS_UNKNOWN";
+}
+
+const char* grs_last_error(void) { return g_last_error.c_str(); }
+
+void grs_destroy(grs_sorter* s) {
+  if (!s) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(s->device);
+  if (s->alt_keys) (void)hipFree(s->alt_keys);
+  if (s->alt_vals) (void)hipFree(s->alt_vals);
+  if (s->status) (void)hipFree(s->status);
+  if (s->ctrl) (void)hipFree(s->ctrl);
+  for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
+    if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
+  delete[] s->ev;
+  delete[] s->info;
+  (void)hipSetDevice(prev);
+  delete s;
+}
+
+grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
+                      int with_u32_payload, int radix_bits, int device) {
+  if (!out) return set_err(GRS_EINVAL, "grs_create: out is NULL");
+  *out = nullptr;
+  if (key_type != GRS_KEY_U32 && key_type != GRS_KEY_U64)
+    return set_err(GRS_EINVAL, "grs_create: bad key type");
+  if (radix_bits == 0) radix_bits = 8;
+  if (radix_bits != 4 && radix_bits != 8)
+    return set_err(GRS_EINVAL, "grs_create: radix_bits must be 4, 8 or 0");
+  if (capacity > GRS_MAX_N)
+    return set_err(GRS_ECAPACITY, "grs_create: capacity exceeds 2^30-1 items per device call");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_err(GRS_ENODEV, "grs_create: no HIP device");
+  if (device < 0 || device >= ndev) return set_err(GRS_ENODEV, "grs_create: bad device ordinal");
+
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  GRS_HIP(hipSetDevice(device));
+  grs_sorter* s = new grs_sorter();
+  s->device = device;
+  s->key_type = key_type;
+  s->pairs = with_u32_payload ? 1 : 0;
+  s->radix_bits = radix_bits;
+  s->capacity = capacity;
+  const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
+  const size_t cap = std::max<size_t>(capacity, 1);
+  const size_t tiles = (cap + max_tile_min() - 1) / max_tile_min();
+  s->status_words = tiles * (size_t(1) << radix_bits);
+  grs_status st = GRS_OK;
+  auto alloc = [&](void** p, size_t bytes) {
+    if (st != GRS_OK) return;
+    if (hipMalloc(p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      st = set_err(GRS_ENOMEM, "grs_create: hipMalloc of " + std::to_string(bytes) + " bytes failed");
+      return;
+    }
+    s->scratch_bytes += bytes;
+  };
+  alloc(&s->alt_keys, cap * kb);
+  if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
+  alloc(reinterpret_cast<void**>(&s->status), 2 * s->status_words * 4);
+  alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
+  if (st == GRS_OK && hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess)
+    st = set_err(GRS_EHIP, "grs_create: hipMemset failed");
+  (void)hipSetDevice(prev);
+  if (st != GRS_OK) {
+    grs_destroy(s);
+    return st;
+  }
+  *out = s;
+  return GRS_OK;
+}
+
+size_t grs_scratch_bytes(const grs_sorter* s) { return s ? s->scratch_bytes : 0; }
+
+grs_status grs_set_profiling(grs_sorter* s, int ring) {
+  if (!s) return set_err(GRS_EINVAL, "grs_set_profiling: NULL sorter");
+  if (ring < 0 || ring > 4096) return set_err(GRS_EINVAL, "grs_set_profiling: ring out of range");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  GRS_HIP(hipSetDevice(s->device));
+  for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
+    if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
+  delete[] s->ev;
+  delete[] s->info;
+  s->ev = nullptr;
+  s->info = nullptr;
+  s->ring = 0;
+  s->calls = 0;
+  grs_status st = GRS_OK;
+  if (ring > 0) {
+    s->ev = new hipEvent_t[ring * grs_sorter::EV_PER_CALL]();
+    s->info = new grs_sorter::CallInfo[ring]();
+    s->ring = ring;
+    for (int i = 0; i < ring * grs_sorter::EV_PER_CALL && st == GRS_OK; ++i)
+      if (hipEventCreate(&s->ev[i]) != hipSuccess)
+        st = set_err(GRS_EHIP, "grs_set_profiling: hipEventCreate failed");
+  }
+  (void)hipSetDevice(prev);
+  return st;
+}
+
+}  // extern "C"
+
+namespace {
+
+template <typename K, bool PAIRS, int RB>
+grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begin_bit,
+                    int end_bit, hipStream_t stream) {
+  using Cfg = TileCfg<K, PAIRS, RB>;
+  constexpr int RADIX = 1 << RB;
+  const int passes = (end_bit - begin_bit + RB - 1) / RB;
+  const uint32_t tiles = (n + Cfg::TILE - 1) / Cfg::TILE;
+  const size_t words = static_cast<size_t>(tiles) * RADIX;
+  if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
+  uint32_t* st0 = s->status;
+  uint32_t* st1 = s->status + s->status_words;
+  uint32_t* hist = s->ctrl;
+  uint32_t* tickets = s->ctrl + GRS_CTRL_TICKETS;
+  uint32_t* err = s->ctrl + GRS_CTRL_ERROR;
+  int ev = 0;
+  hipEvent_t* evs = s->ring ? s->ev + (s->calls % s->ring) * grs_sorter::EV_PER_CALL : nullptr;
+  auto mark = [&]() -> grs_status {
+    if (evs) GRS_HIP(hipEventRecord(evs[ev++], stream));
+    return GRS_OK;
+  };
+
+  grs_status r;
+  if ((r = mark()) != GRS_OK) return r;
+  // zero histograms + tickets (the error word is sticky: only grs_check_error clears it)
+  GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
+  {
+    const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
+    hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
+                       stream, keys, n, begin_bit, end_bit, passes, hist, st0,
+                       static_cast<uint32_t>(words));
+    GRS_HIP(hipGetLastError());
+  }
+  if ((r = mark()) != GRS_OK) return r;
+
+  K* src = keys;
+  K* dst = static_cast<K*>(s->alt_keys);
+  uint32_t* vsrc = vals;
+  uint32_t* vdst = s->alt_vals;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = begin_bit + p * RB;
+    const int bits = std::min(RB, end_bit - shift);
+    uint32_t* st_cur = (p & 1) ? st1 : st0;
+    uint32_t* st_nxt = (p & 1) ? st0 : st1;
+    hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::ITEMS>), dim3(tiles),
+                       dim3(GRS_BLOCK), 0, stream, src, dst, vsrc, vdst, n, shift, bits,
+                       hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+    GRS_HIP(hipGetLastError());
+    if ((r = mark()) != GRS_OK) return r;
+    std::swap(src, dst);
+    std::swap(vsrc, vdst);
+  }
+  const bool copy = (passes & 1) != 0;
+  if (copy) {  // result sits in scratch: copy back (ParallelSort.cpp:312-318)
+    GRS_HIP(hipMemcpyAsync(keys, src, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToDevice,
+                           stream));
+    if (PAIRS)
+      GRS_HIP(hipMemcpyAsync(vals, vsrc, static_cast<size_t>(n) * 4, hipMemcpyDeviceToDevice,
+                             stream));
+    if ((r = mark()) != GRS_OK) return r;
+  }
+  if (evs) {
+    s->info[s->calls % s->ring] = {ev, passes, copy};
+    ++s->calls;
+  }
+  return GRS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, int begin_bit,
+                         int end_bit, void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_sort: NULL sorter");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort: n exceeds sorter capacity");
+  const int kbits = s->key_type == GRS_KEY_U64 ? 64 : 32;
+  if (begin_bit < 0 || end_bit > kbits || begin_bit >= end_bit)
+    return set_err(GRS_EINVAL, "grs_sort: bad bit range");
+  if (n == 0) return GRS_OK;  // the reference's N = 0 "won't crash" (PrefixSumSsbo.cpp:121-124)
+  if (!d_keys) return set_err(GRS_EINVAL, "grs_sort: d_keys is NULL");
+  if (s->pairs && !d_vals) return set_err(GRS_EINVAL, "grs_sort: payload sorter needs d_vals");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint32_t n32 = static_cast<uint32_t>(n);
+  grs_status r = GRS_EINVAL;
+  const bool u64 = s->key_type == GRS_KEY_U64;
+  if (!u64 && !s->pairs && s->radix_bits == 8)
+    r = run_sort<uint32_t, false, 8>(s, (uint32_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
+  else if (!u64 && !s->pairs && s->radix_bits == 4)
+    r = run_sort<uint32_t, false, 4>(s, (uint32_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
+  else if (!u64 && s->pairs && s->radix_bits == 8)
+    r = run_sort<uint32_t, true, 8>(s, (uint32_t*)d_keys, d_vals, n32, begin_bit, end_bit, st);
+  else if (!u64 && s->pairs && s->radix_bits == 4)
+    r = run_sort<uint32_t, true, 4>(s, (uint32_t*)d_keys, d_vals, n32, begin_bit, end_bit, st);
+  else if (u64 && !s->pairs && s->radix_bits == 8)
+    r = run_sort<uint64_t, false, 8>(s, (uint64_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
+  else if (u64 && !s->pairs && s->radix_bits == 4)
+    r = run_sort<uint64_t, false, 4>(s, (uint64_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
+  else if (u64 && s->pairs && s->radix_bits == 8)
+    r = run_sort<uint64_t, true, 8>(s, (uint64_t*)d_keys, d_vals, n32, begin_bit, end_bit, st);
+  else if (u64 && s->pairs && s->radix_bits == 4)
+    r = run_sort<uint64_t, true, 4>(s, (uint64_t*)d_keys, d_vals, n32, begin_bit, end_bit, st);
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_sort(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_sort: NULL sorter");
+  return grs_sort_bits(s, d_keys, d_vals, n, 0, s->key_type == GRS_KEY_U64 ? 64 : 32, stream);
+}
+
+grs_status grs_timing_history(grs_sorter* s, int k, grs_timing* out) {
+  if (!s || !out) return set_err(GRS_EINVAL, "grs_timing_history: NULL argument");
+  std::memset(out, 0, sizeof(*out));
+  if (s->ring == 0 || k < 0 || k >= s->ring || k >= s->calls)
+    return set_err(GRS_EINVAL, "grs_timing_history: no such profiled call");
+  const long long slot = (s->calls - 1 - k) % s->ring;
+  const grs_sorter::CallInfo ci = s->info[slot];
+  hipEvent_t* e = s->ev + slot * grs_sorter::EV_PER_CALL;
+  GRS_HIP(hipEventSynchronize(e[ci.ev_used - 1]));
+  out->passes = ci.passes;
+  float ms = 0;
+  GRS_HIP(hipEventElapsedTime(&ms, e[0], e[1]));
+  out->hist_ms = ms;
+  for (int p = 0; p < ci.passes && p < 16; ++p) {
+    GRS_HIP(hipEventElapsedTime(&ms, e[1 + p], e[2 + p]));
+    out->pass_ms[p] = ms;
+  }
+  if (ci.copy) {
+    GRS_HIP(hipEventElapsedTime(&ms, e[1 + ci.passes], e[2 + ci.passes]));
+    out->copy_ms = ms;
+  }
+  GRS_HIP(hipEventElapsedTime(&ms, e[0], e[ci.ev_used - 1]));
+  out->total_ms = ms;
+  return GRS_OK;
+}
+
+grs_status grs_last_timing(grs_sorter* s, grs_timing* out) { return grs_timing_history(s, 0, out); }
+
+grs_status grs_check_error(grs_sorter* s) {
+  if (!s) return set_err(GRS_EINVAL, "grs_check_error: NULL sorter");
+  uint32_t e = 0;
+  GRS_HIP(hipDeviceSynchronize());
+  GRS_HIP(hipMemcpy(&e, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost));
+  if (e) {
+    GRS_HIP(hipMemset(s->ctrl + GRS_CTRL_ERROR, 0, 4));
+    return set_err(GRS_ETIMEOUT, "a look-back spin exceeded its bound");
+  }
+  return GRS_OK;
+}
+
+static int grid_for(size_t n, int block) {
+  const size_t g = (n + block - 1) / block;
+  return static_cast<int>(std::max<size_t>(1, std::min<size_t>(g, 8192)));
+}
+
+grs_status grs_iota_u32(uint32_t* d_out, size_t n, uint32_t start, void* stream) {
+  if (n == 0) return GRS_OK;
+  if (!d_out) return set_err(GRS_EINVAL, "grs_iota_u32: NULL");
+  hipLaunchKernelGGL(grs::grs_iota_u32, dim3(grid_for(n, 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_out, static_cast<uint64_t>(n), start);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
+grs_status grs_gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
+                              size_t record_bytes, void* stream) {
+  if (n == 0) return GRS_OK;
+  if (!d_src || !d_dst || !d_idx || record_bytes == 0 || record_bytes > 0xFFFFFFFFull)
+    return set_err(GRS_EINVAL, "grs_gather_records: bad argument");
+  hipLaunchKernelGGL(grs::grs_gather_records, dim3(grid_for(n * ((record_bytes + 3) / 4), 256)),
+                     dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), d_idx,
+                     static_cast<uint64_t>(n), static_cast<uint32_t>(record_bytes));
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
+grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t seed,
+                             uint64_t first_index, void* stream) {
+  if (n == 0) return GRS_OK;
+  if (!d_keys || (key_bytes != 4 && key_bytes != 8))
+    return set_err(GRS_EINVAL, "grs_fill_splitmix: bad argument");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (key_bytes == 4)
+    hipLaunchKernelGGL(grs::grs_fill_splitmix<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<uint32_t*>(d_keys), static_cast<uint64_t>(n), seed, first_index);
+  else
+    hipLaunchKernelGGL(grs::grs_fill_splitmix<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<uint64_t*>(d_keys), static_cast<uint64_t>(n), seed, first_index);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
+grs_status grs_count_inversions(const void* d_keys, size_t n, int key_bytes, uint64_t* out_count,
+                                void* stream) {
+  if (!out_count || (key_bytes != 4 && key_bytes != 8))
+    return set_err(GRS_EINVAL, "grs_count_inversions: bad argument");
+  *out_count = 0;
+  if (n < 2) return GRS_OK;
+  if (!d_keys) return set_err(GRS_EINVAL, "grs_count_inversions: NULL keys");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  unsigned long long* d_cnt = nullptr;
+  GRS_HIP(hipMalloc(&d_cnt, sizeof(*d_cnt)));
+  grs_status r = GRS_OK;
+  if (hipMemsetAsync(d_cnt, 0, sizeof(*d_cnt), st) != hipSuccess) r = GRS_EHIP;
+  if (r == GRS_OK) {
+    if (key_bytes == 4)
+      hipLaunchKernelGGL(grs::grs_count_inversions<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0,
+                         st, static_cast<const uint32_t*>(d_keys), static_cast<uint64_t>(n), d_cnt);
+    else
+      hipLaunchKernelGGL(grs::grs_count_inversions<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0,
+                         st, static_cast<const uint64_t*>(d_keys), static_cast<uint64_t>(n), d_cnt);
+    if (hipGetLastError() != hipSuccess) r = GRS_EHIP;
+  }
+  unsigned long long h = 0;
+  if (r == GRS_OK && hipMemcpyAsync(&h, d_cnt, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess)
+    r = GRS_EHIP;
+  if (r == GRS_OK && hipStreamSynchronize(st) != hipSuccess) r = GRS_EHIP;
+  (void)hipFree(d_cnt);
+  if (r != GRS_OK) return set_err(r, "grs_count_inversions: HIP failure");
+  *out_count = h;
+  return GRS_OK;
+}
+
+}  // extern "C"

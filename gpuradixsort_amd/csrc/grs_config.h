@@ -1,0 +1,40 @@
+// grs_config.h — compile-time constants shared by host and device code.
+//
+// Replaces the reference's shared GLSL/C++ constant headers
+// (Shaders/ParallelSort/ParallelSortConstants.comp:17-24,
+//  Shaders/ComputeHeaders/SsboBufferBindings.comp:19-22,
+//  Shaders/ComputeHeaders/UniformLocations.comp:24-38), which #define one 512-thread
+// work group and 1024 items per scan group for a 32 x 1-bit LSD sort.  Here the digit
+// width is a template parameter (4 or 8 bits) and one onesweep tile holds
+// GRS_BLOCK x ITEMS keys; buffer bindings and uniform locations have no equivalent
+// (kernel arguments carry the pointers).
+#pragma once
+
+#include <stdint.h>
+
+#define GRS_WAVE 64                 // CDNA wavefront width (never 32)
+#define GRS_BLOCK 256               // threads per onesweep / histogram workgroup (4 waves)
+#define GRS_HIST_BLOCK 256
+
+// Decoupled look-back status word: [31:30] flag, [29:0] digit count.
+#define GRS_FLAG_SHIFT 30u
+#define GRS_FLAG_NOT_READY 0u
+#define GRS_FLAG_AGGREGATE 1u
+#define GRS_FLAG_INCLUSIVE 2u
+#define GRS_VALUE_MASK 0x3FFFFFFFu
+// Largest element count one device sort call accepts: a tile's inclusive digit
+// prefix must fit the 30-bit value field of a status word.
+#define GRS_MAX_N ((uint64_t)GRS_VALUE_MASK)
+
+// Bounded spins (look-back): give up after this many polls and raise the error word.
+#define GRS_SPIN_LIMIT (1u << 22)
+
+// Layout of the per-sorter control block (uint32 words), zeroed once per sort call.
+//   [0, GRS_CTRL_HIST_WORDS)           global digit histograms, [pass][radix]
+//   GRS_CTRL_TICKETS + pass            per-pass tile ticket counters
+//   GRS_CTRL_ERROR                     nonzero = a bounded spin timed out
+#define GRS_MAX_PASSES 16               // u64 keys at 4-bit digits
+#define GRS_CTRL_HIST_WORDS 4096        // >= max over configs of passes * radix (8*256, 16*16)
+#define GRS_CTRL_TICKETS GRS_CTRL_HIST_WORDS
+#define GRS_CTRL_ERROR (GRS_CTRL_TICKETS + GRS_MAX_PASSES)
+#define GRS_CTRL_WORDS (GRS_CTRL_ERROR + 16)   // multiple of 4 words (16-B memset)

@@ -1,0 +1,366 @@
+// grs_kernels.hpp — hand-written gfx950 (CDNA4) kernels of the LSD radix sort.
+//
+// The reference sorts with 32 one-bit passes, each pass being four GLSL dispatches
+// (Shaders/ParallelSort/GetBitForPrefixScan.comp:25-68, ParallelPrefixScan.comp:41-196,
+// SortIntermediateData.comp:32-67; driven by Source/ComputeControllers/ParallelSort.cpp:236-298).
+// That is 130 dispatches and ~40 B of HBM traffic per key per bit.  This file re-derives the
+// same stable LSD sort for MI355X as:
+//
+//   grs_upfront_hist   one read of the keys; LDS-privatised digit histograms of EVERY pass
+//                      (replaces K2 + K3a + K3b's role of counting digits).
+//   grs_onesweep_pass  one launch per RADIX_BITS-wide digit: load a tile, rank every key
+//                      stably inside the tile with wave64 ballot match masks (__ballot +
+//                      v_mbcnt), publish the tile's digit counts, resolve the tile's global
+//                      offsets with a decoupled look-back over ordered tile tickets, then
+//                      reorder the tile in LDS and scatter it (replaces K4's stable split).
+//
+// Stability (equal keys keep input order) is what makes the multi-bit LSD produce exactly
+// the reference's order: each reference pass is a stable 1-bit split
+// (SortIntermediateData.comp:58-66), so the composite result is the stable sort by key.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "grs_config.h"
+
+namespace grs {
+
+// ----------------------------------------------------------------------------------------
+// small device helpers
+// ----------------------------------------------------------------------------------------
+
+template <typename K>
+__device__ __forceinline__ uint32_t digit_of(K key, int shift, uint32_t mask) {
+  return static_cast<uint32_t>(key >> shift) & mask;
+}
+
+// Number of set bits of `m` in lanes strictly below this lane.
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return mbcnt64(~0ull); }
+
+// Mask of the lanes of this wave whose digit equals this lane's digit (all 64 lanes active).
+template <int RB>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d) {
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = __ballot(bit);
+    m &= bit ? bb : ~bb;
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t ld_status(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Inclusive scan of one 64-bit value per lane across a wave.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < GRS_WAVE; o <<= 1) {
+    const uint64_t n = __shfl_up(v, o, GRS_WAVE);
+    if (lane >= static_cast<uint32_t>(o)) v += n;
+  }
+  return v;
+}
+
+// ----------------------------------------------------------------------------------------
+// upfront histogram: counts of every digit of every pass in one read of the keys
+// ----------------------------------------------------------------------------------------
+//
+// keys:       n keys (the unsorted input)
+// g_hist:     [passes][RADIX] uint32 counters, zeroed by the caller (control-block memset)
+// clear/cw:   status buffer of pass 0, zeroed here (grid-stride) so no separate memset
+//             launch is needed.
+template <typename K, int RB>
+__global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
+    const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
+    uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words) {
+  constexpr int RADIX = 1 << RB;
+  constexpr int MAXP = (8 * sizeof(K) + RB - 1) / RB;
+  // Two sub-histograms (even/odd waves) halve LDS atomic contention on skewed inputs.
+  __shared__ uint32_t s_hist[2][MAXP * RADIX];
+
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < 2 * MAXP * RADIX; i += GRS_HIST_BLOCK) (&s_hist[0][0])[i] = 0;
+  // zero the first pass's look-back status words
+  for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < clear_words; i += gridDim.x * GRS_HIST_BLOCK)
+    clear[i] = 0;
+  __syncthreads();
+
+  uint32_t* h = s_hist[(t >> 6) & 1];
+  int shifts[MAXP];
+  uint32_t masks[MAXP];
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int s = begin_bit + p * RB;
+    shifts[p] = s;
+    const int bits = (end_bit - s) < RB ? (end_bit - s) : RB;
+    masks[p] = (p < passes && bits > 0) ? ((1u << bits) - 1u) : 0u;
+  }
+
+  constexpr int VEC = 16 / sizeof(K);  // keys per 16-byte load
+  using V = uint4;
+  // 16-B vector loads need a 16-B aligned base; otherwise everything takes the scalar tail
+  const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : n / VEC;
+  const V* kv = reinterpret_cast<const V*>(keys);
+  for (uint32_t v = blockIdx.x * GRS_HIST_BLOCK + t; v < nvec; v += gridDim.x * GRS_HIST_BLOCK) {
+    const V x = kv[v];
+    const K* kk = reinterpret_cast<const K*>(&x);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+#pragma unroll
+      for (int p = 0; p < MAXP; ++p)
+        if (p < passes) atomicAdd(&h[p * RADIX + digit_of(kk[e], shifts[p], masks[p])], 1u);
+    }
+  }
+  // ragged tail (fewer than VEC keys)
+  for (uint32_t i = nvec * VEC + blockIdx.x * GRS_HIST_BLOCK + t; i < n;
+       i += gridDim.x * GRS_HIST_BLOCK) {
+    const K k = keys[i];
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p)
+      if (p < passes) atomicAdd(&h[p * RADIX + digit_of(k, shifts[p], masks[p])], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < static_cast<uint32_t>(passes * RADIX); i += GRS_HIST_BLOCK) {
+    const uint32_t c = s_hist[0][i] + s_hist[1][i];
+    if (c) atomicAdd(&g_hist[i], c);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// one LSD pass: rank + look-back + scatter of one RB-bit digit
+// ----------------------------------------------------------------------------------------
+//
+// Tile layout: tile T covers keys [T*TILE, (T+1)*TILE); wave w of the tile owns the
+// contiguous sub-range [w*64*ITEMS, (w+1)*64*ITEMS) and loads it "wave-striped": item j of
+// lane l is key (w*64*ITEMS + j*64 + l).  Every global load instruction is 64 consecutive
+// keys (256 B for u32) and ranking items j = 0..ITEMS-1 in order, lanes in order, visits
+// keys in input order, which is what makes the rank stable.
+//
+// status:      [num_tiles][RADIX] look-back words of this pass (zeroed before the launch)
+// status_next: the other status buffer: this tile zeroes its own slice for the next pass
+// tickets:     per-pass atomic counter; ticket order = tile order, so a tile only ever
+//              waits on tiles that already started (no forward-progress assumption)
+template <typename K, bool PAIRS, int RB, int ITEMS>
+__global__ __launch_bounds__(GRS_BLOCK) void grs_onesweep_pass(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, int shift, int bits,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  constexpr int RADIX = 1 << RB;
+  constexpr int WAVES = GRS_BLOCK / GRS_WAVE;
+  constexpr int TILE = GRS_BLOCK * ITEMS;
+  constexpr int WAVE_TILE = GRS_WAVE * ITEMS;
+  static_assert(RADIX <= GRS_BLOCK, "one look-back thread per digit");
+
+  __shared__ uint32_t s_cnt[WAVES * RADIX];  // per-wave digit counters -> local offsets
+  __shared__ uint32_t s_base[RADIX];         // global dst of tile-local index 0 of digit d
+  __shared__ uint64_t s_wsum[WAVES];         // block-scan carries
+  __shared__ uint32_t s_tile;
+  __shared__ K s_keys[TILE];
+  __shared__ uint32_t s_vals[PAIRS ? TILE : 1];
+
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = (1u << bits) - 1u;
+
+  if (t == 0) s_tile = atomicAdd(ticket, 1u);
+  // zero this wave's digit counters
+  for (uint32_t i = lane; i < RADIX; i += GRS_WAVE) s_cnt[w * RADIX + i] = 0;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  if (t < RADIX) status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
+
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t wbase = tile_base + w * WAVE_TILE;
+
+  // ---- load (wave-striped, coalesced) ----
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  if (valid == TILE) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) key[j] = keys_in[wbase + j * GRS_WAVE + lane];
+    if constexpr (PAIRS) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) val[j] = vals_in[wbase + j * GRS_WAVE + lane];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = wbase + j * GRS_WAVE + lane;
+      // padding sorts after every valid key of its digit: all-ones digit, highest index
+      key[j] = i < n ? keys_in[i] : static_cast<K>(~static_cast<K>(0));
+      if constexpr (PAIRS) val[j] = i < n ? vals_in[i] : 0u;
+    }
+  }
+
+  // ---- stable rank inside the wave: ballot match masks, per-wave LDS counters ----
+  uint32_t rank[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = digit_of(key[j], shift, dmask);
+    const uint64_t m = match_digit<RB>(d);
+    const uint32_t below = mbcnt64(m);
+    const uint32_t old = s_cnt[w * RADIX + d];
+    if (below == 0) s_cnt[w * RADIX + d] = old + static_cast<uint32_t>(__popcll(m));
+    rank[j] = old + below;
+  }
+  __syncthreads();
+
+  // ---- per digit: exclusive over waves, tile count, block scans, look-back ----
+  uint32_t tile_cnt = 0;
+  if (t < RADIX) {
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) {
+      const uint32_t c = s_cnt[ww * RADIX + t];
+      s_cnt[ww * RADIX + t] = tile_cnt;
+      tile_cnt += c;
+    }
+  }
+  // exclusive scans over digits of (pass histogram, tile count), packed in one u64:
+  // hi 32 bits -> global start of digit d, lo 32 bits -> tile-local start of digit d
+  uint64_t packed = 0;
+  if (t < RADIX) packed = (static_cast<uint64_t>(pass_hist[t]) << 32) | tile_cnt;
+  const uint64_t incl = wave_incl_scan(packed, lane);
+  if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
+  __syncthreads();
+  uint64_t carry = 0;
+  for (uint32_t ww = 0; ww < w; ++ww) carry += s_wsum[ww];
+  const uint64_t excl = carry + incl - packed;
+
+  if (t < RADIX) {
+    const uint32_t global_start = static_cast<uint32_t>(excl >> 32);
+    const uint32_t local_start = static_cast<uint32_t>(excl);
+    // padding keys (last tile only) are ranked but never published or stored
+    const uint32_t pad = TILE - valid;
+    const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
+    uint32_t* my = status + static_cast<size_t>(tile) * RADIX + t;
+    uint32_t prefix = 0;
+    if (tile == 0) {
+      st_status(my, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | publish);
+    } else {
+      st_status(my, (GRS_FLAG_AGGREGATE << GRS_FLAG_SHIFT) | publish);
+      int64_t pt = static_cast<int64_t>(tile) - 1;
+      uint32_t spins = 0;
+      while (true) {
+        const uint32_t v = ld_status(status + static_cast<size_t>(pt) * RADIX + t);
+        const uint32_t f = v >> GRS_FLAG_SHIFT;
+        if (f == GRS_FLAG_NOT_READY) {
+          if (++spins > GRS_SPIN_LIMIT) {
+            atomicOr(error_word, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += v & GRS_VALUE_MASK;
+        if (f == GRS_FLAG_INCLUSIVE) break;
+        --pt;
+      }
+      st_status(my, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
+    }
+    s_base[t] = global_start + prefix - local_start;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) s_cnt[ww * RADIX + t] += local_start;
+  }
+  __syncthreads();
+
+  // ---- reorder the tile in LDS by (digit, input order) ----
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = digit_of(key[j], shift, dmask);
+    const uint32_t pos = s_cnt[w * RADIX + d] + rank[j];
+    s_keys[pos] = key[j];
+    if constexpr (PAIRS) s_vals[pos] = val[j];
+  }
+  __syncthreads();
+
+  // ---- scatter: consecutive threads write consecutive slots of each digit run ----
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * GRS_BLOCK + t;
+    if (i < valid) {
+      const K kk = s_keys[i];
+      const uint32_t dst = s_base[digit_of(kk, shift, dmask)] + i;
+      keys_out[dst] = kk;
+      if constexpr (PAIRS) vals_out[dst] = s_vals[i];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// auxiliary kernels (boundary helpers; not on the timed hot path)
+// ----------------------------------------------------------------------------------------
+
+// splitmix64 (Steele, Lea, Flood 2014) — the synthetic key generator of SURVEY §8(d):
+// key[i] = splitmix64(seed ^ (first_index + i)), truncated to the key width.
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+template <typename K>
+__global__ void grs_fill_splitmix(K* __restrict__ out, uint64_t n, uint64_t seed, uint64_t first) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = static_cast<K>(splitmix64(seed ^ (first + i)));
+}
+
+__global__ void grs_iota_u32(uint32_t* __restrict__ out, uint64_t n, uint32_t start) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = start + static_cast<uint32_t>(i);
+}
+
+// K5 generalised (SortOriginalData.comp:27-51): dst[i] = src[idx[i]] for records of
+// `rb` bytes.  Records that are a multiple of 4 bytes move as dwords.
+__global__ void grs_gather_records(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                   const uint32_t* __restrict__ idx, uint64_t n, uint32_t rb) {
+  const uint64_t total = n * rb;
+  if ((rb & 3u) == 0) {
+    const uint32_t wpr = rb >> 2;
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n * wpr;
+         e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+      const uint64_t r = e / wpr, c = e - r * wpr;
+      d[e] = s[static_cast<uint64_t>(idx[r]) * wpr + c];
+    }
+  } else {
+    for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+      const uint64_t r = e / rb, c = e - r * rb;
+      dst[e] = src[static_cast<uint64_t>(idx[r]) * rb + c];
+    }
+  }
+}
+
+// Adjacent-order check of the reference (ParallelSort.cpp:336-352), strengthened: counts
+// every i with key[i] < key[i-1] (the reference skips 0xffffffff padding; we have none).
+template <typename K>
+__global__ void grs_count_inversions(const K* __restrict__ keys, uint64_t n,
+                                     unsigned long long* __restrict__ out) {
+  unsigned long long c = 0;
+  for (uint64_t i = 1 + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    c += keys[i] < keys[i - 1];
+  if (c) atomicAdd(out, c);
+}
+
+}  // namespace grs

@@ -1,0 +1,95 @@
+"""Python mirror of the reference's controller surface (same names, same argument meaning).
+
+Reference (amdreallyfast/GpuRadixSort):
+  OriginalDataSsbo(numItems)      Include/SSBOs/OriginalDataSsbo.h:16-20, Source/SSBOs/OriginalDataSsbo.cpp:20-33
+  ParallelSort(dataToSort)        Include/ComputeControllers/ParallelSort.h:46
+  ParallelSort.Sort()             Include/ComputeControllers/ParallelSort.h:48, ParallelSort.cpp:168-422
+
+The SSBO becomes a device tensor of uint32 `_value`s; Sort() sorts it in place with the
+HIP kernels of libgrs (no CPU path).  Errors raise GrsError instead of printing.
+RecordSort generalises the reference's IntermediateData design (ParallelSort.h:27-31,
+IntermediateSortBuffers.comp:5-25): sort (key, original index) pairs, then gather whole
+records by index (K5, SortOriginalData.comp:27-51) and copy them back (ParallelSort.cpp:311-318).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .sorter import RadixSorter, gather_records, iota_u32
+
+
+class OriginalDataSsbo:
+    """Device buffer of `numItems` OriginalData records (uint32 `_value`), zero-filled."""
+
+    def __init__(self, numItems: int, device: Optional[int] = None):
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self._data = torch.zeros(int(numItems), dtype=torch.uint32, device=dev)
+
+    def NumItems(self) -> int:
+        return self._data.numel()
+
+    def Buffer(self) -> torch.Tensor:
+        """The device tensor (the reference's BufferId())."""
+        return self._data
+
+    def Upload(self, values) -> None:
+        """glBufferSubData (main.cpp:146-149)."""
+        t = torch.as_tensor(values).to(torch.int64).to(torch.uint32)
+        if t.numel() != self.NumItems():
+            raise ValueError("Upload: size mismatch")
+        self._data.copy_(t.to(self._data.device))
+
+    def Download(self) -> torch.Tensor:
+        """glMapBufferRange readback (ParallelSort.cpp:330-333)."""
+        return self._data.cpu()
+
+
+class ParallelSort:
+    """Bound to one OriginalDataSsbo; owns the sort scratch (ParallelSort.cpp:36-145)."""
+
+    def __init__(self, dataToSort: OriginalDataSsbo, stream: Optional[torch.cuda.Stream] = None):
+        if dataToSort is None:
+            raise ValueError("ParallelSort: dataToSort is None")
+        self._originalDataSsbo = dataToSort
+        self._stream = stream
+        # the record is its own key: a keys-only u32 sort at 8-bit digits
+        self._sorter = RadixSorter(max(dataToSort.NumItems(), 1), key_bits=32, pairs=False,
+                                   radix_bits=8, device=dataToSort.Buffer().device.index)
+
+    def Sort(self) -> None:
+        buf = self._originalDataSsbo.Buffer()
+        self._sorter.sort(buf, stream=self._stream)
+
+
+class RecordSort:
+    """Sort arbitrary fixed-size records by a uint32 key (the reference's intended use:
+    ParallelSort.h:13-31, e.g. particles by Morton code).
+
+    records: device tensor of shape (N, record_bytes) uint8 (or any contiguous tensor whose
+    first dimension is N); keys: device uint32 tensor of N keys (the K1 key-extraction hook,
+    OriginalDataToIntermediateData.comp:12-19,42, is the caller computing `keys`)."""
+
+    def __init__(self, capacity: int, radix_bits: int = 8, device: Optional[int] = None):
+        self.capacity = int(capacity)
+        self._sorter = RadixSorter(max(self.capacity, 1), key_bits=32, pairs=True,
+                                   radix_bits=radix_bits, device=device)
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self._idx = torch.empty(max(self.capacity, 1), dtype=torch.uint32, device=dev)
+
+    def sort(self, records: torch.Tensor, keys: torch.Tensor,
+             stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+        n = keys.numel()
+        if records.shape[0] != n:
+            raise ValueError("records and keys disagree on N")
+        if n == 0:
+            return records
+        rb = records.numel() * records.element_size() // n
+        idx = self._idx[:n]
+        iota_u32(idx, 0, stream)                       # K1: _globalIndexOfOriginalData = tid
+        self._sorter.sort(keys, idx, n=n, stream=stream)  # stable (key, idx) sort
+        copy = torch.empty_like(records)
+        gather_records(records, copy, idx, n, rb, stream)  # K5 gather
+        records.copy_(copy)                             # copy back
+        return records

@@ -1,0 +1,135 @@
+"""RadixSorter: the C-ABI sorter (grs_create / grs_sort) over torch device tensors.
+
+torch is only plumbing here: it owns the device buffers and the stream; every byte of the
+sort is moved by libgrs's HIP kernels (gpuradixsort_amd/csrc/grs_kernels.hpp).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from ._lib import GRS_KEY_U32, GRS_KEY_U64, check, grs_timing, lib
+
+_KEY_TYPES = {torch.int32: GRS_KEY_U32, torch.uint32: GRS_KEY_U32,
+              torch.int64: GRS_KEY_U64, torch.uint64: GRS_KEY_U64}
+
+
+def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class RadixSorter:
+    """Stable ascending LSD radix sort of unsigned keys (u32 or u64), optionally carrying a
+    uint32 payload; mirrors ParallelSort's ctor/Sort() split (ParallelSort.cpp:36-145 /
+    168-422): scratch is sized once at construction, sort() is asynchronous on the stream.
+
+    Keys are interpreted as UNSIGNED integers of their width whatever torch dtype holds
+    them (torch.int32 / torch.uint32 / torch.int64 / torch.uint64)."""
+
+    def __init__(self, capacity: int, key_bits: int = 32, pairs: bool = False,
+                 radix_bits: int = 8, device: Optional[int] = None):
+        L = lib()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.capacity = int(capacity)
+        self.key_bits = int(key_bits)
+        self.pairs = bool(pairs)
+        self.radix_bits = int(radix_bits)
+        self.device = int(device)
+        kt = GRS_KEY_U32 if key_bits == 32 else GRS_KEY_U64
+        if key_bits not in (32, 64):
+            raise ValueError("key_bits must be 32 or 64")
+        h = ctypes.c_void_p()
+        check(L.grs_create(ctypes.byref(h), self.capacity, kt, int(self.pairs), self.radix_bits,
+                           self.device), "grs_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().grs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def scratch_bytes(self) -> int:
+        return int(lib().grs_scratch_bytes(self._h))
+
+    def _check_keys(self, keys: torch.Tensor, vals: Optional[torch.Tensor]) -> None:
+        if not keys.is_cuda or not keys.is_contiguous():
+            raise ValueError("keys must be a contiguous device tensor")
+        if keys.element_size() * 8 != self.key_bits:
+            raise ValueError(f"keys must be {self.key_bits}-bit")
+        if self.pairs:
+            if vals is None or vals.numel() < keys.numel() or vals.element_size() != 4 \
+                    or not vals.is_contiguous() or not vals.is_cuda:
+                raise ValueError("pairs sorter needs a contiguous 32-bit device payload tensor")
+        elif vals is not None:
+            raise ValueError("this sorter was created without a payload")
+
+    def sort(self, keys: torch.Tensor, vals: Optional[torch.Tensor] = None, n: Optional[int] = None,
+             begin_bit: int = 0, end_bit: Optional[int] = None,
+             stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Sort keys[:n] (and vals[:n]) in place, stably, on `stream` (default: current)."""
+        self._check_keys(keys, vals)
+        n = keys.numel() if n is None else int(n)
+        end_bit = self.key_bits if end_bit is None else int(end_bit)
+        vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
+        check(lib().grs_sort_bits(self._h, _ptr(keys), vp, n, int(begin_bit), end_bit,
+                                  _stream_ptr(stream)), "grs_sort")
+
+    def set_profiling(self, ring: int) -> None:
+        """Keep per-phase hipEvent timings of the last `ring` sort calls (0 = off)."""
+        check(lib().grs_set_profiling(self._h, int(ring)), "grs_set_profiling")
+
+    def timing(self, k: int = 0) -> dict:
+        """Per-phase GPU ms of the k-th most recent profiled call (synchronises)."""
+        t = grs_timing()
+        check(lib().grs_timing_history(self._h, int(k), ctypes.byref(t)), "grs_timing_history")
+        return {"passes": t.passes, "total_ms": t.total_ms, "hist_ms": t.hist_ms,
+                "pass_ms": list(t.pass_ms)[: t.passes], "copy_ms": t.copy_ms}
+
+    def check_error(self) -> None:
+        check(lib().grs_check_error(self._h), "grs_check_error")
+
+
+# ---- boundary helpers -----------------------------------------------------------------
+
+def fill_splitmix(out: torch.Tensor, seed: int, first_index: int = 0,
+                  stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """key[i] = splitmix64(seed ^ (first_index + i)) truncated to out's width (device)."""
+    check(lib().grs_fill_splitmix(_ptr(out), out.numel(), out.element_size(),
+                                  seed & (2**64 - 1), first_index, _stream_ptr(stream)),
+          "grs_fill_splitmix")
+    return out
+
+
+def iota_u32(out: torch.Tensor, start: int = 0, stream=None) -> torch.Tensor:
+    check(lib().grs_iota_u32(_ptr(out), out.numel(), start, _stream_ptr(stream)), "grs_iota_u32")
+    return out
+
+
+def gather_records(src: torch.Tensor, dst: torch.Tensor, idx: torch.Tensor, n: int,
+                   record_bytes: int, stream=None) -> torch.Tensor:
+    check(lib().grs_gather_records(_ptr(src), _ptr(dst), _ptr(idx), n, record_bytes,
+                                   _stream_ptr(stream)), "grs_gather_records")
+    return dst
+
+
+def count_inversions(keys: torch.Tensor, n: Optional[int] = None, stream=None) -> int:
+    n = keys.numel() if n is None else n
+    out = ctypes.c_uint64()
+    check(lib().grs_count_inversions(_ptr(keys), n, keys.element_size(), ctypes.byref(out),
+                                     _stream_ptr(stream)), "grs_count_inversions")
+    return int(out.value)

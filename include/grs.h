@@ -1,0 +1,131 @@
+/* grs.h — C-ABI of libgrs, the MI355X-native (gfx950) stable LSD radix sort.
+ *
+ * This is the drop-in boundary for the reference's hot path: the ParallelSort compute
+ * controller of amdreallyfast/GpuRadixSort.  Every entry point below names the reference
+ * interface it replaces (paths relative to the reference repository root).
+ *
+ *   reference (OpenGL 4.5 / GLSL)                         libgrs (HIP, gfx950)
+ *   ---------------------------------------------------   ---------------------------------
+ *   ParallelSort::ParallelSort(const OriginalDataSsbo&)    grs_create      (scratch sized once)
+ *     Include/ComputeControllers/ParallelSort.h:46,
+ *     Source/ComputeControllers/ParallelSort.cpp:36-145
+ *   ParallelSort::Sort()                                   grs_sort / grs_sort_bits
+ *     ParallelSort.h:48, ParallelSort.cpp:168-422
+ *   K1 OriginalDataToIntermediateData.comp:24-52           grs_iota_u32 (idx = i) + the key
+ *                                                          extraction is the caller's layout
+ *   K5 SortOriginalData.comp:27-51 + copy-back             grs_gather_records
+ *     (ParallelSort.cpp:300-320)
+ *   verification loop ParallelSort.cpp:325-352             grs_count_inversions
+ *   durations.txt timing dump ParallelSort.cpp:357-417      grs_last_timing
+ *   ~SsboBase() (Source/SSBOs/SsboBase.cpp:55-59)           grs_destroy
+ *
+ * Conventions:
+ *  - All data pointers are HIP device pointers owned by the caller; the sorter owns its
+ *    scratch (ping-pong buffers, look-back status, control block), sized at create time.
+ *  - Calls are asynchronous on the given stream (a hipStream_t passed as void*; NULL = the
+ *    null stream).  No call synchronises except grs_last_timing and grs_count_inversions.
+ *  - The sort is stable and in place from the caller's view (the result lands back in
+ *    d_keys / d_vals, as ParallelSort.cpp:311-318 copies the result back).
+ *  - Errors are returned, never printed: n > capacity is GRS_ECAPACITY (the reference
+ *    silently corrupts memory beyond 1,048,576 items: PrefixScanBuffer.comp:36).
+ *  - One sorter per stream / host thread (the reference is single-context too).
+ */
+#ifndef GRS_H_
+#define GRS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GRS_VERSION 100 /* 1.0.0 */
+
+typedef enum grs_status {
+  GRS_OK = 0,
+  GRS_EINVAL = 1,      /* bad argument (null pointer, bad radix/bit range, ...) */
+  GRS_ENOMEM = 2,      /* hipMalloc failed */
+  GRS_EHIP = 3,        /* a HIP runtime call failed; see grs_last_error() */
+  GRS_ECAPACITY = 4,   /* n exceeds the sorter's capacity or the 2^30-1 per-call limit */
+  GRS_ENODEV = 5,      /* no HIP device / bad device ordinal */
+  GRS_ETIMEOUT = 6     /* a look-back spin exceeded its bound (reported by grs_check_error) */
+} grs_status;
+
+typedef enum grs_key_type { GRS_KEY_U32 = 0, GRS_KEY_U64 = 1 } grs_key_type;
+
+typedef struct grs_sorter grs_sorter;
+
+/* Per-phase GPU times of the last profiled grs_sort call (hipEvents on the call's stream).
+ * Replaces the reference's durations.txt (ParallelSort.cpp:357-417), which timed host
+ * submission only. */
+typedef struct grs_timing {
+  int passes;
+  float total_ms;
+  float hist_ms;             /* memset of the control block + upfront histogram */
+  float pass_ms[16];         /* one onesweep launch per digit */
+  float copy_ms;             /* final copy for an odd pass count (0 otherwise) */
+} grs_timing;
+
+/* Library version (GRS_VERSION) and the last error message of this host thread. */
+int grs_version(void);
+const char* grs_status_string(grs_status s);
+const char* grs_last_error(void);
+
+/* Create a sorter for up to `capacity` items of key type `key_type`, optionally moving a
+ * uint32 payload with every key (with_u32_payload = 1: the reference's IntermediateData
+ * {_data, _globalIndexOfOriginalData} pair, Include/SSBOs/IntermediateData.h:12-30).
+ * radix_bits: 4 or 8 digit width, 0 = auto (8).  device: HIP device ordinal.
+ * Replaces ParallelSort::ParallelSort (ParallelSort.cpp:36-145). */
+grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
+                      int with_u32_payload, int radix_bits, int device);
+void grs_destroy(grs_sorter* s);
+
+/* Bytes of device scratch the sorter holds (ping-pong + look-back status + control). */
+size_t grs_scratch_bytes(const grs_sorter* s);
+
+/* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a
+ * payload, d_vals[0..n) is permuted with its keys (d_vals may be NULL otherwise).
+ * Replaces ParallelSort::Sort() (ParallelSort.cpp:168-422). */
+grs_status grs_sort(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, void* stream);
+
+/* As grs_sort, restricted to key bits [begin_bit, end_bit) (the reference's fixed
+ * `for bitNumber in 0..31` loop, ParallelSort.cpp:236, made a parameter). */
+grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
+                         int begin_bit, int end_bit, void* stream);
+
+/* Per-phase hipEvent timing of later grs_sort calls: ring = number of most recent calls
+ * whose events are kept (0 = off).  Events are recorded on each call's own stream. */
+grs_status grs_set_profiling(grs_sorter* s, int ring);
+/* Synchronises on the last profiled call and returns its per-phase times. */
+grs_status grs_last_timing(grs_sorter* s, grs_timing* out);
+/* Same for the k-th most recent profiled call (k = 0: the last one; k < ring). */
+grs_status grs_timing_history(grs_sorter* s, int k, grs_timing* out);
+/* Synchronises and returns GRS_ETIMEOUT if any look-back spin of past calls gave up. */
+grs_status grs_check_error(grs_sorter* s);
+
+/* ---- boundary helpers (reference K1/K5/verification, synthetic data) ---- */
+
+/* d_out[i] = start + i  (K1's idx = tid, OriginalDataToIntermediateData.comp:42). */
+grs_status grs_iota_u32(uint32_t* d_out, size_t n, uint32_t start, void* stream);
+
+/* d_dst[i] = d_src[d_idx[i]] for records of record_bytes bytes (K5 gather,
+ * SortOriginalData.comp:27-51; the caller then owns the sorted copy). */
+grs_status grs_gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
+                              size_t record_bytes, void* stream);
+
+/* Synthetic keys of SURVEY §8(d): key[i] = splitmix64(seed ^ (first_index + i)) truncated
+ * to key_bytes (4 or 8). */
+grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t seed,
+                             uint64_t first_index, void* stream);
+
+/* Number of i in [1, n) with key[i] < key[i-1] (the reference's monotonic check,
+ * ParallelSort.cpp:336-352).  Synchronises. */
+grs_status grs_count_inversions(const void* d_keys, size_t n, int key_bytes,
+                                uint64_t* out_count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GRS_H_ */

@@ -1,0 +1,65 @@
+"""CPU tests of the drop-in boundary: libgrs.so loads, exports every symbol include/grs.h
+declares, and validates arguments before touching a device (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(REPO, "include", "grs.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(grs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("grs_create", "grs_sort", "grs_sort_bits", "grs_destroy", "grs_last_timing",
+                     "grs_gather_records", "grs_iota_u32", "grs_count_inversions"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    bound = {name for name, _, _ in _lib.SIGNATURES}
+    for name in declared_functions():
+        assert hasattr(L, name), f"libgrs.so does not export {name}"
+        assert name in bound, f"_lib.SIGNATURES lacks {name}"
+
+
+def test_version_and_status_strings():
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    assert L.grs_version() == 100
+    assert L.grs_status_string(0) == b"GRS_OK"
+    assert L.grs_status_string(4) == b"GRS_ECAPACITY"
+
+
+def test_create_validates_arguments_without_a_device():
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.grs_create(None, 10, 0, 0, 8, 0) == _lib.GRS_EINVAL
+    assert L.grs_create(ctypes.byref(h), 10, 0, 0, 5, 0) == _lib.GRS_EINVAL      # radix 5
+    assert L.grs_create(ctypes.byref(h), 10, 7, 0, 8, 0) == _lib.GRS_EINVAL      # key type
+    assert L.grs_create(ctypes.byref(h), 1 << 30, 0, 0, 8, 0) == _lib.GRS_ECAPACITY
+    assert L.grs_sort(None, None, None, 0, None) == _lib.GRS_EINVAL
+    import torch
+
+    if not torch.cuda.is_available():
+        assert L.grs_create(ctypes.byref(h), 10, 0, 0, 8, 0) == _lib.GRS_ENODEV
+        assert b"device" in L.grs_last_error()
+
+
+def test_python_errors_are_loud():
+    from gpuradixsort_amd import GrsError, _lib
+
+    with pytest.raises(GrsError):
+        _lib.check(_lib.GRS_EINVAL, "probe")

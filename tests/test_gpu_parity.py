@@ -1,0 +1,213 @@
+"""GPU parity tests: libgrs's HIP sort (through the C-ABI) against the oracle.
+
+Bar: bit-exact keys AND the exact stable permutation (payload = input index, the reference's
+_globalIndexOfOriginalData).  N <= 1,048,576 u32 cases are checked against the restatement
+of the reference's own GLSL path (oracle.ref_parallel_sort); larger and u64 cases against
+stable sorts (C merge sort / numpy stable argsort); full BASELINE sizes against committed
+SHA-256 digests of the expected output plus size-independent properties.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_SORTERS = {}
+
+
+def sorter(key_bits, pairs, radix_bits, capacity):
+    import gpuradixsort_amd as grs
+
+    k = (key_bits, pairs, radix_bits)
+    s = _SORTERS.get(k)
+    if s is None or s.capacity < capacity:
+        if s is not None:
+            s.close()
+        s = grs.RadixSorter(max(capacity, 1 << 20), key_bits=key_bits, pairs=pairs,
+                            radix_bits=radix_bits)
+        _SORTERS[k] = s
+    return s
+
+
+def to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def gpu_sort(keys: np.ndarray, pairs: bool, radix_bits: int, dev, begin_bit=0, end_bit=None):
+    kb = keys.dtype.itemsize * 8
+    s = sorter(kb, pairs, radix_bits, keys.size)
+    k = to_dev(keys, dev)
+    v = to_dev(np.arange(keys.size, dtype=np.uint32), dev) if pairs else None
+    s.sort(k, v, begin_bit=begin_bit, end_bit=end_bit)
+    torch.cuda.synchronize()
+    s.check_error()
+    return k.cpu().numpy(), (v.cpu().numpy() if pairs else None)
+
+
+def distributions(n, kb, rng):
+    dt = np.uint32 if kb == 32 else np.uint64
+    top = np.iinfo(dt).max
+    yield "uniform", rng.integers(0, top, n, dtype=dt, endpoint=True)
+    yield "perm", rng.permutation(n).astype(dt)                 # main.cpp:120-125
+    yield "all_equal", np.full(n, 7, dt)
+    yield "all_max", np.full(n, top, dt)                        # 0xffffffff is a real key
+    yield "sorted", np.sort(rng.integers(0, top, n, dtype=dt, endpoint=True))
+    yield "reversed", np.arange(n, 0, -1).astype(dt)
+    yield "16_unique", (rng.integers(0, 16, n).astype(dt) * dt(0x10000001))
+    yield "mixed_max", np.where(rng.random(n) < 0.3, top, rng.integers(0, 100, n)).astype(dt)
+    yield "low_entropy", (rng.integers(0, top, n, dtype=dt, endpoint=True)
+                          & rng.integers(0, top, n, dtype=dt, endpoint=True)
+                          & rng.integers(0, top, n, dtype=dt, endpoint=True))
+
+
+SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 12289, 65536, 1 << 20]
+
+
+@pytest.mark.parametrize("radix_bits", [4, 8])
+@pytest.mark.parametrize("pairs", [False, True])
+@pytest.mark.parametrize("n", SIZES)
+def test_u32_matches_reference_path(gpu, n, pairs, radix_bits):
+    """u32, N <= 2^20: keys and stable permutation == the reference's GLSL path."""
+    rng = np.random.default_rng(1000 + n)
+    for name, keys in distributions(n, 32, rng):
+        if n > 65536 and name not in ("uniform", "perm", "16_unique"):
+            continue
+        rk, rp = oracle.ref_parallel_sort(keys)
+        gk, gv = gpu_sort(keys, pairs, radix_bits, gpu)
+        assert np.array_equal(gk, rk), f"{name}: keys differ"
+        if pairs:
+            assert np.array_equal(gv, rp), f"{name}: permutation differs (stability)"
+
+
+@pytest.mark.parametrize("radix_bits", [4, 8])
+@pytest.mark.parametrize("pairs", [False, True])
+@pytest.mark.parametrize("n", [0, 1, 65, 4097, 12289, 100003, 1 << 20])
+def test_u64_matches_stable_sort(gpu, n, pairs, radix_bits):
+    rng = np.random.default_rng(2000 + n)
+    for name, keys in distributions(n, 64, rng):
+        if n > 65536 and name not in ("uniform", "16_unique", "mixed_max"):
+            continue
+        perm = oracle.stable_argsort(keys)
+        gk, gv = gpu_sort(keys, pairs, radix_bits, gpu)
+        assert np.array_equal(gk, keys[perm]), f"{name}: keys differ"
+        if pairs:
+            assert np.array_equal(gv, perm), f"{name}: permutation differs"
+
+
+def test_golden_16key_kat(gpu):
+    kat = json.load(open(os.path.join(GOLDEN, "main_cpp_16key.json")))
+    keys = np.array(kat["input"], np.uint32)
+    for rb in (4, 8):
+        gk, gv = gpu_sort(keys, True, rb, gpu)
+        assert gk.tolist() == kat["sorted"] and gv.tolist() == kat["perm"]
+
+
+def test_bit_ranges(gpu):
+    """grs_sort_bits: sort on key bits [b, e) only, stably (the reference's bit loop,
+    ParallelSort.cpp:236, made a parameter)."""
+    rng = np.random.default_rng(7)
+    keys = rng.integers(0, 2**32, 300_001, dtype=np.uint64).astype(np.uint32)
+    for b, e in ((0, 12), (5, 17), (16, 32), (3, 4), (0, 31)):
+        sub = (keys >> np.uint32(b)) & np.uint32((1 << (e - b)) - 1)
+        perm = oracle.stable_argsort(sub)
+        for rb in (4, 8):
+            gk, gv = gpu_sort(keys, True, rb, gpu, b, e)
+            assert np.array_equal(gv, perm) and np.array_equal(gk, keys[perm]), (b, e, rb)
+
+
+def test_larger_u32(gpu):
+    rng = np.random.default_rng(11)
+    for n in ((1 << 20) + 1, 3_000_017):
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        keys[::97] = 0xFFFFFFFF
+        perm = oracle.stable_argsort(keys)
+        for rb in (4, 8):
+            gk, gv = gpu_sort(keys, True, rb, gpu)
+            assert np.array_equal(gv, perm) and np.array_equal(gk, keys[perm])
+
+
+def _digest(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name,radix_bits", [("c1_64k_u32", 8), ("c1_64k_u32_pairs", 8),
+                                             ("c2_16m_u32", 4)])
+def test_config_digests_small(gpu, name, radix_bits):
+    import gpuradixsort_amd as grs
+
+    rec = json.load(open(os.path.join(GOLDEN, "digests.json")))[name]
+    n, kb, pairs = rec["n"], rec["key_bits"], rec["pairs"]
+    k = torch.empty(n, dtype=torch.uint32, device=gpu)
+    grs.fill_splitmix(k, rec["seed"])   # device generator == oracle generator
+    assert np.array_equal(k.cpu().numpy(), oracle.splitmix_keys(n, kb, rec["seed"]))
+    s = sorter(kb, pairs, radix_bits, n)
+    v = None
+    if pairs:
+        v = torch.empty(n, dtype=torch.uint32, device=gpu)
+        grs.iota_u32(v)
+    s.sort(k, v)
+    torch.cuda.synchronize()
+    assert _digest(k.cpu().numpy()) == rec["sha256_keys"]
+    if pairs:
+        assert _digest(v.cpu().numpy()) == rec["sha256_perm"]
+
+
+@pytest.mark.parametrize("name,radix_bits", [("c3_256m_u32_pairs", 8), ("c5_256m_u64", 8)])
+def test_config_digests_full_size(gpu, name, radix_bits):
+    """Full BASELINE sizes: exact SHA-256 of the expected output, plus the properties
+    (sortedness via the device inversion counter)."""
+    import gpuradixsort_amd as grs
+
+    digests = json.load(open(os.path.join(GOLDEN, "digests.json")))
+    if name not in digests:
+        pytest.fail(f"{name} digest missing: run tests/golden/make_golden.py --large")
+    rec = digests[name]
+    n, kb, pairs = rec["n"], rec["key_bits"], rec["pairs"]
+    dt = torch.uint32 if kb == 32 else torch.uint64
+    k = torch.empty(n, dtype=dt, device=gpu)
+    grs.fill_splitmix(k, rec["seed"])
+    v = None
+    if pairs:
+        v = torch.empty(n, dtype=torch.uint32, device=gpu)
+        grs.iota_u32(v)
+    s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=radix_bits)
+    s.sort(k, v)
+    torch.cuda.synchronize()
+    s.check_error()
+    assert grs.count_inversions(k) == 0
+    assert _digest(k.cpu().numpy()) == rec["sha256_keys"]
+    if pairs:
+        assert _digest(v.cpu().numpy()) == rec["sha256_perm"]
+    s.close()
+    del k, v
+    torch.cuda.empty_cache()
+
+
+def test_capacity_and_argument_errors(gpu):
+    import gpuradixsort_amd as grs
+
+    s = grs.RadixSorter(1000, key_bits=32, pairs=False)
+    k = torch.zeros(2000, dtype=torch.uint32, device=gpu)
+    with pytest.raises(grs.GrsError, match="ECAPACITY"):
+        s.sort(k)
+    with pytest.raises(grs.GrsError, match="EINVAL"):
+        s.sort(k, n=10, begin_bit=8, end_bit=8)
+    s.sort(k, n=0)   # N = 0 is a no-op (PrefixSumSsbo.cpp:121-124)
+
+
+def test_repeated_sorts_reuse_scratch(gpu):
+    """Sort() twice on one controller (main.cpp:159-160): the second call must still be
+    exact (status/ticket re-initialisation between calls)."""
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 2**32, 777_777, dtype=np.uint64).astype(np.uint32)
+    perm = oracle.stable_argsort(keys)
+    for _ in range(3):
+        gk, gv = gpu_sort(keys, True, 8, gpu)
+        assert np.array_equal(gv, perm)
