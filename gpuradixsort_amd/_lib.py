@@ -51,6 +51,8 @@ SIGNATURES = [
     ("grs_last_timing", c_int, [c_void_p, POINTER(grs_timing)]),
     ("grs_timing_history", c_int, [c_void_p, c_int, POINTER(grs_timing)]),
     ("grs_check_error", c_int, [c_void_p]),
+    ("grs_partition", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
+                              c_int, c_void_p, c_void_p]),
     ("grs_iota_u32", c_int, [c_void_p, c_size_t, c_uint32, c_void_p]),
     ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),

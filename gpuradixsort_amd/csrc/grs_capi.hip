@@ -37,11 +37,12 @@ grs_status set_err(grs_status s, const std::string& msg) {
 // Tile geometry per (key type, payload, radix).  ITEMS keys per thread, GRS_BLOCK threads.
 template <typename K, bool PAIRS, int RB>
 struct TileCfg {
+  static constexpr int BLOCK = GRS_BLOCK;
   static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 12 : 16) : (PAIRS ? 16 : 16);
-  static constexpr int TILE = GRS_BLOCK * ITEMS;
+  static constexpr int TILE = BLOCK * ITEMS;
 };
 
-constexpr int max_tile_min() { return GRS_BLOCK * 12; }  // smallest TILE over configs
+constexpr int max_tile_min() { return 2048; }  // smallest TILE over configs (sizes status)
 
 }  // namespace
 
@@ -232,9 +233,10 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     const int bits = std::min(RB, end_bit - shift);
     uint32_t* st_cur = (p & 1) ? st1 : st0;
     uint32_t* st_nxt = (p & 1) ? st0 : st1;
-    hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::ITEMS>), dim3(tiles),
-                       dim3(GRS_BLOCK), 0, stream, src, dst, vsrc, vdst, n, shift, bits,
-                       hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+    hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
+                       dim3(Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n,
+                       grs::RadixDigit<K>{shift, (1u << bits) - 1u}, hist + p * RADIX, tickets + p,
+                       st_cur, st_nxt, err);
     GRS_HIP(hipGetLastError());
     if ((r = mark()) != GRS_OK) return r;
     std::swap(src, dst);
@@ -256,9 +258,86 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   return GRS_OK;
 }
 
+// Stable key-range partition: one histogram launch + one onesweep launch with a splitter
+// digit (4-bit slot, up to 16 buckets).  Buckets land contiguously in keys_out/vals_out in
+// bucket order; bucket sizes are copied to d_counts[0..count].
+template <typename K, bool PAIRS>
+grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
+                         uint32_t* vals_out, uint32_t n, const K* splitters, int count,
+                         uint32_t* d_counts, hipStream_t stream) {
+  constexpr int RB = 4;
+  using Cfg = TileCfg<K, PAIRS, RB>;
+  grs::SplitterDigit<K> dig{};
+  dig.count = static_cast<uint32_t>(count);
+  for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) dig.s[i] = i < count ? splitters[i] : K(0);
+  const uint32_t tiles = (n + Cfg::TILE - 1) / Cfg::TILE;
+  const size_t words = static_cast<size_t>(tiles) * (1u << RB);
+  if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
+  uint32_t* hist = s->ctrl;
+  GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
+  const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
+  hipLaunchKernelGGL((grs::grs_digit_hist<K, grs::SplitterDigit<K>>), dim3(grid),
+                     dim3(GRS_HIST_BLOCK), 0, stream, keys, n, dig, hist, s->status,
+                     static_cast<uint32_t>(words));
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
+                                             grs::SplitterDigit<K>>),
+                     dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
+                     dig, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
+                     s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
+  GRS_HIP(hipGetLastError());
+  GRS_HIP(hipMemcpyAsync(d_counts, hist, (count + 1) * 4, hipMemcpyDeviceToDevice, stream));
+  return GRS_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+grs_status grs_partition(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                         void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                         const void* splitters, int n_splitters, uint32_t* d_counts,
+                         void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_partition: NULL sorter");
+  if (n_splitters < 0 || n_splitters > GRS_MAX_SPLITTERS || (n_splitters > 0 && !splitters))
+    return set_err(GRS_EINVAL, "grs_partition: 0..15 splitters required");
+  if (!d_counts) return set_err(GRS_EINVAL, "grs_partition: d_counts is NULL");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_partition: n exceeds sorter capacity");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (n == 0) {
+    GRS_HIP(hipMemsetAsync(d_counts, 0, (n_splitters + 1) * 4, st));
+    return GRS_OK;
+  }
+  if (!d_keys || !d_keys_out) return set_err(GRS_EINVAL, "grs_partition: NULL keys");
+  if (s->pairs && (!d_vals || !d_vals_out))
+    return set_err(GRS_EINVAL, "grs_partition: payload sorter needs d_vals / d_vals_out");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  const uint32_t n32 = static_cast<uint32_t>(n);
+  grs_status r;
+  if (s->key_type == GRS_KEY_U32) {
+    if (s->pairs)
+      r = run_partition<uint32_t, true>(s, (const uint32_t*)d_keys, d_vals, (uint32_t*)d_keys_out,
+                                        d_vals_out, n32, (const uint32_t*)splitters, n_splitters,
+                                        d_counts, st);
+    else
+      r = run_partition<uint32_t, false>(s, (const uint32_t*)d_keys, nullptr, (uint32_t*)d_keys_out,
+                                         nullptr, n32, (const uint32_t*)splitters, n_splitters,
+                                         d_counts, st);
+  } else {
+    if (s->pairs)
+      r = run_partition<uint64_t, true>(s, (const uint64_t*)d_keys, d_vals, (uint64_t*)d_keys_out,
+                                        d_vals_out, n32, (const uint64_t*)splitters, n_splitters,
+                                        d_counts, st);
+    else
+      r = run_partition<uint64_t, false>(s, (const uint64_t*)d_keys, nullptr, (uint64_t*)d_keys_out,
+                                         nullptr, n32, (const uint64_t*)splitters, n_splitters,
+                                         d_counts, st);
+  }
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
 
 grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, int begin_bit,
                          int end_bit, void* stream) {

@@ -28,6 +28,13 @@
 
 // Bounded spins (look-back): give up after this many polls and raise the error word.
 #define GRS_SPIN_LIMIT (1u << 22)
+// Key-range partition (multi-GPU exchange): at most this many splitters -> 16 buckets.
+#define GRS_MAX_SPLITTERS 15
+
+// Predecessor tiles polled per look-back step (loads in flight per digit thread).
+#ifndef GRS_LB_WIN
+#define GRS_LB_WIN 16
+#endif
 
 // Layout of the per-sorter control block (uint32 words), zeroed once per sort call.
 //   [0, GRS_CTRL_HIST_WORDS)           global digit histograms, [pass][radix]

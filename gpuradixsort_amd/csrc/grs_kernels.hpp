@@ -35,6 +35,31 @@ __device__ __forceinline__ uint32_t digit_of(K key, int shift, uint32_t mask) {
   return static_cast<uint32_t>(key >> shift) & mask;
 }
 
+// Digit of an LSD pass: key bits [shift, shift + bits).
+template <typename K>
+struct RadixDigit {
+  int shift;
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t operator()(K k) const { return digit_of(k, shift, mask); }
+  // digit of the all-ones padding key (the largest digit this functor can return)
+  __device__ __forceinline__ uint32_t max_digit() const { return mask; }
+};
+
+// Bucket of a key-range partition (multi-GPU exchange, gpuradixsort_amd/sharded.py):
+// number of splitters <= key, monotone in the key; `count` <= GRS_MAX_SPLITTERS.
+template <typename K>
+struct SplitterDigit {
+  uint32_t count;
+  K s[GRS_MAX_SPLITTERS];
+  __device__ __forceinline__ uint32_t operator()(K k) const {
+    uint32_t b = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < count; ++i) b += s[i] <= k;
+    return b;
+  }
+  __device__ __forceinline__ uint32_t max_digit() const { return count; }
+};
+
 // Number of set bits of `m` in lanes strictly below this lane.
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -44,16 +69,22 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
 __device__ __forceinline__ uint32_t lane_id() { return mbcnt64(~0ull); }
 
 // Mask of the lanes of this wave whose digit equals this lane's digit (all 64 lanes active).
+// Per digit bit b: sel = splat(bit b of d) (v_bfe_i32), one ballot of it (v_cmp -> SGPR
+// pair), then m &= ~(ballot ^ sel) as ONE v_bitop3_b32 per 32-bit half (LUT 0x90 over
+// (m, ballot, sel)): 4 VALU per digit bit.  The empty asm pins `sel` in a VGPR so the
+// compiler derives the ballot from it instead of re-shifting the digit.
 template <int RB>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d) {
-  uint64_t m = ~0ull;
+  uint32_t lo = ~0u, hi = ~0u;
 #pragma unroll
   for (int b = 0; b < RB; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t bb = __ballot(bit);
-    m &= bit ? bb : ~bb;
+    uint32_t sel = static_cast<uint32_t>(static_cast<int32_t>(d << (31 - b)) >> 31);
+    asm volatile("" : "+v"(sel));
+    const uint64_t bb = __builtin_amdgcn_ballot_w64(sel != 0);
+    lo = __builtin_amdgcn_bitop3_b32(lo, static_cast<uint32_t>(bb), sel, 0x90);
+    hi = __builtin_amdgcn_bitop3_b32(hi, static_cast<uint32_t>(bb >> 32), sel, 0x90);
   }
-  return m;
+  return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
 __device__ __forceinline__ uint32_t ld_status(const uint32_t* p) {
@@ -138,8 +169,25 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
   }
 }
 
+// Histogram of one digit functor (the bucket sizes of a key-range partition).
+template <typename K, typename DigitF>
+__global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_digit_hist(
+    const K* __restrict__ keys, uint32_t n, const DigitF dig, uint32_t* __restrict__ g_hist,
+    uint32_t* __restrict__ clear, uint32_t clear_words) {
+  __shared__ uint32_t s_hist[GRS_MAX_SPLITTERS + 1];
+  const uint32_t t = threadIdx.x;
+  if (t <= GRS_MAX_SPLITTERS) s_hist[t] = 0;
+  for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < clear_words; i += gridDim.x * GRS_HIST_BLOCK)
+    clear[i] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < n; i += gridDim.x * GRS_HIST_BLOCK)
+    atomicAdd(&s_hist[dig(keys[i])], 1u);
+  __syncthreads();
+  if (t <= GRS_MAX_SPLITTERS && s_hist[t]) atomicAdd(&g_hist[t], s_hist[t]);
+}
+
 // ----------------------------------------------------------------------------------------
-// one LSD pass: rank + look-back + scatter of one RB-bit digit
+// one LSD pass: count + publish + rank + look-back + scatter of one RB-bit digit
 // ----------------------------------------------------------------------------------------
 //
 // Tile layout: tile T covers keys [T*TILE, (T+1)*TILE); wave w of the tile owns the
@@ -148,50 +196,47 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
 // keys (256 B for u32) and ranking items j = 0..ITEMS-1 in order, lanes in order, visits
 // keys in input order, which is what makes the rank stable.
 //
+// Order of work inside a tile (the look-back latency hides behind the ranking):
+//   1. ticket -> tile id; load the tile into registers
+//   2. tile digit counts by LDS atomics; publish them (AGGREGATE, or INCLUSIVE for tile 0)
+//   3. stable rank: per item, a ballot match mask; one leader lane per distinct digit does
+//      a returning LDS atomic on the wave's counter (in program order, so items stay in
+//      order without a read->write chain per item); peers read the leader's old count
+//   4. look-back over predecessor tiles -> global offset of each digit; publish INCLUSIVE
+//   5. reorder the tile in LDS by (digit, input order); store runs to their global slots
+//
 // status:      [num_tiles][RADIX] look-back words of this pass (zeroed before the launch)
 // status_next: the other status buffer: this tile zeroes its own slice for the next pass
 // tickets:     per-pass atomic counter; ticket order = tile order, so a tile only ever
 //              waits on tiles that already started (no forward-progress assumption)
-template <typename K, bool PAIRS, int RB, int ITEMS>
-__global__ __launch_bounds__(GRS_BLOCK) void grs_onesweep_pass(
-    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
-    uint32_t* __restrict__ vals_out, uint32_t n, int shift, int bits,
-    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
-    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word) {
-  constexpr int RADIX = 1 << RB;
-  constexpr int WAVES = GRS_BLOCK / GRS_WAVE;
-  constexpr int TILE = GRS_BLOCK * ITEMS;
-  constexpr int WAVE_TILE = GRS_WAVE * ITEMS;
-  static_assert(RADIX <= GRS_BLOCK, "one look-back thread per digit");
+// DBG (timing ablations in tools/, never set by the library): bit 0 = no look-back (uniform-
+// data estimate of the prefix instead), bit 1 = contiguous stores instead of the scatter,
+// bit 2 = publish late (after ranking) instead of early.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS>
+struct OnesweepSmem {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int TILE = BLOCK * ITEMS;
+  uint32_t cnt[WAVES * RADIX];  // per-wave digit counters -> local offsets
+  uint32_t hist[RADIX];         // tile digit counts (early publish)
+  uint32_t base[RADIX];         // global dst of tile-local index 0 of digit d
+  uint64_t wsum[WAVES];         // block-scan carries
+  uint32_t ticket[2];
+  K keys[TILE];
+  uint32_t vals[PAIRS ? TILE : 1];
+};
 
-  __shared__ uint32_t s_cnt[WAVES * RADIX];  // per-wave digit counters -> local offsets
-  __shared__ uint32_t s_base[RADIX];         // global dst of tile-local index 0 of digit d
-  __shared__ uint64_t s_wsum[WAVES];         // block-scan carries
-  __shared__ uint32_t s_tile;
-  __shared__ K s_keys[TILE];
-  __shared__ uint32_t s_vals[PAIRS ? TILE : 1];
-
-  const uint32_t t = threadIdx.x;
-  const uint32_t lane = t & (GRS_WAVE - 1);
-  const uint32_t w = t >> 6;
-  const uint32_t dmask = (1u << bits) - 1u;
-
-  if (t == 0) s_tile = atomicAdd(ticket, 1u);
-  // zero this wave's digit counters
-  for (uint32_t i = lane; i < RADIX; i += GRS_WAVE) s_cnt[w * RADIX + i] = 0;
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  if (t < RADIX) status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
-
+// Load tile `tile` wave-striped into registers; padding slots get the all-ones key.
+template <typename K, bool PAIRS, int BLOCK, int ITEMS>
+__device__ __forceinline__ void load_tile(const K* __restrict__ keys_in,
+                                          const uint32_t* __restrict__ vals_in, uint32_t n,
+                                          uint32_t tile, K (&key)[ITEMS], uint32_t (&val)[ITEMS]) {
+  constexpr int TILE = BLOCK * ITEMS;
+  const uint32_t lane = threadIdx.x & (GRS_WAVE - 1);
+  const uint32_t w = threadIdx.x >> 6;
   const uint32_t tile_base = tile * TILE;
-  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
-  const uint32_t wbase = tile_base + w * WAVE_TILE;
-
-  // ---- load (wave-striped, coalesced) ----
-  K key[ITEMS];
-  uint32_t val[ITEMS];
-  if (valid == TILE) {
+  const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS);
+  if (n - tile_base >= static_cast<uint32_t>(TILE)) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) key[j] = keys_in[wbase + j * GRS_WAVE + lane];
     if constexpr (PAIRS) {
@@ -207,27 +252,78 @@ __global__ __launch_bounds__(GRS_BLOCK) void grs_onesweep_pass(
       if constexpr (PAIRS) val[j] = i < n ? vals_in[i] : 0u;
     }
   }
+}
 
-  // ---- stable rank inside the wave: ballot match masks, per-wave LDS counters ----
+// Steps 2-5 for one tile whose keys are in registers.  Precondition: every thread of the
+// block has passed a barrier since the previous tile's last LDS access.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF>
+__device__ __forceinline__ void process_tile(
+    OnesweepSmem<K, PAIRS, RB, BLOCK, ITEMS>& sm, const K (&key)[ITEMS],
+    const uint32_t (&val)[ITEMS], uint32_t tile, K* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ status,
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word) {
+  constexpr int RADIX = 1 << RB;
+  constexpr int WAVES = BLOCK / GRS_WAVE;
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr bool EARLY = (DBG & 4) == 0;
+  static_assert(RADIX <= BLOCK, "one look-back thread per digit");
+
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = dig.max_digit();  // digit of the padding key
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t pad = TILE - valid;
+  uint32_t* my_status = status + static_cast<size_t>(tile) * RADIX + t;
+
+  for (uint32_t i = t; i < WAVES * RADIX; i += BLOCK) sm.cnt[i] = 0;
+  if (EARLY && t < RADIX) sm.hist[t] = 0;
+  if (t < RADIX) status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
+  // digits once per item: rank[j] = digit << 16 | (tile-local rank, filled in step 3)
   uint32_t rank[ITEMS];
 #pragma unroll
+  for (int j = 0; j < ITEMS; ++j) rank[j] = dig(key[j]) << 16;
+  __syncthreads();
+
+  // ---- 2. tile digit counts, published before the (long) ranking ----
+  if constexpr (EARLY) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) atomicAdd(&sm.hist[rank[j] >> 16], 1u);
+    __syncthreads();
+    if constexpr ((DBG & 1) == 0) {
+      if (t < RADIX) {
+        const uint32_t c = sm.hist[t] - ((t == dmask) ? pad : 0u);
+        st_status(my_status, ((tile == 0 ? GRS_FLAG_INCLUSIVE : GRS_FLAG_AGGREGATE) << GRS_FLAG_SHIFT) | c);
+      }
+    }
+  }
+
+  // ---- 3. stable rank inside the wave ----
+  // Item by item: every lane reads its digit's running wave count, then ONE leader lane per
+  // distinct digit adds the item's count for that digit (no-return LDS atomic).  LDS
+  // executes a wave's instructions in order, so item j's read sees items < j and no
+  // read -> write dependency stalls the loop.  rank[j] = (local rank) | digit << 16.
+#pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t d = digit_of(key[j], shift, dmask);
+    const uint32_t d = rank[j] >> 16;
     const uint64_t m = match_digit<RB>(d);
     const uint32_t below = mbcnt64(m);
-    const uint32_t old = s_cnt[w * RADIX + d];
-    if (below == 0) s_cnt[w * RADIX + d] = old + static_cast<uint32_t>(__popcll(m));
-    rank[j] = old + below;
+    uint32_t* c = &sm.cnt[w * RADIX + d];
+    const uint32_t old = *c;
+    if (below == 0) atomicAdd(c, static_cast<uint32_t>(__popcll(m)));
+    rank[j] |= old + below;
   }
   __syncthreads();
 
-  // ---- per digit: exclusive over waves, tile count, block scans, look-back ----
+  // ---- 4. per digit: exclusive over waves, block scans, look-back ----
   uint32_t tile_cnt = 0;
   if (t < RADIX) {
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) {
-      const uint32_t c = s_cnt[ww * RADIX + t];
-      s_cnt[ww * RADIX + t] = tile_cnt;
+      const uint32_t c = sm.cnt[ww * RADIX + t];
+      sm.cnt[ww * RADIX + t] = tile_cnt;
       tile_cnt += c;
     }
   }
@@ -236,69 +332,153 @@ __global__ __launch_bounds__(GRS_BLOCK) void grs_onesweep_pass(
   uint64_t packed = 0;
   if (t < RADIX) packed = (static_cast<uint64_t>(pass_hist[t]) << 32) | tile_cnt;
   const uint64_t incl = wave_incl_scan(packed, lane);
-  if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
+  if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
   __syncthreads();
   uint64_t carry = 0;
-  for (uint32_t ww = 0; ww < w; ++ww) carry += s_wsum[ww];
+  for (uint32_t ww = 0; ww < w; ++ww) carry += sm.wsum[ww];
   const uint64_t excl = carry + incl - packed;
 
   if (t < RADIX) {
     const uint32_t global_start = static_cast<uint32_t>(excl >> 32);
     const uint32_t local_start = static_cast<uint32_t>(excl);
     // padding keys (last tile only) are ranked but never published or stored
-    const uint32_t pad = TILE - valid;
     const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
-    uint32_t* my = status + static_cast<size_t>(tile) * RADIX + t;
     uint32_t prefix = 0;
-    if (tile == 0) {
-      st_status(my, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | publish);
+    if constexpr (DBG & 1) {
+      prefix = static_cast<uint32_t>((static_cast<uint64_t>(pass_hist[t]) * tile) /
+                                     ((n + TILE - 1) / TILE));
+    } else if (tile == 0) {
+      if (!EARLY) st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | publish);
     } else {
-      st_status(my, (GRS_FLAG_AGGREGATE << GRS_FLAG_SHIFT) | publish);
-      int64_t pt = static_cast<int64_t>(tile) - 1;
+      if (!EARLY) st_status(my_status, (GRS_FLAG_AGGREGATE << GRS_FLAG_SHIFT) | publish);
+      // Windowed look-back: poll GRS_LB_WIN predecessors at once (independent loads in
+      // flight), consume AGGREGATEs nearest-first up to the first INCLUSIVE; restart the
+      // window at the first NOT_READY.  Tile 0 is always INCLUSIVE, so the walk ends.
+      int32_t pt = static_cast<int32_t>(tile) - 1;
       uint32_t spins = 0;
       while (true) {
-        const uint32_t v = ld_status(status + static_cast<size_t>(pt) * RADIX + t);
-        const uint32_t f = v >> GRS_FLAG_SHIFT;
-        if (f == GRS_FLAG_NOT_READY) {
+        uint32_t v[GRS_LB_WIN];
+#pragma unroll
+        for (int k = 0; k < GRS_LB_WIN; ++k)
+          v[k] = (pt - k >= 0) ? ld_status(status + static_cast<size_t>(pt - k) * RADIX + t)
+                               : (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT);
+        int consumed = 0;
+        bool done = false;
+        bool blocked = false;
+#pragma unroll
+        for (int k = 0; k < GRS_LB_WIN; ++k) {
+          if (!done && !blocked) {
+            const uint32_t f = v[k] >> GRS_FLAG_SHIFT;
+            if (f == GRS_FLAG_NOT_READY) {
+              blocked = true;
+            } else {
+              prefix += v[k] & GRS_VALUE_MASK;
+              ++consumed;
+              done = f == GRS_FLAG_INCLUSIVE;
+            }
+          }
+        }
+        if (done) break;
+        pt -= consumed;
+        if (consumed == 0) {
           if (++spins > GRS_SPIN_LIMIT) {
             atomicOr(error_word, 1u);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
-          continue;
         }
-        prefix += v & GRS_VALUE_MASK;
-        if (f == GRS_FLAG_INCLUSIVE) break;
-        --pt;
       }
-      st_status(my, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
+      st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
     }
-    s_base[t] = global_start + prefix - local_start;
+    sm.base[t] = global_start + prefix - local_start;
 #pragma unroll
-    for (int ww = 0; ww < WAVES; ++ww) s_cnt[ww * RADIX + t] += local_start;
+    for (int ww = 0; ww < WAVES; ++ww) sm.cnt[ww * RADIX + t] += local_start;
   }
   __syncthreads();
 
-  // ---- reorder the tile in LDS by (digit, input order) ----
+  // ---- 5. reorder the tile in LDS by (digit, input order), then store the runs ----
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t d = digit_of(key[j], shift, dmask);
-    const uint32_t pos = s_cnt[w * RADIX + d] + rank[j];
-    s_keys[pos] = key[j];
-    if constexpr (PAIRS) s_vals[pos] = val[j];
+    const uint32_t d = rank[j] >> 16;
+    const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
+    sm.keys[pos] = key[j];
+    if constexpr (PAIRS) sm.vals[pos] = val[j];
   }
   __syncthreads();
 
-  // ---- scatter: consecutive threads write consecutive slots of each digit run ----
+  // consecutive threads write consecutive slots of each digit run
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
-    const uint32_t i = k * GRS_BLOCK + t;
+    const uint32_t i = k * BLOCK + t;
     if (i < valid) {
-      const K kk = s_keys[i];
-      const uint32_t dst = s_base[digit_of(kk, shift, dmask)] + i;
+      const K kk = sm.keys[i];
+      uint32_t dst = (DBG & 2) ? tile_base + i : sm.base[dig(kk)] + i;
+      if constexpr ((DBG & 1) != 0) dst = dst < n ? dst : n - 1;  // estimated prefix may overrun
       keys_out[dst] = kk;
-      if constexpr (PAIRS) vals_out[dst] = s_vals[i];
+      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
     }
+  }
+}
+
+// One tile per workgroup (grid = number of tiles).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK) void grs_onesweep_pass(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  __shared__ OnesweepSmem<K, PAIRS, RB, BLOCK, ITEMS> sm;
+  if (threadIdx.x == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = sm.ticket[0];
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, tile, key, val);
+  process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out, n, dig,
+                                                pass_hist, status, status_next, error_word);
+}
+
+// Persistent variant: a fixed grid of workgroups loops over tickets; the next tile's keys
+// are loaded into a second register set while the current tile is ranked and scattered,
+// so HBM reads stay in flight across the compute and look-back phases of every tile.
+// A workgroup processes its tickets in increasing order, so it never waits on a tile it
+// holds itself (no deadlock whatever the residency).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK) void grs_onesweep_persistent(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  __shared__ OnesweepSmem<K, PAIRS, RB, BLOCK, ITEMS> sm;
+  constexpr uint32_t TILE = BLOCK * ITEMS;
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  K ka[ITEMS], kb[ITEMS];
+  uint32_t va[ITEMS], vb[ITEMS];
+  if (threadIdx.x == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+  __syncthreads();
+  uint32_t cur = sm.ticket[0];
+  if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
+  while (cur < tiles) {
+    // ticket for the tile after `cur` (the barrier orders it after every read of ticket[0])
+    __syncthreads();
+    if (threadIdx.x == 0) sm.ticket[1] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t nxt = sm.ticket[1];
+    if (nxt < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, nxt, kb, vb);
+    process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, ka, va, cur, keys_out, vals_out, n, dig,
+                                                  pass_hist, status, status_next, error_word);
+    if (nxt >= tiles) break;
+    __syncthreads();
+    if (threadIdx.x == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    cur = sm.ticket[0];
+    if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
+    process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, kb, vb, nxt, keys_out, vals_out, n, dig,
+                                                  pass_hist, status, status_next, error_word);
   }
 }
 

@@ -89,6 +89,23 @@ class RadixSorter:
         check(lib().grs_sort_bits(self._h, _ptr(keys), vp, n, int(begin_bit), end_bit,
                                   _stream_ptr(stream)), "grs_sort")
 
+    def partition(self, keys: torch.Tensor, keys_out: torch.Tensor, splitters, counts: torch.Tensor,
+                  vals: Optional[torch.Tensor] = None, vals_out: Optional[torch.Tensor] = None,
+                  n: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Stable key-range partition (grs_partition): bucket(k) = #splitters <= k; buckets
+        land contiguously in keys_out (and vals_out); bucket sizes -> counts (device u32)."""
+        import numpy as np
+
+        self._check_keys(keys, vals)
+        n = keys.numel() if n is None else int(n)
+        sp = np.ascontiguousarray(np.asarray(splitters, dtype=np.uint32 if self.key_bits == 32
+                                             else np.uint64))
+        vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
+        vo = _ptr(vals_out) if vals_out is not None else ctypes.c_void_p(0)
+        check(lib().grs_partition(self._h, _ptr(keys), vp, _ptr(keys_out), vo, n,
+                                  ctypes.c_void_p(sp.ctypes.data), int(sp.size), _ptr(counts),
+                                  _stream_ptr(stream)), "grs_partition")
+
     def set_profiling(self, ring: int) -> None:
         """Keep per-phase hipEvent timings of the last `ring` sort calls (0 = off)."""
         check(lib().grs_set_profiling(self._h, int(ring)), "grs_set_profiling")

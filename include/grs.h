@@ -104,6 +104,17 @@ grs_status grs_timing_history(grs_sorter* s, int k, grs_timing* out);
 /* Synchronises and returns GRS_ETIMEOUT if any look-back spin of past calls gave up. */
 grs_status grs_check_error(grs_sorter* s);
 
+/* Stable key-range partition for the multi-GPU exchange (gpuradixsort_amd/sharded.py):
+ * bucket(key) = number of splitters <= key (splitters: host array of n_splitters <= 15
+ * non-decreasing keys of the sorter's key type).  Writes the keys (and payload) to
+ * d_keys_out / d_vals_out grouped by bucket, input order kept inside each bucket, and the
+ * n_splitters + 1 bucket sizes to d_counts (device uint32).  New with respect to the
+ * reference, which has no multi-device path. */
+grs_status grs_partition(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                         void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                         const void* splitters, int n_splitters, uint32_t* d_counts,
+                         void* stream);
+
 /* ---- boundary helpers (reference K1/K5/verification, synthetic data) ---- */
 
 /* d_out[i] = start + i  (K1's idx = tid, OriginalDataToIntermediateData.comp:42). */

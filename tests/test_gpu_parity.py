@@ -211,3 +211,34 @@ def test_repeated_sorts_reuse_scratch(gpu):
     for _ in range(3):
         gk, gv = gpu_sort(keys, True, 8, gpu)
         assert np.array_equal(gv, perm)
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+@pytest.mark.parametrize("pairs", [False, True])
+def test_partition_is_stable_range_split(gpu, kb, pairs):
+    """grs_partition (the multi-GPU exchange's local step): bucket = #splitters <= key,
+    buckets contiguous in order, input order kept inside each bucket."""
+    import gpuradixsort_amd as grs
+
+    rng = np.random.default_rng(kb + pairs)
+    dt = np.uint32 if kb == 32 else np.uint64
+    for n, nsplit in ((1, 1), (1000, 3), (100_003, 7), (777_777, 15), (50_000, 0)):
+        keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        keys[::13] = np.iinfo(dt).max
+        sp = np.sort(rng.choice(keys, nsplit)) if nsplit else np.zeros(0, dt)
+        bucket = np.searchsorted(sp, keys, side="right")
+        perm = np.argsort(bucket, kind="stable")
+        s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=8)
+        k = to_dev(keys, gpu)
+        ko = torch.empty_like(k)
+        v = vo = None
+        if pairs:
+            v = to_dev(np.arange(n, dtype=np.uint32), gpu)
+            vo = torch.empty_like(v)
+        cnt = torch.zeros(nsplit + 1, dtype=torch.uint32, device=gpu)
+        s.partition(k, ko, sp, cnt, v, vo)
+        torch.cuda.synchronize()
+        assert np.array_equal(cnt.cpu().numpy(), np.bincount(bucket, minlength=nsplit + 1))
+        assert np.array_equal(ko.cpu().numpy(), keys[perm])
+        if pairs:
+            assert np.array_equal(vo.cpu().numpy(), perm)
