@@ -226,6 +226,62 @@ struct OnesweepSmem {
   uint32_t vals[PAIRS ? TILE : 1];
 };
 
+// Exclusive prefix of digit d over tiles [0, tile): windowed decoupled look-back.  Polls
+// GRS_LB_WIN predecessors at once (independent loads in flight), consumes AGGREGATEs
+// nearest-first up to the first INCLUSIVE, restarts the window at the first NOT_READY.
+// Tile 0 is always INCLUSIVE, so the walk ends; spins are bounded (error word).
+template <int RADIX>
+__device__ __forceinline__ uint32_t lookback(const uint32_t* status, uint32_t tile, uint32_t d,
+                                             uint32_t* error_word) {
+  uint32_t prefix = 0;
+  int32_t pt = static_cast<int32_t>(tile) - 1;
+  uint32_t spins = 0;
+  while (true) {
+    uint32_t v[GRS_LB_WIN];
+#pragma unroll
+    for (int k = 0; k < GRS_LB_WIN; ++k)
+      v[k] = (pt - k >= 0) ? ld_status(status + static_cast<size_t>(pt - k) * RADIX + d)
+                           : (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT);
+    int consumed = 0;
+    bool done = false;
+    bool blocked = false;
+#pragma unroll
+    for (int k = 0; k < GRS_LB_WIN; ++k) {
+      if (!done && !blocked) {
+        const uint32_t f = v[k] >> GRS_FLAG_SHIFT;
+        if (f == GRS_FLAG_NOT_READY) {
+          blocked = true;
+        } else {
+          prefix += v[k] & GRS_VALUE_MASK;
+          ++consumed;
+          done = f == GRS_FLAG_INCLUSIVE;
+        }
+      }
+    }
+    if (done) break;
+    pt -= consumed;
+    if (consumed == 0) {
+      if (++spins > GRS_SPIN_LIMIT) {
+        atomicOr(error_word, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return prefix;
+}
+
+// Diagnostic build only (DBG bit 3, tools/lab): thread 0 records s_memtime at phase
+// boundaries into dbg[64 + tile * 8 + k] (cycles since the workgroup started).
+#define GRS_STAMP(k)                                                                       \
+  do {                                                                                     \
+    if constexpr ((DBG & 8) != 0) {                                                        \
+      if (threadIdx.x == 0)                                                                \
+        error_word[64 + static_cast<size_t>(tile) * 8 + (k)] =                             \
+            static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);                 \
+    }                                                                                      \
+  } while (0)
+
 // Load tile `tile` wave-striped into registers; padding slots get the all-ones key.
 template <typename K, bool PAIRS, int BLOCK, int ITEMS>
 __device__ __forceinline__ void load_tile(const K* __restrict__ keys_in,
@@ -262,11 +318,13 @@ __device__ __forceinline__ void process_tile(
     const uint32_t (&val)[ITEMS], uint32_t tile, K* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ status,
-    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word) {
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word,
+    uint64_t t_begin = 0) {
   constexpr int RADIX = 1 << RB;
   constexpr int WAVES = BLOCK / GRS_WAVE;
   constexpr int TILE = BLOCK * ITEMS;
   constexpr bool EARLY = (DBG & 4) == 0;
+  GRS_STAMP(0);
   static_assert(RADIX <= BLOCK, "one look-back thread per digit");
 
   const uint32_t t = threadIdx.x;
@@ -292,6 +350,7 @@ __device__ __forceinline__ void process_tile(
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) atomicAdd(&sm.hist[rank[j] >> 16], 1u);
     __syncthreads();
+    GRS_STAMP(1);
     if constexpr ((DBG & 1) == 0) {
       if (t < RADIX) {
         const uint32_t c = sm.hist[t] - ((t == dmask) ? pad : 0u);
@@ -316,6 +375,7 @@ __device__ __forceinline__ void process_tile(
     rank[j] |= old + below;
   }
   __syncthreads();
+  GRS_STAMP(2);
 
   // ---- 4. per digit: exclusive over waves, block scans, look-back ----
   uint32_t tile_cnt = 0;
@@ -334,6 +394,7 @@ __device__ __forceinline__ void process_tile(
   const uint64_t incl = wave_incl_scan(packed, lane);
   if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
   __syncthreads();
+  GRS_STAMP(3);
   uint64_t carry = 0;
   for (uint32_t ww = 0; ww < w; ++ww) carry += sm.wsum[ww];
   const uint64_t excl = carry + incl - packed;
@@ -351,43 +412,7 @@ __device__ __forceinline__ void process_tile(
       if (!EARLY) st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | publish);
     } else {
       if (!EARLY) st_status(my_status, (GRS_FLAG_AGGREGATE << GRS_FLAG_SHIFT) | publish);
-      // Windowed look-back: poll GRS_LB_WIN predecessors at once (independent loads in
-      // flight), consume AGGREGATEs nearest-first up to the first INCLUSIVE; restart the
-      // window at the first NOT_READY.  Tile 0 is always INCLUSIVE, so the walk ends.
-      int32_t pt = static_cast<int32_t>(tile) - 1;
-      uint32_t spins = 0;
-      while (true) {
-        uint32_t v[GRS_LB_WIN];
-#pragma unroll
-        for (int k = 0; k < GRS_LB_WIN; ++k)
-          v[k] = (pt - k >= 0) ? ld_status(status + static_cast<size_t>(pt - k) * RADIX + t)
-                               : (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT);
-        int consumed = 0;
-        bool done = false;
-        bool blocked = false;
-#pragma unroll
-        for (int k = 0; k < GRS_LB_WIN; ++k) {
-          if (!done && !blocked) {
-            const uint32_t f = v[k] >> GRS_FLAG_SHIFT;
-            if (f == GRS_FLAG_NOT_READY) {
-              blocked = true;
-            } else {
-              prefix += v[k] & GRS_VALUE_MASK;
-              ++consumed;
-              done = f == GRS_FLAG_INCLUSIVE;
-            }
-          }
-        }
-        if (done) break;
-        pt -= consumed;
-        if (consumed == 0) {
-          if (++spins > GRS_SPIN_LIMIT) {
-            atomicOr(error_word, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
+      prefix = lookback<RADIX>(status, tile, t, error_word);
       st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
     }
     sm.base[t] = global_start + prefix - local_start;
@@ -395,6 +420,7 @@ __device__ __forceinline__ void process_tile(
     for (int ww = 0; ww < WAVES; ++ww) sm.cnt[ww * RADIX + t] += local_start;
   }
   __syncthreads();
+  GRS_STAMP(4);
 
   // ---- 5. reorder the tile in LDS by (digit, input order), then store the runs ----
 #pragma unroll
@@ -405,6 +431,7 @@ __device__ __forceinline__ void process_tile(
     if constexpr (PAIRS) sm.vals[pos] = val[j];
   }
   __syncthreads();
+  GRS_STAMP(5);
 
   // consecutive threads write consecutive slots of each digit run
 #pragma unroll
@@ -418,6 +445,124 @@ __device__ __forceinline__ void process_tile(
       if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
     }
   }
+  if constexpr ((DBG & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    GRS_STAMP(6);
+  }
+}
+
+// Variant of process_tile that resolves the look-back BEFORE ranking (DBG bit 4): the
+// tile's INCLUSIVE words are published as soon as its counts and its predecessors' prefixes
+// are known, so the chain of inclusive prefixes is not gated by ranking time.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF>
+__device__ __forceinline__ void process_tile_lbfirst(
+    OnesweepSmem<K, PAIRS, RB, BLOCK, ITEMS>& sm, const K (&key)[ITEMS],
+    const uint32_t (&val)[ITEMS], uint32_t tile, K* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ status,
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word,
+    uint64_t t_begin = 0) {
+  constexpr int RADIX = 1 << RB;
+  constexpr int WAVES = BLOCK / GRS_WAVE;
+  constexpr int TILE = BLOCK * ITEMS;
+  static_assert(RADIX <= BLOCK, "one look-back thread per digit");
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = dig.max_digit();
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t pad = TILE - valid;
+  uint32_t* my_status = status + static_cast<size_t>(tile) * RADIX + t;
+  GRS_STAMP(0);
+
+  for (uint32_t i = t; i < WAVES * RADIX; i += BLOCK) sm.cnt[i] = 0;
+  if (t < RADIX) sm.hist[t] = 0;
+  if (t < RADIX) status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
+  uint32_t rank[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) rank[j] = dig(key[j]) << 16;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) atomicAdd(&sm.hist[rank[j] >> 16], 1u);
+  __syncthreads();
+  GRS_STAMP(1);
+
+  // tile counts -> (global start, tile-local start) per digit, then the look-back
+  const uint32_t tile_cnt = t < RADIX ? sm.hist[t] : 0u;
+  const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
+  if (t < RADIX) {
+    st_status(my_status, ((tile == 0 ? GRS_FLAG_INCLUSIVE : GRS_FLAG_AGGREGATE) << GRS_FLAG_SHIFT) | publish);
+  }
+  uint64_t packed = 0;
+  if (t < RADIX) packed = (static_cast<uint64_t>(pass_hist[t]) << 32) | tile_cnt;
+  const uint64_t incl = wave_incl_scan(packed, lane);
+  if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
+  __syncthreads();
+  uint64_t carry = 0;
+  for (uint32_t ww = 0; ww < w; ++ww) carry += sm.wsum[ww];
+  const uint64_t excl = carry + incl - packed;
+  GRS_STAMP(2);
+  if (t < RADIX) {
+    uint32_t prefix = 0;
+    if (tile != 0) {
+      prefix = lookback<RADIX>(status, tile, t, error_word);
+      st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
+    }
+    sm.base[t] = static_cast<uint32_t>(excl >> 32) + prefix - static_cast<uint32_t>(excl);
+    sm.hist[t] = static_cast<uint32_t>(excl);  // tile-local start of digit t
+  }
+  GRS_STAMP(3);
+
+  // stable rank inside the wave (as process_tile step 3)
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = rank[j] >> 16;
+    const uint64_t m = match_digit<RB>(d);
+    const uint32_t below = mbcnt64(m);
+    uint32_t* c = &sm.cnt[w * RADIX + d];
+    const uint32_t old = *c;
+    if (below == 0) atomicAdd(c, static_cast<uint32_t>(__popcll(m)));
+    rank[j] |= old + below;
+  }
+  __syncthreads();
+  GRS_STAMP(4);
+  if (t < RADIX) {
+    uint32_t run = sm.hist[t];
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) {
+      const uint32_t c = sm.cnt[ww * RADIX + t];
+      sm.cnt[ww * RADIX + t] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = rank[j] >> 16;
+    const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
+    sm.keys[pos] = key[j];
+    if constexpr (PAIRS) sm.vals[pos] = val[j];
+  }
+  __syncthreads();
+  GRS_STAMP(5);
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * BLOCK + t;
+    if (i < valid) {
+      const K kk = sm.keys[i];
+      const uint32_t dst = sm.base[dig(kk)] + i;
+      keys_out[dst] = kk;
+      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+    }
+  }
+  if constexpr ((DBG & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    GRS_STAMP(6);
+  }
 }
 
 // One tile per workgroup (grid = number of tiles).
@@ -430,14 +575,26 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_pass(
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
     uint32_t* __restrict__ error_word) {
   __shared__ OnesweepSmem<K, PAIRS, RB, BLOCK, ITEMS> sm;
+  const uint64_t t_begin = (DBG & 8) ? __builtin_amdgcn_s_memtime() : 0;
   if (threadIdx.x == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
   __syncthreads();
   const uint32_t tile = sm.ticket[0];
   K key[ITEMS];
   uint32_t val[ITEMS];
   load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, tile, key, val);
-  process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out, n, dig,
-                                                pass_hist, status, status_next, error_word);
+  if constexpr ((DBG & 16) != 0)
+    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out,
+                                                          n, dig, pass_hist, status, status_next,
+                                                          error_word, t_begin);
+  else
+    process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out, n, dig,
+                                                  pass_hist, status, status_next, error_word,
+                                                  t_begin);
+  if constexpr ((DBG & 8) != 0) {
+    if (threadIdx.x == 0) {
+      error_word[64 + static_cast<size_t>(tile) * 8 + 7] = static_cast<uint32_t>(t_begin >> 8);
+    }
+  }
 }
 
 // Persistent variant: a fixed grid of workgroups loops over tickets; the next tile's keys

@@ -1,7 +1,9 @@
 """Kernel laboratory: interleaved timing of onesweep-pass variants (tools/lab.hip).
 
-python tools/lab.py [--n N] [--rounds R] [--variants 16:0,16:1,...]
-Prints one line per variant: median / min ms and algorithmic GB/s (8 B per key per pass).
+python tools/lab.py [--n N] [--rounds R] [--lib liblab.so] [--copy]
+                    [--variants kb:pairs:block:items:dbg[:grid],...]
+Prints one line per variant: median / min ms and algorithmic GB/s of one pass
+(2 x (key + payload bytes) per key); DBG & 8 variants also print per-phase cycle stamps.
 """
 import argparse
 import ctypes
@@ -9,6 +11,7 @@ import os
 import statistics
 import sys
 
+import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -20,65 +23,93 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 27)
     ap.add_argument("--lib", default="liblab.so")
-    ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--variants", default="256:16:0,256:16:4,256:16:1,256:16:2,256:16:3,256:16:7,"
-                    "256:24:0,256:32:0,256:32:4,256:32:1,256:32:2,256:32:3,512:8:0,512:12:0,"
-                    "512:16:0,512:16:4,512:16:1,512:16:3,1024:8:0,1024:16:0")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="32:0:256:32:16,32:0:256:32:0")
+    ap.add_argument("--copy", action="store_true")
     a = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, a.lib))
     vp = ctypes.c_void_p
+    P = lambda t: vp(t.data_ptr())  # noqa: E731
     n = a.n
     dev = torch.device("cuda", 0)
-    keys = torch.empty(n, dtype=torch.uint32, device=dev)
-    grs.fill_splitmix(keys, 0x6A09E667F3BCC908 + 4)
-    out = torch.empty_like(keys)
-    hist = torch.zeros(4 * 256, dtype=torch.uint32, device=dev)
-    ticket = torch.zeros(4, dtype=torch.uint32, device=dev)
-    err = torch.zeros(4, dtype=torch.uint32, device=dev)
-    max_tiles = (n + 1023) // 1024
-    st = torch.zeros(max_tiles * 256, dtype=torch.uint32, device=dev)
-    st2 = torch.zeros_like(st)
-    s = torch.cuda.current_stream()
-    sp = vp(s.cuda_stream)
-    P = lambda t: vp(t.data_ptr())  # noqa: E731
-    assert L.lab_hist(P(keys), ctypes.c_uint32(n), P(hist), P(st), ctypes.c_uint32(0), sp) == 0
-    torch.cuda.synchronize()
+    sp = vp(torch.cuda.current_stream().cuda_stream)
 
     variants = []
     for v in a.variants.split(","):
-        parts = v.split(":")
-        b, it, dbg = parts[:3]
-        grid = int(parts[3]) if len(parts) > 3 else 0   # persistent grid (0 = one tile per WG)
-        variants.append((int(b), int(it), int(dbg), grid))
-    times = {v: [] for v in variants}
-    copy_t = {0: [], 1: []}
+        parts = [int(x) for x in v.split(":")]
+        variants.append(tuple(parts + [0] * (6 - len(parts))))
+    bufs = {}
+    for kb in sorted({v[0] for v in variants}):
+        dt = torch.uint32 if kb == 32 else torch.uint64
+        keys = torch.empty(n, dtype=dt, device=dev)
+        grs.fill_splitmix(keys, 0x6A09E667F3BCC908 + 4)
+        hist = torch.zeros(8 * 256, dtype=torch.uint32, device=dev)
+        scratch = torch.zeros(1, dtype=torch.uint32, device=dev)
+        assert L.lab_hist(kb, P(keys), ctypes.c_uint32(n), P(hist), P(scratch), ctypes.c_uint32(0), sp) == 0
+        bufs[kb] = (keys, torch.empty_like(keys), hist)
+    vin = torch.arange(n, dtype=torch.int64, device=dev).to(torch.uint32)
+    vout = torch.empty_like(vin)
+    ticket = torch.zeros(4, dtype=torch.uint32, device=dev)
+    max_tiles = (n + 1023) // 1024
+    err = torch.zeros(64 + 8 * max_tiles + 64, dtype=torch.uint32, device=dev)
+    st = torch.zeros(max_tiles * 256, dtype=torch.uint32, device=dev)
+    st2 = torch.zeros_like(st)
+    torch.cuda.synchronize()
+
+    def run(v):
+        kb, pairs, block, items, dbg, grid = v
+        keys, out, hist = bufs[kb]
+        L.lab_set_persistent(grid)
+        rc = L.lab_pass2(kb, pairs, block, items, dbg, P(keys), P(out), P(vin), P(vout),
+                         ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
+        assert rc == 0, (v, rc)
+
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for r in range(a.rounds):
+    times = {v: [] for v in variants}
+    copy_t = []
+    for _ in range(a.rounds):
         for v in variants:
             st.zero_()
             ticket.zero_()
-            L.lab_set_persistent(v[3])
+            torch.cuda.synchronize()
             e0.record()
-            rc = L.lab_pass(v[0] * 10000 + v[1] * 16 + v[2], P(keys), P(out), ctypes.c_uint32(n), P(hist), P(ticket),
-                            P(st), P(st2), P(err), 0, sp)
+            run(v)
             e1.record()
-            assert rc == 0, (v, rc)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1))
-        for w in (0, 1):
+        if a.copy:
+            k32 = bufs[min(bufs)]
             e0.record()
-            L.lab_copy(w, P(keys), P(out), ctypes.c_uint32(n), sp)
+            L.lab_copy(P(k32[0]), P(k32[1]), ctypes.c_uint32(n), sp)
             e1.record()
             torch.cuda.synchronize()
-            copy_t[w].append(e0.elapsed_time(e1))
-    alg = n * 8
+            copy_t.append(e0.elapsed_time(e1))
     print(f"n={n}  error word={int(err[0].item())}")
-    for w in (0, 1):
-        med = statistics.median(copy_t[w])
-        print(f"copy {'x4   ' if w else 'dword'}          median {med:8.4f} ms  {alg / med / 1e6:8.1f} GB/s")
+    if copy_t:
+        med = statistics.median(copy_t)
+        print(f"copy x4 of n u32: median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s")
     for v in variants:
+        kb, pairs = v[0], v[1]
+        alg = n * 2 * (kb // 8 + (4 if pairs else 0))
         med, mn = statistics.median(times[v]), min(times[v])
-        print(f"block={v[0]:4d} items={v[1]:2d} dbg={v[2]} grid={v[3]:4d}  median {med:8.4f} ms  min {mn:8.4f}  {alg / med / 1e6:8.1f} GB/s")
+        print(f"kb={kb} pairs={pairs} block={v[2]:4d} items={v[3]:2d} dbg={v[4]:2d} grid={v[5]:4d}"
+              f"  median {med:8.4f} ms  min {mn:8.4f}  {alg / med / 1e6:8.1f} GB/s")
+    names = ["ticket+issue", "load+hist", "p2", "p3", "p4", "reorder", "store"]
+    for v in variants:
+        if not (v[4] & 8):
+            continue
+        err.zero_()
+        st.zero_()
+        ticket.zero_()
+        run(v)
+        torch.cuda.synchronize()
+        tiles = (n + v[2] * v[3] - 1) // (v[2] * v[3])
+        a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+        ph = a_[:, :7]
+        d = np.diff(np.concatenate([np.zeros((tiles, 1)), ph], axis=1), axis=1)
+        print(f"stamps {v}: mean cycles per phase "
+              + ", ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d.mean(0)))
+              + f"  total={ph[:, 6].mean():.0f}")
 
 
 if __name__ == "__main__":
