@@ -37,8 +37,9 @@ grs_status set_err(grs_status s, const std::string& msg) {
 // Tile geometry per (key type, payload, radix).  ITEMS keys per thread, GRS_BLOCK threads.
 template <typename K, bool PAIRS, int RB>
 struct TileCfg {
+  // measured on MI355X, 2^27 uniform keys (tools/lab.py)
   static constexpr int BLOCK = GRS_BLOCK;
-  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 12 : 16) : (PAIRS ? 16 : 16);
+  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 8 : 16) : (PAIRS ? 16 : 24);
   static constexpr int TILE = BLOCK * ITEMS;
 };
 

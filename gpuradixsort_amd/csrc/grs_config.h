@@ -13,7 +13,7 @@
 #include <stdint.h>
 
 #define GRS_WAVE 64                 // CDNA wavefront width (never 32)
-#define GRS_BLOCK 256               // threads per onesweep / histogram workgroup (4 waves)
+#define GRS_BLOCK 512               // threads per onesweep workgroup (8 waves)
 #define GRS_HIST_BLOCK 256
 
 // Decoupled look-back status word: [31:30] flag, [29:0] digit count.
@@ -33,7 +33,7 @@
 
 // Predecessor tiles polled per look-back step (loads in flight per digit thread).
 #ifndef GRS_LB_WIN
-#define GRS_LB_WIN 16
+#define GRS_LB_WIN 8
 #endif
 
 // Layout of the per-sorter control block (uint32 words), zeroed once per sort call.

@@ -452,7 +452,8 @@ __device__ __forceinline__ void process_tile(
   }
 }
 
-// Variant of process_tile that resolves the look-back BEFORE ranking (DBG bit 4): the
+// Default tile body: resolves the look-back BEFORE ranking (process_tile, DBG bit 5, ranks
+// first and is kept for ablations): the
 // tile's INCLUSIVE words are published as soon as its counts and its predecessors' prefixes
 // are known, so the chain of inclusive prefixes is not gated by ranking time.
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF>
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_pass(
   K key[ITEMS];
   uint32_t val[ITEMS];
   load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, tile, key, val);
-  if constexpr ((DBG & 16) != 0)
+  if constexpr ((DBG & 32) == 0)   // default: look-back before ranking
     process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out,
                                                           n, dig, pass_hist, status, status_next,
                                                           error_word, t_begin);
@@ -626,16 +627,18 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_persistent(
     __syncthreads();
     const uint32_t nxt = sm.ticket[1];
     if (nxt < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, nxt, kb, vb);
-    process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, ka, va, cur, keys_out, vals_out, n, dig,
-                                                  pass_hist, status, status_next, error_word);
+    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, ka, va, cur, keys_out, vals_out, n,
+                                                          dig, pass_hist, status, status_next,
+                                                          error_word);
     if (nxt >= tiles) break;
     __syncthreads();
     if (threadIdx.x == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
     __syncthreads();
     cur = sm.ticket[0];
     if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
-    process_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, kb, vb, nxt, keys_out, vals_out, n, dig,
-                                                  pass_hist, status, status_next, error_word);
+    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, kb, vb, nxt, keys_out, vals_out, n,
+                                                          dig, pass_hist, status, status_next,
+                                                          error_word);
   }
 }
 
