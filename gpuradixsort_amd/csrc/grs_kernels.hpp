@@ -112,23 +112,41 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 // g_hist:     [passes][RADIX] uint32 counters, zeroed by the caller (control-block memset)
 // clear/cw:   status buffer of pass 0, zeroed here (grid-stride) so no separate memset
 //             launch is needed.
+//
+// Bank-private counters: lane l adds into copy (l % COPIES) of the histogram, laid out so
+// that copy c lives entirely in LDS bank c.  The 32 lanes of one half-wave LDS access then
+// never collide (no bank conflicts, no same-address serialisation, whatever the key
+// distribution — with 4-bit digits 64 lanes share 16 counters).  Two digits share one
+// 32-bit word as 16-bit halves; a copy counts at most ceil(n / grid / COPIES) keys, which the
+// launch keeps below 2^16 (grid > n / 2^18, COPIES >= 8).  32 KB of LDS per block.
+template <typename K, int RB>
+struct HistLayout {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int MAXP = (8 * sizeof(K) + RB - 1) / RB;
+  static constexpr int PER_COPY = MAXP * (RADIX / 2);   // words of one copy
+  static constexpr int COPIES = (8192 / PER_COPY) >= 32 ? 32 : (8192 / PER_COPY);
+  static constexpr int WORDS = PER_COPY * COPIES;
+  static_assert(COPIES >= 8, "16-bit counters need >= 8 copies");
+};
+
 template <typename K, int RB>
 __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
     uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words) {
-  constexpr int RADIX = 1 << RB;
-  constexpr int MAXP = (8 * sizeof(K) + RB - 1) / RB;
-  // Two sub-histograms (even/odd waves) halve LDS atomic contention on skewed inputs.
-  __shared__ uint32_t s_hist[2][MAXP * RADIX];
+  using HL = HistLayout<K, RB>;
+  constexpr int RADIX = HL::RADIX;
+  constexpr int MAXP = HL::MAXP;
+  constexpr int COPIES = HL::COPIES;
+  __shared__ uint32_t s_hist[HL::WORDS];
 
   const uint32_t t = threadIdx.x;
-  for (uint32_t i = t; i < 2 * MAXP * RADIX; i += GRS_HIST_BLOCK) (&s_hist[0][0])[i] = 0;
+  for (uint32_t i = t; i < HL::WORDS; i += GRS_HIST_BLOCK) s_hist[i] = 0;
   // zero the first pass's look-back status words
   for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < clear_words; i += gridDim.x * GRS_HIST_BLOCK)
     clear[i] = 0;
   __syncthreads();
 
-  uint32_t* h = s_hist[(t >> 6) & 1];
+  const uint32_t copy = t & (COPIES - 1);
   int shifts[MAXP];
   uint32_t masks[MAXP];
 #pragma unroll
@@ -138,33 +156,52 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
     const int bits = (end_bit - s) < RB ? (end_bit - s) : RB;
     masks[p] = (p < passes && bits > 0) ? ((1u << bits) - 1u) : 0u;
   }
+  auto count = [&](K k) {
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      if (p < passes) {
+        const uint32_t d = digit_of(k, shifts[p], masks[p]);
+        atomicAdd(&s_hist[(p * (RADIX / 2) + (d >> 1)) * COPIES + copy], 1u << ((d & 1u) << 4));
+      }
+    }
+  };
 
   constexpr int VEC = 16 / sizeof(K);  // keys per 16-byte load
   using V = uint4;
   // 16-B vector loads need a 16-B aligned base; otherwise everything takes the scalar tail
   const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : n / VEC;
   const V* kv = reinterpret_cast<const V*>(keys);
-  for (uint32_t v = blockIdx.x * GRS_HIST_BLOCK + t; v < nvec; v += gridDim.x * GRS_HIST_BLOCK) {
+  const uint32_t stride = gridDim.x * GRS_HIST_BLOCK;
+  uint32_t v = blockIdx.x * GRS_HIST_BLOCK + t;
+  for (; v + 3 * stride < nvec; v += 4 * stride) {   // 4 loads in flight per thread
+    V x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = kv[v + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const K* kk = reinterpret_cast<const K*>(&x[u]);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) count(kk[e]);
+    }
+  }
+  for (; v < nvec; v += stride) {
     const V x = kv[v];
     const K* kk = reinterpret_cast<const K*>(&x);
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-#pragma unroll
-      for (int p = 0; p < MAXP; ++p)
-        if (p < passes) atomicAdd(&h[p * RADIX + digit_of(kk[e], shifts[p], masks[p])], 1u);
-    }
+    for (int e = 0; e < VEC; ++e) count(kk[e]);
   }
   // ragged tail (fewer than VEC keys)
   for (uint32_t i = nvec * VEC + blockIdx.x * GRS_HIST_BLOCK + t; i < n;
-       i += gridDim.x * GRS_HIST_BLOCK) {
-    const K k = keys[i];
-#pragma unroll
-    for (int p = 0; p < MAXP; ++p)
-      if (p < passes) atomicAdd(&h[p * RADIX + digit_of(k, shifts[p], masks[p])], 1u);
-  }
+       i += gridDim.x * GRS_HIST_BLOCK)
+    count(keys[i]);
   __syncthreads();
+  // reduce the copies: one (pass, digit) counter per thread iteration
   for (uint32_t i = t; i < static_cast<uint32_t>(passes * RADIX); i += GRS_HIST_BLOCK) {
-    const uint32_t c = s_hist[0][i] + s_hist[1][i];
+    const uint32_t p = i / RADIX, d = i % RADIX;
+    const uint32_t* row = &s_hist[(p * (RADIX / 2) + (d >> 1)) * COPIES];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < COPIES; ++k) c += (row[(k + t) & (COPIES - 1)] >> ((d & 1u) << 4)) & 0xFFFFu;
     if (c) atomicAdd(&g_hist[i], c);
   }
 }
@@ -456,14 +493,21 @@ __device__ __forceinline__ void process_tile(
 // first and is kept for ablations): the
 // tile's INCLUSIVE words are published as soon as its counts and its predecessors' prefixes
 // are known, so the chain of inclusive prefixes is not gated by ranking time.
-template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF>
+// `after_lookback()` runs on every thread once its look-back part is done (the persistent
+// kernel issues the next tile's loads there, so they never sit in front of a look-back wait).
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF,
+          typename Hook = NoHook>
 __device__ __forceinline__ void process_tile_lbfirst(
     OnesweepSmem<K, PAIRS, RB, BLOCK, ITEMS>& sm, const K (&key)[ITEMS],
     const uint32_t (&val)[ITEMS], uint32_t tile, K* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ status,
     uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word,
-    uint64_t t_begin = 0) {
+    uint64_t t_begin = 0, const Hook& after_lookback = Hook()) {
   constexpr int RADIX = 1 << RB;
   constexpr int WAVES = BLOCK / GRS_WAVE;
   constexpr int TILE = BLOCK * ITEMS;
@@ -515,6 +559,7 @@ __device__ __forceinline__ void process_tile_lbfirst(
     sm.hist[t] = static_cast<uint32_t>(excl);  // tile-local start of digit t
   }
   GRS_STAMP(3);
+  after_lookback();
 
   // stable rank inside the wave (as process_tile step 3)
 #pragma unroll
@@ -567,9 +612,10 @@ __device__ __forceinline__ void process_tile_lbfirst(
 }
 
 // One tile per workgroup (grid = number of tiles).
+// DBG bits 8-11 (lab only): minimum waves per SIMD for __launch_bounds__ (0 = no bound).
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
           typename DigitF = RadixDigit<K>>
-__global__ __launch_bounds__(BLOCK) void grs_onesweep_pass(
+__global__ __launch_bounds__(BLOCK, ((DBG >> 8) & 15) ? ((DBG >> 8) & 15) : 1) void grs_onesweep_pass(
     const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
@@ -598,14 +644,14 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_pass(
   }
 }
 
-// Persistent variant: a fixed grid of workgroups loops over tickets; the next tile's keys
-// are loaded into a second register set while the current tile is ranked and scattered,
-// so HBM reads stay in flight across the compute and look-back phases of every tile.
-// A workgroup processes its tickets in increasing order, so it never waits on a tile it
-// holds itself (no deadlock whatever the residency).
+// Persistent variant: a fixed grid of workgroups loops over tickets.  The next tile's keys
+// are loaded into a second register set right after the current tile's look-back (so no
+// look-back wait drains them) and stay in flight through ranking, reorder and stores.  A
+// workgroup processes its tickets in increasing order, so it never waits on a tile it holds
+// itself (no deadlock whatever the residency).
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
           typename DigitF = RadixDigit<K>>
-__global__ __launch_bounds__(BLOCK) void grs_onesweep_persistent(
+__global__ __launch_bounds__(BLOCK, ((DBG >> 8) & 15) ? ((DBG >> 8) & 15) : 1) void grs_onesweep_persistent(
     const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
@@ -620,25 +666,275 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_persistent(
   __syncthreads();
   uint32_t cur = sm.ticket[0];
   if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
+  uint32_t nxt = tiles;
   while (cur < tiles) {
-    // ticket for the tile after `cur` (the barrier orders it after every read of ticket[0])
-    __syncthreads();
+    // next ticket; visible to all threads after process_tile's first barrier
     if (threadIdx.x == 0) sm.ticket[1] = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t nxt = sm.ticket[1];
-    if (nxt < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, nxt, kb, vb);
-    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, ka, va, cur, keys_out, vals_out, n,
-                                                          dig, pass_hist, status, status_next,
-                                                          error_word);
+    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(
+        sm, ka, va, cur, keys_out, vals_out, n, dig, pass_hist, status, status_next, error_word,
+        0, [&]() {
+          nxt = sm.ticket[1];
+          if (nxt < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, nxt, kb, vb);
+        });
     if (nxt >= tiles) break;
-    __syncthreads();
+    __syncthreads();   // every read of ticket[0] (long done) and of the LDS tile is finished
     if (threadIdx.x == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(
+        sm, kb, vb, nxt, keys_out, vals_out, n, dig, pass_hist, status, status_next, error_word,
+        0, [&]() {
+          cur = sm.ticket[0];
+          if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
+        });
     __syncthreads();
-    cur = sm.ticket[0];
-    if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
-    process_tile_lbfirst<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, kb, vb, nxt, keys_out, vals_out, n,
-                                                          dig, pass_hist, status, status_next,
-                                                          error_word);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// streaming onesweep pass: persistent workgroups, LDS-DMA double-buffered tile prefetch
+// ----------------------------------------------------------------------------------------
+//
+// A fixed grid loops over tile tickets.  Tile i+1 is fetched HBM -> LDS with
+// global_load_lds_dwordx4 (no VGPRs) as soon as tile i's look-back is resolved, and stays in
+// flight through tile i's ranking, reorder and stores and the top of iteration i+1, so every
+// workgroup keeps a tile's worth of reads outstanding almost all the time.  Barriers after
+// the DMA issue are raw s_barrier + lgkmcnt(0) (a __syncthreads() would drain the DMA); the
+// DMA is retired by a counted vmcnt that skips exactly the tile's own scatter stores, which
+// are issued after it.  Tickets run two tiles ahead (fetched during a look-back, whose wait
+// absorbs the atomic's latency).  A workgroup processes its tickets in increasing order, so
+// it never waits on a tile it holds (no deadlock whatever the residency).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS>
+struct StreamSmem {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int TILE = BLOCK * ITEMS;
+  uint32_t cnt[WAVES * RADIX];
+  uint32_t hist[RADIX];
+  uint32_t base[RADIX];
+  uint64_t wsum[WAVES];
+  uint32_t ticket[4];
+  alignas(16) K kbuf[2][TILE];
+  alignas(16) uint32_t vbuf[PAIRS ? 2 : 1][PAIRS ? TILE : 4];
+};
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One global_load_lds_dwordx4: 16 bytes per lane from `gsrc` (per lane) into LDS at
+// `lds` + 16 * lane (lds wave-uniform).  Written as inline asm on purpose: the compiler
+// does not track the DMA, so it inserts no vmcnt(0) in front of unrelated LDS reads (which
+// would drain the prefetch); the kernel retires it with its own counted s_waitcnt.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, void* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :
+               : "s"(m0), "v"(gsrc)
+               : "memory", "m0");
+}
+
+// HBM -> LDS copy of one full tile (keys, and payload), 1 KiB per wave instruction.
+template <typename K, bool PAIRS, int BLOCK, int ITEMS>
+__device__ __forceinline__ void dma_tile(const K* __restrict__ keys_in,
+                                         const uint32_t* __restrict__ vals_in, uint32_t tile,
+                                         K* kdst, uint32_t* vdst) {
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr int WAVES = BLOCK / GRS_WAVE;
+  constexpr int KCH = TILE * static_cast<int>(sizeof(K)) / 1024;
+  constexpr int VCH = TILE * 4 / 1024;
+  static_assert(KCH % WAVES == 0 && VCH % WAVES == 0, "whole 1 KiB chunks per wave");
+  const uint32_t lane = threadIdx.x & (GRS_WAVE - 1);
+  const uint32_t w = threadIdx.x >> 6;
+  const char* ks = reinterpret_cast<const char*>(keys_in + static_cast<size_t>(tile) * TILE);
+#pragma unroll
+  for (int c = 0; c < KCH / WAVES; ++c) {
+    const int ch = c * WAVES + w;
+    lds_dma16(ks + ch * 1024 + lane * 16, reinterpret_cast<char*>(kdst) + ch * 1024);
+  }
+  if constexpr (PAIRS) {
+    const char* vs = reinterpret_cast<const char*>(vals_in + static_cast<size_t>(tile) * TILE);
+#pragma unroll
+    for (int c = 0; c < VCH / WAVES; ++c) {
+      const int ch = c * WAVES + w;
+      lds_dma16(vs + ch * 1024 + lane * 16, reinterpret_cast<char*>(vdst) + ch * 1024);
+    }
+  }
+}
+
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK) void grs_onesweep_stream(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  using SM = StreamSmem<K, PAIRS, RB, BLOCK, ITEMS>;
+  constexpr int RADIX = SM::RADIX;
+  constexpr int WAVES = SM::WAVES;
+  constexpr int TILE = SM::TILE;
+  constexpr int WAVE_TILE = GRS_WAVE * ITEMS;
+  // scatter stores a wave issues after the DMA of the next tile (full tiles)
+  constexpr int NST = ITEMS * (PAIRS ? 2 : 1);
+  static_assert(NST <= 63, "vmcnt field");
+  static_assert(RADIX <= BLOCK, "one look-back thread per digit");
+  __shared__ SM sm;
+
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = dig.max_digit();
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  const uint32_t full_tiles = n / TILE;
+
+  // tickets run ahead: at the top of an iteration on tile T_i, T_{i+1} is prefetched into
+  // LDS, thread 0 holds T_{i+2} in a register (publishes it to LDS now) and fetches
+  // T_{i+3} during the look-back
+  constexpr uint32_t TK_THREAD = BLOCK - GRS_WAVE;   // lane 0 of the last wave
+  uint32_t tk_reg = 0;
+  if (t == TK_THREAD) {
+    sm.ticket[0] = atomicAdd(ticket, 1u);
+    sm.ticket[1] = atomicAdd(ticket, 1u);
+    tk_reg = atomicAdd(ticket, 1u);
+  }
+  __syncthreads();
+  uint32_t cur = sm.ticket[0];
+  uint32_t nxt = sm.ticket[1];
+  if (cur < full_tiles) dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, cur, sm.kbuf[0], sm.vbuf[0]);
+  bool prev_full_stores = false;  // previous iteration issued NST scatter stores after its DMA
+  int b = 0;
+  const uint32_t my_hist = t < RADIX ? pass_hist[t] : 0u;  // this pass's count of digit t
+
+  while (cur < tiles) {
+    // ---- retire the DMA of `cur` (older than the previous tile's NST scatter stores) ----
+    if (prev_full_stores)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+
+    if (t == TK_THREAD) sm.ticket[2 + b] = tk_reg;   // T_{i+2}, read at the end of this iteration
+    const uint32_t tile_base = cur * TILE;
+    const bool full = cur < full_tiles;
+    const uint32_t valid = full ? TILE : n - tile_base;
+    const uint32_t pad = TILE - valid;
+    if (!full) {
+      // the ragged last tile was not prefetched: stage it through LDS in the same layout
+      // (padding = all-ones keys), so the common path below reads LDS only
+      for (uint32_t i = t; i < static_cast<uint32_t>(TILE); i += BLOCK) {
+        sm.kbuf[b][i] = i < valid ? keys_in[tile_base + i] : static_cast<K>(~static_cast<K>(0));
+        if constexpr (PAIRS) sm.vbuf[b][i] = i < valid ? vals_in[tile_base + i] : 0u;
+      }
+      lds_barrier();
+    }
+    K key[ITEMS];
+    uint32_t val[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) key[j] = sm.kbuf[b][w * WAVE_TILE + j * GRS_WAVE + lane];
+    if constexpr (PAIRS) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) val[j] = sm.vbuf[b][w * WAVE_TILE + j * GRS_WAVE + lane];
+    }
+
+    uint32_t* my_status = status + static_cast<size_t>(cur) * RADIX + t;
+    for (uint32_t i = t; i < WAVES * RADIX; i += BLOCK) sm.cnt[i] = 0;
+    if (t < RADIX) sm.hist[t] = 0;
+    if (t < RADIX) status_next[static_cast<size_t>(cur) * RADIX + t] = 0;
+    uint32_t rank[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) rank[j] = dig(key[j]) << 16;
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) atomicAdd(&sm.hist[rank[j] >> 16], 1u);
+    lds_barrier();
+
+    const uint32_t tile_cnt = t < RADIX ? sm.hist[t] : 0u;
+    const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
+    if (t < RADIX)
+      st_status(my_status, ((cur == 0 ? GRS_FLAG_INCLUSIVE : GRS_FLAG_AGGREGATE) << GRS_FLAG_SHIFT) | publish);
+    uint64_t packed = 0;
+    if (t < RADIX) packed = (static_cast<uint64_t>(my_hist) << 32) | tile_cnt;
+    const uint64_t incl = wave_incl_scan(packed, lane);
+    if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
+    lds_barrier();
+    uint64_t carry = 0;
+    for (uint32_t ww = 0; ww < w; ++ww) carry += sm.wsum[ww];
+    const uint64_t excl = carry + incl - packed;
+    // T_{i+3}, used one iteration later; fetched by the last wave, which does no look-back
+    // (RADIX <= BLOCK - 64) or looks back last, so the atomic's wait costs nobody time
+    if (t == TK_THREAD) tk_reg = atomicAdd(ticket, 1u);
+    if (t < RADIX) {
+      uint32_t prefix = 0;
+      if (cur != 0) {
+        prefix = lookback<RADIX>(status, cur, t, error_word);
+        st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
+      }
+      sm.base[t] = static_cast<uint32_t>(excl >> 32) + prefix - static_cast<uint32_t>(excl);
+      sm.hist[t] = static_cast<uint32_t>(excl);  // tile-local start of digit t
+    }
+    // ---- prefetch the next tile into the other buffer ----
+    const bool nxt_full = nxt < full_tiles;
+    if (nxt_full) dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
+
+    // ---- stable rank inside the wave ----
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t d = rank[j] >> 16;
+      const uint64_t m = match_digit<RB>(d);
+      const uint32_t below = mbcnt64(m);
+      uint32_t* c = &sm.cnt[w * RADIX + d];
+      const uint32_t old = *c;
+      if (below == 0) atomicAdd(c, static_cast<uint32_t>(__popcll(m)));
+      rank[j] |= old + below;
+    }
+    lds_barrier();
+    if (t < RADIX) {
+      uint32_t run = sm.hist[t];
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) {
+        const uint32_t c = sm.cnt[ww * RADIX + t];
+        sm.cnt[ww * RADIX + t] = run;
+        run += c;
+      }
+    }
+    lds_barrier();
+    // reorder into the current tile's buffer (its keys are in registers now)
+    K* kr = sm.kbuf[b];
+    uint32_t* vr = sm.vbuf[PAIRS ? b : 0];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t d = rank[j] >> 16;
+      const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
+      kr[pos] = key[j];
+      if constexpr (PAIRS) vr[pos] = val[j];
+    }
+    lds_barrier();
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t i = k * BLOCK + t;
+        const K kk = kr[i];
+        const uint32_t dst = sm.base[dig(kk)] + i;
+        keys_out[dst] = kk;
+        if constexpr (PAIRS) vals_out[dst] = vr[i];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t i = k * BLOCK + t;
+        if (i < valid) {
+          const K kk = kr[i];
+          const uint32_t dst = sm.base[dig(kk)] + i;
+          keys_out[dst] = kk;
+          if constexpr (PAIRS) vals_out[dst] = vr[i];
+        }
+      }
+    }
+    prev_full_stores = full && nxt_full;
+    // ---- advance: next = prefetched tile; the ticket after it was stored two slots on ----
+    lds_barrier();   // every read of kr / base / ticket of this iteration is done
+    cur = nxt;
+    nxt = sm.ticket[2 + b];
+    b ^= 1;
   }
 }
 

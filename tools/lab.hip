@@ -14,6 +14,7 @@ __global__ void copy_x4(const uint4* __restrict__ in, uint4* __restrict__ out, u
 }
 
 int g_persist_grid = 0;
+int g_stream = 0;
 
 template <typename K, bool PAIRS, int BLOCK, int ITEMS, int DBG>
 void launch(const void* in, void* out, const uint32_t* vin, uint32_t* vout, uint32_t n,
@@ -23,7 +24,13 @@ void launch(const void* in, void* out, const uint32_t* vin, uint32_t* vout, uint
   const uint32_t tiles = (n + TILE - 1) / TILE;
   const K* ki = static_cast<const K*>(in);
   K* ko = static_cast<K*>(out);
-  if (g_persist_grid > 0)
+  if (g_stream > 0) {
+    if constexpr (DBG == 0 && ITEMS * (PAIRS ? 2 : 1) <= 63 &&
+                  sizeof(grs::StreamSmem<K, PAIRS, 8, BLOCK, ITEMS>) <= 160 * 1024)
+      hipLaunchKernelGGL((grs::grs_onesweep_stream<K, PAIRS, 8, BLOCK, ITEMS>), dim3(g_stream),
+                         dim3(BLOCK), 0, s, ki, ko, vin, vout, n, grs::RadixDigit<K>{shift, 255u},
+                         hist, ticket, st, st2, err);
+  } else if (g_persist_grid > 0)
     hipLaunchKernelGGL((grs::grs_onesweep_persistent<K, PAIRS, 8, BLOCK, ITEMS, DBG>),
                        dim3(g_persist_grid), dim3(BLOCK), 0, s, ki, ko, vin, vout, n,
                        grs::RadixDigit<K>{shift, 255u}, hist, ticket, st, st2, err);
@@ -37,7 +44,11 @@ void launch(const void* in, void* out, const uint32_t* vin, uint32_t* vout, uint
 
 extern "C" {
 
-void lab_set_persistent(int grid) { g_persist_grid = grid; }
+void lab_set_persistent(int grid) {
+  // grid > 0: register-prefetch persistent kernel; grid < 0: LDS-DMA stream kernel (-grid WGs)
+  g_persist_grid = grid > 0 ? grid : 0;
+  g_stream = grid < 0 ? -grid : 0;
+}
 
 // key (kb = 32/64), payload, block, items, dbg
 int lab_pass2(int kb, int pairs, int block, int items, int dbg, const void* in, void* out,
@@ -56,6 +67,12 @@ int lab_pass2(int kb, int pairs, int block, int items, int dbg, const void* in, 
     V(32, 0, 512, 16, 0) V(32, 0, 512, 16, 16) V(32, 0, 256, 24, 16) V(32, 0, 512, 24, 16)
     V(32, 0, 256, 32, 24) V(32, 0, 256, 32, 25) V(32, 0, 512, 16, 24) V(32, 0, 256, 32, 17)
     V(32, 0, 256, 32, 19)
+    V(32, 0, 512, 24, 0) V(32, 0, 512, 24, 8) V(32, 0, 512, 16, 1536) V(32, 0, 512, 16, 1280)
+    V(32, 0, 512, 16, 1544) V(32, 0, 512, 24, 1280) V(32, 0, 256, 16, 2048) V(32, 0, 256, 24, 1536)
+    V(32, 0, 512, 32, 0) V(32, 0, 1024, 16, 0) V(32, 0, 1024, 12, 0) V(32, 0, 512, 20, 0)
+    V(32, 0, 512, 24, 32) V(32, 0, 512, 24, 1) V(32, 0, 512, 12, 0) V(32, 0, 256, 24, 0)
+    V(32, 0, 512, 16, 1024) V(32, 0, 256, 16, 1024) V(32, 0, 256, 32, 1024)
+    V(32, 0, 512, 8, 0) V(32, 1, 512, 8, 0) V(64, 0, 512, 8, 0) V(32, 0, 256, 16, 0x8000)
     // u32 pairs
     V(32, 1, 256, 16, 16) V(32, 1, 256, 24, 16) V(32, 1, 256, 32, 16) V(32, 1, 512, 16, 16)
     V(32, 1, 512, 8, 16) V(32, 1, 256, 16, 0) V(32, 1, 256, 32, 0)

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 27)
     ap.add_argument("--lib", default="liblab.so")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="32:0:256:32:16,32:0:256:32:0")
+    ap.add_argument("--variants", default="32:0:512:24:0")
     ap.add_argument("--copy", action="store_true")
     a = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, a.lib))
@@ -52,6 +52,7 @@ def main():
     ticket = torch.zeros(4, dtype=torch.uint32, device=dev)
     max_tiles = (n + 1023) // 1024
     err = torch.zeros(64 + 8 * max_tiles + 64, dtype=torch.uint32, device=dev)
+    print("lib", a.lib)
     st = torch.zeros(max_tiles * 256, dtype=torch.uint32, device=dev)
     st2 = torch.zeros_like(st)
     torch.cuda.synchronize()
