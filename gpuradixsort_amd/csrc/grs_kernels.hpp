@@ -529,8 +529,10 @@ __device__ __forceinline__ void process_tile_lbfirst(
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) rank[j] = dig(key[j]) << 16;
   __syncthreads();
+  if constexpr ((DBG & 64) == 0) {   // lab ablation: DBG bit 6 skips the tile histogram
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) atomicAdd(&sm.hist[rank[j] >> 16], 1u);
+    for (int j = 0; j < ITEMS; ++j) atomicAdd(&sm.hist[rank[j] >> 16], 1u);
+  }
   __syncthreads();
   GRS_STAMP(1);
 
@@ -588,9 +590,11 @@ __device__ __forceinline__ void process_tile_lbfirst(
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t d = rank[j] >> 16;
-    const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
-    sm.keys[pos] = key[j];
-    if constexpr (PAIRS) sm.vals[pos] = val[j];
+    // lab ablation: DBG bit 12 drops the offset lookup (positions become wrong)
+    const uint32_t pos = ((DBG & 4096) ? 0u : sm.cnt[w * RADIX + d]) + (rank[j] & 0xFFFFu);
+    const uint32_t p2 = (DBG & 4096) ? pos % TILE : pos;
+    sm.keys[p2] = key[j];
+    if constexpr (PAIRS) sm.vals[p2] = val[j];
   }
   __syncthreads();
   GRS_STAMP(5);
@@ -599,7 +603,9 @@ __device__ __forceinline__ void process_tile_lbfirst(
     const uint32_t i = k * BLOCK + t;
     if (i < valid) {
       const K kk = sm.keys[i];
-      const uint32_t dst = sm.base[dig(kk)] + i;
+      // lab ablation: DBG bit 7 reads one uniform base instead of the digit's
+      uint32_t dst = ((DBG & 128) ? sm.base[0] : sm.base[dig(kk)]) + i;
+      if constexpr ((DBG & (1 | 128)) != 0) dst = dst < n ? dst : n - 1;
       keys_out[dst] = kk;
       if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
     }

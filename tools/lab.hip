@@ -72,7 +72,9 @@ int lab_pass2(int kb, int pairs, int block, int items, int dbg, const void* in, 
     V(32, 0, 512, 32, 0) V(32, 0, 1024, 16, 0) V(32, 0, 1024, 12, 0) V(32, 0, 512, 20, 0)
     V(32, 0, 512, 24, 32) V(32, 0, 512, 24, 1) V(32, 0, 512, 12, 0) V(32, 0, 256, 24, 0)
     V(32, 0, 512, 16, 1024) V(32, 0, 256, 16, 1024) V(32, 0, 256, 32, 1024)
-    V(32, 0, 512, 8, 0) V(32, 1, 512, 8, 0) V(64, 0, 512, 8, 0) V(32, 0, 256, 16, 0x8000)
+    V(32, 0, 512, 8, 0) V(32, 1, 512, 8, 0) V(64, 0, 512, 8, 0)
+    V(32, 0, 512, 24, 65) V(32, 0, 512, 24, 129) V(32, 0, 512, 24, 4097) V(32, 0, 512, 24, 4289)
+    V(32, 0, 512, 24, 3)
     // u32 pairs
     V(32, 1, 256, 16, 16) V(32, 1, 256, 24, 16) V(32, 1, 256, 32, 16) V(32, 1, 512, 16, 16)
     V(32, 1, 512, 8, 16) V(32, 1, 256, 16, 0) V(32, 1, 256, 32, 0)
