@@ -36,6 +36,14 @@
 #define GRS_LB_WIN 8
 #endif
 
+// Two-level look-back: tiles per group, and groups polled per group-level step.
+#ifndef GRS_LB_GROUP
+#define GRS_LB_GROUP 8
+#endif
+#ifndef GRS_LB_GWIN
+#define GRS_LB_GWIN 4
+#endif
+
 // Layout of the per-sorter control block (uint32 words), zeroed once per sort call.
 //   [0, GRS_CTRL_HIST_WORDS)           global digit histograms, [pass][radix]
 //   GRS_CTRL_TICKETS + pass            per-pass tile ticket counters

@@ -94,6 +94,12 @@ __device__ __forceinline__ void st_status(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier that drains LDS only: __syncthreads() also waits for every outstanding
+// global load (vmcnt(0)), which would drain prefetches that are meant to stay in flight.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Inclusive scan of one 64-bit value per lane across a wave.
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 #pragma unroll
@@ -267,13 +273,17 @@ struct OnesweepSmem {
 // GRS_LB_WIN predecessors at once (independent loads in flight), consumes AGGREGATEs
 // nearest-first up to the first INCLUSIVE, restarts the window at the first NOT_READY.
 // Tile 0 is always INCLUSIVE, so the walk ends; spins are bounded (error word).
-template <int RADIX>
+template <int RADIX, bool STATS = false>
 __device__ __forceinline__ uint32_t lookback(const uint32_t* status, uint32_t tile, uint32_t d,
                                              uint32_t* error_word) {
   uint32_t prefix = 0;
   int32_t pt = static_cast<int32_t>(tile) - 1;
   uint32_t spins = 0;
+  uint32_t rounds = 0, walked = 0;
+  const uint64_t t0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+  uint32_t first_rt = 0;
   while (true) {
+    ++rounds;
     uint32_t v[GRS_LB_WIN];
 #pragma unroll
     for (int k = 0; k < GRS_LB_WIN; ++k)
@@ -295,6 +305,10 @@ __device__ __forceinline__ uint32_t lookback(const uint32_t* status, uint32_t ti
         }
       }
     }
+    if constexpr (STATS) {
+      if (rounds == 1) first_rt = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t0);
+      walked += consumed;
+    }
     if (done) break;
     pt -= consumed;
     if (consumed == 0) {
@@ -305,7 +319,186 @@ __device__ __forceinline__ uint32_t lookback(const uint32_t* status, uint32_t ti
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  if constexpr (STATS) {   // lab only: per tile max rounds / spins / walk over digits, RT of digit 0
+    uint32_t* st = error_word + 64 + static_cast<size_t>(tile) * 8;
+    atomicMax(st + 0, rounds);
+    atomicMax(st + 1, spins);
+    atomicMax(st + 2, walked);
+    if (d == 0) st[3] = first_rt;
+  }
   return prefix;
+}
+
+// Two-level look-back.  With hundreds of tiles in flight and a poll round trip of 1-2 us
+// under full HBM streaming, the INCLUSIVE frontier of a plain decoupled look-back lags
+// ~100+ tiles behind the newest tile, and every tile walks that whole distance (measured:
+// 115-140 predecessor words per digit, 15-30 poll rounds, half of a tile's lifetime).  So
+// tiles are also grouped: group g = tiles [g*G, (g+1)*G).  Every tile adds
+// (1 << 24) | its digit count into the group's accumulator word gacc[g][d] (one no-return
+// atomic per digit); a word whose top byte reads G holds the complete group aggregate
+// (sum < 2^24).  The walk then covers the own group tile by tile (< G words), and earlier
+// groups one word each: the group's last tile if it is already INCLUSIVE, else the group
+// accumulator; only a group whose accumulator is still incomplete is walked tile by tile.
+// Tile words and group words are each single 32-bit values written atomically, so no
+// release/acquire ordering is needed anywhere (a poll that reads an old state just polls
+// again).
+template <int RADIX>
+__device__ __forceinline__ bool walk_tiles(const uint32_t* status, int32_t& pt, int32_t bottom,
+                                           uint32_t d, uint32_t& prefix, uint32_t& spins,
+                                           uint32_t* error_word, uint32_t& rounds) {
+  // walks tiles pt, pt-1, ... >= bottom; true = an INCLUSIVE word ended the walk
+  while (pt >= bottom) {
+    ++rounds;
+    uint32_t v[GRS_LB_WIN];
+#pragma unroll
+    for (int k = 0; k < GRS_LB_WIN; ++k)
+      v[k] = (pt - k >= bottom) ? ld_status(status + static_cast<size_t>(pt - k) * RADIX + d) : 0u;
+    int consumed = 0;
+    bool done = false, blocked = false;
+#pragma unroll
+    for (int k = 0; k < GRS_LB_WIN; ++k) {
+      if (!done && !blocked && pt - k >= bottom) {
+        const uint32_t f = v[k] >> GRS_FLAG_SHIFT;
+        if (f == GRS_FLAG_NOT_READY) {
+          blocked = true;
+        } else {
+          prefix += v[k] & GRS_VALUE_MASK;
+          ++consumed;
+          done = f == GRS_FLAG_INCLUSIVE;
+        }
+      }
+    }
+    if (done) return true;
+    pt -= consumed;
+    if (consumed == 0) {
+      if (++spins > GRS_SPIN_LIMIT) {
+        atomicOr(error_word, 1u);
+        return true;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return false;
+}
+
+template <int RADIX, int G, bool STATS = false>
+__device__ __forceinline__ uint32_t lookback2(const uint32_t* status, const uint32_t* gacc,
+                                              uint32_t tile, uint32_t d, uint32_t* error_word) {
+  uint32_t prefix = 0, spins = 0, trounds = 0, grounds = 0, fallbacks = 0;
+  const int32_t g = static_cast<int32_t>(tile / G);
+  int32_t pt = static_cast<int32_t>(tile) - 1;
+  bool fin = walk_tiles<RADIX>(status, pt, g * G, d, prefix, spins, error_word, trounds);
+  int32_t ph = g - 1;  // groups below g are full (only the last group can be ragged)
+  while (!fin && ph >= 0) {
+    ++grounds;
+    uint32_t sl[GRS_LB_GWIN], ga[GRS_LB_GWIN];
+#pragma unroll
+    for (int k = 0; k < GRS_LB_GWIN; ++k) {
+      const int32_t h = ph - k;
+      sl[k] = h >= 0 ? ld_status(status + static_cast<size_t>(h * G + G - 1) * RADIX + d) : 0u;
+      ga[k] = h >= 0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
+    }
+    int consumed = 0;
+    bool done = false, blocked = false;
+#pragma unroll
+    for (int k = 0; k < GRS_LB_GWIN; ++k) {
+      if (!done && !blocked && ph - k >= 0) {
+        if ((sl[k] >> GRS_FLAG_SHIFT) == GRS_FLAG_INCLUSIVE) {
+          prefix += sl[k] & GRS_VALUE_MASK;
+          done = true;
+        } else if ((ga[k] >> 24) == static_cast<uint32_t>(G)) {
+          prefix += ga[k] & 0xFFFFFFu;
+          ++consumed;
+        } else {
+          blocked = true;
+        }
+      }
+    }
+    if (done) break;
+    ph -= consumed;
+    if (blocked && ph >= 0) {
+      // group ph is not complete yet: walk its tiles (ends on an INCLUSIVE or at its start)
+      ++fallbacks;
+      int32_t p2 = ph * G + G - 1;
+      if (walk_tiles<RADIX>(status, p2, ph * G, d, prefix, spins, error_word, trounds)) break;
+      --ph;
+    }
+  }
+  if constexpr (STATS) {   // lab only: per tile max over digits of tile rounds / group rounds / fallbacks / spins
+    uint32_t* st = error_word + 64 + static_cast<size_t>(tile) * 8;
+    atomicMax(st + 0, trounds);
+    atomicMax(st + 1, spins);
+    atomicMax(st + 2, grounds);
+    atomicMax(st + 3, fallbacks);
+  }
+  return prefix;
+}
+
+// Three-word look-back (LB3): tiles publish AGGREGATE words only; the group accumulator
+// gacc[g][d] gathers (1 << 24) | count of every tile of group g by RETURNING atomics, and the
+// tile whose add completes it (old arrivals == tiles in the group - 1) publishes the group's
+// INCLUSIVE prefix ginc[g][d].  A tile's exclusive prefix = (aggregates of its own group's
+// earlier tiles, < G words) + (prefix of its group: ginc of an earlier group plus the complete
+// accumulators in between).  The group-level frontier advances by a whole window of groups
+// per poll round trip, and nobody waits on another tile's look-back except the group
+// completers (one per group and digit).
+template <int RADIX, int G, bool STATS = false>
+__device__ __forceinline__ uint32_t lookback3(const uint32_t* status, const uint32_t* gacc,
+                                              uint32_t* ginc, uint32_t tile, uint32_t tiles,
+                                              uint32_t d, uint32_t old, uint32_t publish,
+                                              uint32_t* error_word) {
+  uint32_t own = 0, spins = 0, trounds = 0, grounds = 0;
+  const int32_t g = static_cast<int32_t>(tile / G);
+  int32_t pt = static_cast<int32_t>(tile) - 1;
+  walk_tiles<RADIX>(status, pt, g * G, d, own, spins, error_word, trounds);  // no INCLUSIVE words
+  uint32_t gp = 0;
+  int32_t ph = g - 1;
+  while (ph >= 0) {
+    ++grounds;
+    uint32_t gi[GRS_LB_GWIN], ga[GRS_LB_GWIN];
+#pragma unroll
+    for (int k = 0; k < GRS_LB_GWIN; ++k) {
+      const int32_t h = ph - k;
+      gi[k] = h >= 0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      ga[k] = h >= 0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
+    }
+    int consumed = 0;
+    bool done = false, blocked = false;
+#pragma unroll
+    for (int k = 0; k < GRS_LB_GWIN; ++k) {
+      if (!done && !blocked && ph - k >= 0) {
+        if ((gi[k] >> GRS_FLAG_SHIFT) == GRS_FLAG_INCLUSIVE) {
+          gp += gi[k] & GRS_VALUE_MASK;
+          done = true;
+        } else if ((ga[k] >> 24) == static_cast<uint32_t>(G)) {
+          gp += ga[k] & 0xFFFFFFu;
+          ++consumed;
+        } else {
+          blocked = true;
+        }
+      }
+    }
+    if (done) break;
+    ph -= consumed;
+    if (consumed == 0) {
+      if (++spins > GRS_SPIN_LIMIT) {
+        atomicOr(error_word, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  const uint32_t in_group = min(static_cast<uint32_t>(G), tiles - static_cast<uint32_t>(g) * G);
+  if ((old >> 24) == in_group - 1)   // this tile completed the group's accumulator
+    st_status(ginc + static_cast<size_t>(g) * RADIX + d,
+              (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((gp + (old & 0xFFFFFFu) + publish) & GRS_VALUE_MASK));
+  if constexpr (STATS) {
+    uint32_t* st = error_word + 64 + static_cast<size_t>(tile) * 8;
+    atomicMax(st + 0, trounds);
+    atomicMax(st + 1, spins);
+    atomicMax(st + 2, grounds);
+  }
+  return gp + own;
 }
 
 // Diagnostic build only (DBG bit 3, tools/lab): thread 0 records s_memtime at phase
@@ -722,9 +915,6 @@ struct StreamSmem {
   alignas(16) uint32_t vbuf[PAIRS ? 2 : 1][PAIRS ? TILE : 4];
 };
 
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // One global_load_lds_dwordx4: 16 bytes per lane from `gsrc` (per lane) into LDS at
 // `lds` + 16 * lane (lds wave-uniform).  Written as inline asm on purpose: the compiler
@@ -942,6 +1132,693 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_stream(
     nxt = sm.ticket[2 + b];
     b ^= 1;
   }
+}
+
+// ----------------------------------------------------------------------------------------
+// atomic-rank onesweep pass (default path)
+// ----------------------------------------------------------------------------------------
+//
+// Ranking by ONE returning LDS atomic per key: lane l of wave w adds 1 to the wave's counter
+// of its digit with ds_add_rtn_u32 and gets back the count of that digit over the wave's
+// earlier items plus the LOWER lanes of this item.  That holds because the LDS serialises the
+// lanes of one atomic wave-instruction that hit one address in ascending lane order (gfx950
+// property, probed by tools/ldsorder.hip and checked at sorter creation by grs_probe_lds_order;
+// the library falls back to the ballot-match pass above if the probe fails).  It replaces
+// the 8-ballot match (≈40 VALU per item) with one LDS instruction per item, and the tile
+// histogram falls out of the per-wave counters (no separate atomics).
+//
+// Per tile: rank -> B1 -> per-digit wave prefix + tile count, publish AGGREGATE, block scan
+// -> B2 -> look-back (waves holding digits) -> B3 -> reorder into LDS by (digit, input order)
+// -> B4 -> zero counters for the next tile; store each digit run to its global slot.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS>
+struct ArSmem {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int TILE = BLOCK * ITEMS;
+  uint32_t cnt[WAVES * RADIX];  // per-wave digit counters -> wave start of each digit in the tile
+  uint32_t base[RADIX];         // global destination of tile position 0 of digit d
+  uint64_t wsum[WAVES];
+  uint32_t ticket[2];
+  K keys[TILE];
+  uint32_t vals[PAIRS ? TILE : 1];
+};
+
+// Steps of one tile whose keys are in registers.  Precondition: sm.cnt is zero and every
+// thread passed a barrier after that zeroing and after the previous tile's last LDS read.
+// Leaves sm.cnt zero again (zeroed after B4).  `early_hook` runs on waves without a digit to
+// look back (right after B1); `late_hook` on the look-back waves once their look-back is
+// done: the persistent kernel issues the next tile's loads there, so no look-back poll ever
+// waits behind them.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF,
+          typename Hook>
+__device__ __forceinline__ void ar_tile(ArSmem<K, PAIRS, RB, BLOCK, ITEMS>& sm,
+                                        const K (&key)[ITEMS], const uint32_t (&val)[ITEMS],
+                                        uint32_t tile, K* __restrict__ keys_out,
+                                        uint32_t* __restrict__ vals_out, uint32_t n,
+                                        const DigitF& dig, uint32_t my_hist,
+                                        uint32_t* __restrict__ status,
+                                        uint32_t* __restrict__ status_next,
+                                        uint32_t* __restrict__ error_word, const Hook& hook,
+                                        uint64_t t_begin = 0) {
+  constexpr int RADIX = 1 << RB;
+  constexpr int WAVES = BLOCK / GRS_WAVE;
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr int LB_WAVES = (RADIX + GRS_WAVE - 1) / GRS_WAVE;
+  static_assert(RADIX <= BLOCK, "one look-back thread per digit");
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = dig.max_digit();
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t pad = TILE - valid;
+  constexpr bool LB3 = (DBG & 64) != 0;
+  constexpr bool LB2 = (DBG & 32) != 0 || LB3;
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  const uint32_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
+  uint32_t* gacc = status + static_cast<size_t>(tiles) * RADIX;  // [groups][RADIX] after the tile words
+  uint32_t* ginc = gacc + static_cast<size_t>(groups) * RADIX;   // LB3: [groups][RADIX] group inclusives
+
+  GRS_STAMP(0);
+  // ---- rank: one returning LDS atomic per item (lane-ordered, see above) ----
+  uint32_t rank[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = dig(key[j]);
+    rank[j] = (d << 16) | atomicAdd(&sm.cnt[w * RADIX + d], 1u);
+  }
+  if (t < RADIX) {
+    status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
+    if (LB2 && tile % GRS_LB_GROUP == 0)
+      status_next[static_cast<size_t>(tiles) * RADIX + (tile / GRS_LB_GROUP) * RADIX + t] = 0;
+    if (LB3 && tile % GRS_LB_GROUP == 0)
+      status_next[static_cast<size_t>(tiles + groups) * RADIX + (tile / GRS_LB_GROUP) * RADIX + t] = 0;
+  }
+  lds_barrier();  // B1
+  GRS_STAMP(1);
+  if (w >= LB_WAVES) hook();
+
+  // ---- per digit: wave starts, tile count, early publish, block scan over digits ----
+  uint32_t tile_cnt = 0, gold = 0;
+  uint32_t* my_status = status + static_cast<size_t>(tile) * RADIX + t;
+  if (t < RADIX) {
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) {
+      const uint32_t c = sm.cnt[ww * RADIX + t];
+      sm.cnt[ww * RADIX + t] = tile_cnt;
+      tile_cnt += c;
+    }
+    const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
+    st_status(my_status, ((tile == 0 && !LB3 ? GRS_FLAG_INCLUSIVE : GRS_FLAG_AGGREGATE) << GRS_FLAG_SHIFT) | publish);
+    if constexpr (LB3)
+      gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / GRS_LB_GROUP) * RADIX + t,
+                                    (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr (LB2)
+      __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / GRS_LB_GROUP) * RADIX + t,
+                             (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // hi 32 bits -> global start of digit d over the pass, lo 32 bits -> start in the tile
+  const uint64_t packed = t < RADIX ? (static_cast<uint64_t>(my_hist) << 32) | tile_cnt : 0ull;
+  uint64_t excl = 0;
+  if (w < LB_WAVES) {
+    const uint64_t incl = wave_incl_scan(packed, lane);
+    if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
+    excl = incl - packed;
+  }
+  lds_barrier();  // B2
+  GRS_STAMP(2);
+  if (t < RADIX) {
+    for (uint32_t ww = 0; ww < w; ++ww) excl += sm.wsum[ww];
+    const uint32_t local_start = static_cast<uint32_t>(excl);
+    uint32_t prefix = 0;
+    if constexpr (LB3) {
+      const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
+      prefix = lookback3<RADIX, GRS_LB_GROUP, (DBG & 16) != 0>(status, gacc, ginc, tile, tiles, t,
+                                                               gold, publish, error_word);
+    } else if (tile != 0) {
+      const uint32_t publish = (t == dmask) ? tile_cnt - pad : tile_cnt;
+      if constexpr (LB2)
+        prefix = lookback2<RADIX, GRS_LB_GROUP, (DBG & 16) != 0>(status, gacc, tile, t, error_word);
+      else
+        prefix = lookback<RADIX, (DBG & 16) != 0>(status, tile, t, error_word);
+      st_status(my_status, (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix + publish) & GRS_VALUE_MASK));
+    }
+    sm.base[t] = static_cast<uint32_t>(excl >> 32) + prefix - local_start;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) sm.cnt[ww * RADIX + t] += local_start;
+  }
+  if (w < LB_WAVES) hook();
+  lds_barrier();  // B3
+  GRS_STAMP(3);
+
+  // ---- reorder the tile in LDS by (digit, input order) ----
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = rank[j] >> 16;
+    const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
+    sm.keys[pos] = key[j];
+    if constexpr (PAIRS) sm.vals[pos] = val[j];
+  }
+  lds_barrier();  // B4
+  GRS_STAMP(4);
+  for (uint32_t i = t; i < static_cast<uint32_t>(WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
+
+  // ---- store: consecutive threads write consecutive slots of each digit run ----
+  if (valid == static_cast<uint32_t>(TILE)) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const uint32_t i = k * BLOCK + t;
+      const K kk = sm.keys[i];
+      const uint32_t dst = sm.base[dig(kk)] + i;
+      keys_out[dst] = kk;
+      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const uint32_t i = k * BLOCK + t;
+      if (i < valid) {
+        const K kk = sm.keys[i];
+        const uint32_t dst = sm.base[dig(kk)] + i;
+        keys_out[dst] = kk;
+        if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+      }
+    }
+  }
+  if constexpr ((DBG & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    GRS_STAMP(5);
+  }
+}
+
+// One tile per workgroup (grid = number of tiles).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK) void grs_onesweep_ar(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  using SM = ArSmem<K, PAIRS, RB, BLOCK, ITEMS>;
+  __shared__ SM sm;
+  const uint64_t t_begin = (DBG & 8) ? __builtin_amdgcn_s_memtime() : 0;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+  for (uint32_t i = t; i < static_cast<uint32_t>(SM::WAVES * SM::RADIX); i += BLOCK) sm.cnt[i] = 0;
+  const uint32_t my_hist = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
+  __syncthreads();
+  const uint32_t tile = (DBG & 8192) ? blockIdx.x : sm.ticket[0];  // lab: DBG 8192 = no ticket
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, tile, key, val);
+  if constexpr ((DBG & 8) != 0) {   // stamp 6 = load issue done, 7 = start time
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t == 0) {
+      error_word[64 + static_cast<size_t>(tile) * 8 + 6] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);
+      error_word[64 + static_cast<size_t>(tile) * 8 + 7] = static_cast<uint32_t>(t_begin >> 8);
+    }
+  }
+  ar_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out, n, dig, my_hist,
+                                           status, status_next, error_word, NoHook(), t_begin);
+}
+
+// Persistent variant: a fixed grid loops over tickets.  The next tile's keys are loaded into
+// a second register set as soon as a wave has nothing left to poll (ar_tile's hooks), so they
+// are in flight through the current tile's look-back, reorder and stores.  A workgroup
+// processes its tickets in increasing order and so never waits on a tile it holds itself.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK) void grs_onesweep_ar_persist(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  using SM = ArSmem<K, PAIRS, RB, BLOCK, ITEMS>;
+  __shared__ SM sm;
+  constexpr uint32_t TILE = BLOCK * ITEMS;
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  const uint32_t t = threadIdx.x;
+  K ka[ITEMS], kb[ITEMS];
+  uint32_t va[ITEMS], vb[ITEMS];
+  if (t == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+  for (uint32_t i = t; i < static_cast<uint32_t>(SM::WAVES * SM::RADIX); i += BLOCK) sm.cnt[i] = 0;
+  const uint32_t my_hist = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
+  __syncthreads();
+  uint32_t cur = sm.ticket[0];
+  if (cur < tiles) load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
+  while (cur < tiles) {
+    // next ticket: written before ar_tile's B1, read by the hooks after it
+    if (t == 0) sm.ticket[1] = atomicAdd(ticket, 1u);
+    uint32_t nxt = tiles;
+    ar_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, ka, va, cur, keys_out, vals_out, n, dig, my_hist,
+                                             status, status_next, error_word, [&]() {
+                                               nxt = sm.ticket[1];
+                                               if (nxt < tiles)
+                                                 load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, nxt, kb, vb);
+                                             });
+    lds_barrier();  // counters zeroed, every LDS read of this tile done
+    if (nxt >= tiles) break;
+    if (t == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+    cur = tiles;
+    ar_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, kb, vb, nxt, keys_out, vals_out, n, dig, my_hist,
+                                             status, status_next, error_word, [&]() {
+                                               cur = sm.ticket[0];
+                                               if (cur < tiles)
+                                                 load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, cur, ka, va);
+                                             });
+    lds_barrier();
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// atomic-rank onesweep pass, one-wave vectorised two-level look-back (ar2)
+// ----------------------------------------------------------------------------------------
+//
+// As ar_tile, but everything between ranking and reordering is done by wave 0 alone, DPL
+// digits per lane (4 for 8-bit digits): column prefixes over the per-wave counters (b128 LDS
+// rows), tile counts, the AGGREGATE publish (one 16-B sc1 store per lane = 1 KB per tile in
+// one instruction), the group accumulators, the tile-local digit starts (one wave scan) and the
+// two-level look-back with 16-B sc1 polls (one load instruction per predecessor tile for all
+// 256 digits, 4x fewer than one dword per digit).  Wave 0 issues its first poll window, then
+// takes part in the reorder (which needs only tile-local offsets), then finishes the look-back;
+// the global base of each digit is needed only by the stores after the next barrier.
+template <int RADIX>
+struct LbCfg {
+  static constexpr int DPL = RADIX >= 64 ? RADIX / 64 : 1;  // digits per look-back lane
+  static constexpr int LANES = RADIX / DPL;                 // active look-back lanes
+  static_assert(DPL == 1 || DPL == 4, "look-back vector width");
+};
+
+using lb_rsrc = __amdgpu_buffer_rsrc_t;
+
+__device__ __forceinline__ lb_rsrc make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+
+// agent-coherent (sc1) vector load / store of DPL consecutive status words
+template <int DPL>
+__device__ __forceinline__ void lb_ld(lb_rsrc r, uint32_t word, uint32_t (&o)[DPL]) {
+  if constexpr (DPL == 4) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, word * 4u, 0, 16);
+    o[0] = x[0]; o[1] = x[1]; o[2] = x[2]; o[3] = x[3];
+  } else {
+    o[0] = __builtin_amdgcn_raw_buffer_load_b32(r, word * 4u, 0, 16);
+  }
+}
+template <int DPL>
+__device__ __forceinline__ void lb_st(lb_rsrc r, uint32_t word, const uint32_t (&v)[DPL]) {
+  if constexpr (DPL == 4) {
+    using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+    const v4 x = {v[0], v[1], v[2], v[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, word * 4u, 0, 16);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, word * 4u, 0, 16);
+  }
+}
+
+// Look-back state of one lane (DPL digits).  Phase 1 walks the tiles of the own group, phase 2
+// whole groups (see lookback2).  `issue` loads the first window; `finish` completes the walk.
+template <int RADIX, int DPL>
+struct Lb2 {
+  static constexpr int W = GRS_LB_WIN;
+  static constexpr int GW = GRS_LB_GWIN;
+  static constexpr int G = GRS_LB_GROUP;
+  static constexpr uint32_t ALL = (1u << DPL) - 1u;
+  uint32_t prefix[DPL];
+  uint32_t done;       // bit k: digit k complete
+  int32_t pt;          // next tile to consume (phase 1)
+  int32_t bottom;      // first tile of the own group
+  uint32_t v[W][DPL];  // window of tile words pt, pt-1, ...
+
+  __device__ __forceinline__ void issue(lb_rsrc st, uint32_t tile, uint32_t lane) {
+#pragma unroll
+    for (int k = 0; k < DPL; ++k) prefix[k] = 0;
+    done = 0;
+    pt = static_cast<int32_t>(tile) - 1;
+    bottom = static_cast<int32_t>(tile / G) * G;
+    load_window(st, lane);
+  }
+  __device__ __forceinline__ void load_window(lb_rsrc st, uint32_t lane) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      if (pt - k >= bottom) {
+        lb_ld<DPL>(st, static_cast<uint32_t>(pt - k) * RADIX + lane * DPL, v[k]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < DPL; ++e) v[k][e] = 0;
+      }
+    }
+  }
+  // consume one tile's words for the not-done digits; false = some digit NOT_READY
+  __device__ __forceinline__ bool take(const uint32_t (&x)[DPL]) {
+    bool ready = true;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e)
+      if (!(done >> e & 1u) && (x[e] >> GRS_FLAG_SHIFT) == GRS_FLAG_NOT_READY) ready = false;
+    if (!ready) return false;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) {
+      if (!(done >> e & 1u)) {
+        prefix[e] += x[e] & GRS_VALUE_MASK;
+        if ((x[e] >> GRS_FLAG_SHIFT) == GRS_FLAG_INCLUSIVE) done |= 1u << e;
+      }
+    }
+    return true;
+  }
+  // walk tiles [bottom, pt] starting from the loaded window; true = all digits done
+  __device__ __forceinline__ bool walk(lb_rsrc st, uint32_t lane, uint32_t& spins,
+                                       uint32_t* error_word) {
+    while (true) {
+      int consumed = 0;
+      bool blocked = false;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        if (!blocked && done != ALL && pt - k >= bottom) {
+          if (take(v[k])) ++consumed; else blocked = true;
+        }
+      }
+      pt -= consumed;
+      if (done == ALL) return true;
+      if (pt < bottom) return false;
+      if (consumed == 0) {
+        if (++spins > GRS_SPIN_LIMIT) {
+          atomicOr(error_word, 1u);
+          done = ALL;
+          return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      load_window(st, lane);
+    }
+  }
+  __device__ __forceinline__ void finish(lb_rsrc st, lb_rsrc ga, uint32_t lane,
+                                         uint32_t* error_word) {
+    uint32_t spins = 0;
+    if (walk(st, lane, spins, error_word)) return;
+    int32_t ph = bottom / G - 1;  // groups below the own group are full
+    while (ph >= 0 && done != ALL) {
+      uint32_t sl[GW][DPL], gv[GW][DPL];
+#pragma unroll
+      for (int k = 0; k < GW; ++k) {
+        if (ph - k >= 0) {
+          lb_ld<DPL>(st, static_cast<uint32_t>((ph - k) * G + G - 1) * RADIX + lane * DPL, sl[k]);
+          lb_ld<DPL>(ga, static_cast<uint32_t>(ph - k) * RADIX + lane * DPL, gv[k]);
+        }
+      }
+      int consumed = 0;
+      bool blocked = false;
+#pragma unroll
+      for (int k = 0; k < GW; ++k) {
+        if (!blocked && done != ALL && ph - k >= 0) {
+          bool ok = true;
+#pragma unroll
+          for (int e = 0; e < DPL; ++e)
+            if (!(done >> e & 1u) && (sl[k][e] >> GRS_FLAG_SHIFT) != GRS_FLAG_INCLUSIVE &&
+                (gv[k][e] >> 24) != static_cast<uint32_t>(G))
+              ok = false;
+          if (!ok) {
+            blocked = true;
+          } else {
+#pragma unroll
+            for (int e = 0; e < DPL; ++e) {
+              if (!(done >> e & 1u)) {
+                if ((sl[k][e] >> GRS_FLAG_SHIFT) == GRS_FLAG_INCLUSIVE) {
+                  prefix[e] += sl[k][e] & GRS_VALUE_MASK;
+                  done |= 1u << e;
+                } else {
+                  prefix[e] += gv[k][e] & 0xFFFFFFu;
+                }
+              }
+            }
+            ++consumed;
+          }
+        }
+      }
+      ph -= consumed;
+      if (blocked && ph >= 0 && done != ALL) {
+        // group ph incomplete: walk its tiles (ends on INCLUSIVE words or at its first tile)
+        pt = ph * G + G - 1;
+        bottom = ph * G;
+        load_window(st, lane);
+        if (walk(st, lane, spins, error_word)) return;
+        --ph;
+      }
+    }
+  }
+};
+
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS>
+struct Ar2Smem {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int TILE = BLOCK * ITEMS;
+  alignas(16) uint32_t cnt[WAVES * RADIX];  // per-wave digit counters -> tile positions
+  alignas(16) uint32_t base[RADIX];         // global destination of tile position 0 of digit d
+  uint32_t ticket[2];
+  K keys[TILE];
+  uint32_t vals[PAIRS ? TILE : 1];
+};
+
+// Tile body.  Precondition: sm.cnt is zero and every thread passed a barrier after that and
+// after the previous tile's last LDS read.  Leaves sm.cnt zero.  gstart[e] (wave 0, lanes <
+// LANES): global start of digit lane*DPL+e in this pass (exclusive scan of the pass histogram).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG, typename DigitF,
+          typename Hook>
+__device__ __forceinline__ void ar2_tile(Ar2Smem<K, PAIRS, RB, BLOCK, ITEMS>& sm,
+                                         const K (&key)[ITEMS], const uint32_t (&val)[ITEMS],
+                                         uint32_t tile, K* __restrict__ keys_out,
+                                         uint32_t* __restrict__ vals_out, uint32_t n,
+                                         const DigitF& dig,
+                                         const uint32_t (&gstart)[LbCfg<1 << RB>::DPL],
+                                         lb_rsrc st_r, lb_rsrc ga_r, uint32_t* __restrict__ gacc,
+                                         uint32_t* __restrict__ status_next,
+                                         uint32_t tiles, uint32_t* __restrict__ error_word,
+                                         const Hook& hook, uint64_t t_begin = 0) {
+  constexpr int RADIX = 1 << RB;
+  constexpr int WAVES = BLOCK / GRS_WAVE;
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr int DPL = LbCfg<RADIX>::DPL;
+  constexpr int LANES = LbCfg<RADIX>::LANES;
+  constexpr int G = GRS_LB_GROUP;
+  static_assert(G <= 255 && static_cast<long>(G) * TILE < (1l << 24), "group accumulator fields");
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = dig.max_digit();
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t pad = TILE - valid;
+
+  GRS_STAMP(0);
+  // ---- rank: one returning LDS atomic per item (lane-ordered) ----
+  uint32_t rank[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = dig(key[j]);
+    rank[j] = (d << 16) | atomicAdd(&sm.cnt[w * RADIX + d], 1u);
+  }
+  // zero this tile's words of the next pass's status buffer (and its group's accumulators)
+  for (uint32_t i = t; i < static_cast<uint32_t>(RADIX); i += BLOCK) {
+    status_next[static_cast<size_t>(tile) * RADIX + i] = 0;
+    if (tile % G == 0) status_next[static_cast<size_t>(tiles) * RADIX + (tile / G) * RADIX + i] = 0;
+  }
+  lds_barrier();  // B1
+  GRS_STAMP(1);
+  if (w != 0) hook();
+
+  uint32_t lstart[DPL], publish[DPL];
+  if (w == 0) {
+    uint32_t c[WAVES][DPL];
+    uint32_t tc[DPL];
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) tc[e] = 0;
+    if (lane < static_cast<uint32_t>(LANES)) {
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) {
+        if constexpr (DPL == 4) {
+          const uint4 x = *reinterpret_cast<const uint4*>(&sm.cnt[ww * RADIX + lane * 4]);
+          c[ww][0] = x.x; c[ww][1] = x.y; c[ww][2] = x.z; c[ww][3] = x.w;
+        } else {
+          c[ww][0] = sm.cnt[ww * RADIX + lane];
+        }
+#pragma unroll
+        for (int e = 0; e < DPL; ++e) tc[e] += c[ww][e];
+      }
+    }
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) {
+      publish[e] = (lane * DPL + e == dmask) ? tc[e] - pad : tc[e];
+      lsum += tc[e];
+    }
+    if (lane < static_cast<uint32_t>(LANES)) {
+      uint32_t pv[DPL];
+#pragma unroll
+      for (int e = 0; e < DPL; ++e)
+        pv[e] = ((tile == 0 ? GRS_FLAG_INCLUSIVE : GRS_FLAG_AGGREGATE) << GRS_FLAG_SHIFT) | publish[e];
+      lb_st<DPL>(st_r, tile * RADIX + lane * DPL, pv);
+      // group accumulators: (1 << 24) | count, one no-return atomic per digit
+#pragma unroll
+      for (int e = 0; e < DPL; ++e)
+        __hip_atomic_fetch_add(gacc + (tile / G) * RADIX + lane * DPL + e, (1u << 24) | publish[e],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // exclusive wave scan of the lane sums -> tile-local start of each digit
+    uint32_t incl = lsum;
+#pragma unroll
+    for (int o = 1; o < GRS_WAVE; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
+      if (lane >= static_cast<uint32_t>(o)) incl += y;
+    }
+    uint32_t run = incl - lsum;
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) {
+      lstart[e] = run;
+      run += tc[e];
+    }
+    if (lane < static_cast<uint32_t>(LANES)) {
+      uint32_t colrun[DPL];
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) colrun[e] = lstart[e];
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) {
+        if constexpr (DPL == 4) {
+          *reinterpret_cast<uint4*>(&sm.cnt[ww * RADIX + lane * 4]) =
+              make_uint4(colrun[0], colrun[1], colrun[2], colrun[3]);
+        } else {
+          sm.cnt[ww * RADIX + lane] = colrun[0];
+        }
+#pragma unroll
+        for (int e = 0; e < DPL; ++e) colrun[e] += c[ww][e];
+      }
+    }
+  }
+  lds_barrier();  // B2
+  GRS_STAMP(2);
+
+  Lb2<RADIX, DPL> lb;
+  if (w == 0 && tile != 0 && lane < static_cast<uint32_t>(LANES)) lb.issue(st_r, tile, lane);
+
+  // ---- reorder the tile in LDS by (digit, input order) ----
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = rank[j] >> 16;
+    const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
+    sm.keys[pos] = key[j];
+    if constexpr (PAIRS) sm.vals[pos] = val[j];
+  }
+
+  if (w == 0 && lane < static_cast<uint32_t>(LANES)) {
+    uint32_t prefix[DPL];
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) prefix[e] = 0;
+    if (tile != 0) {
+      lb.finish(st_r, ga_r, lane, error_word);
+      uint32_t iv[DPL];
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) {
+        prefix[e] = lb.prefix[e];
+        iv[e] = (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) | ((prefix[e] + publish[e]) & GRS_VALUE_MASK);
+      }
+      lb_st<DPL>(st_r, tile * RADIX + lane * DPL, iv);
+    }
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) sm.base[lane * DPL + e] = gstart[e] + prefix[e] - lstart[e];
+  }
+  if (w == 0) hook();
+  lds_barrier();  // B3
+  GRS_STAMP(3);
+  for (uint32_t i = t; i < static_cast<uint32_t>(WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
+
+  // ---- store: consecutive threads write consecutive slots of each digit run ----
+  if (valid == static_cast<uint32_t>(TILE)) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const uint32_t i = k * BLOCK + t;
+      const K kk = sm.keys[i];
+      const uint32_t dst = sm.base[dig(kk)] + i;
+      keys_out[dst] = kk;
+      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const uint32_t i = k * BLOCK + t;
+      if (i < valid) {
+        const K kk = sm.keys[i];
+        const uint32_t dst = sm.base[dig(kk)] + i;
+        keys_out[dst] = kk;
+        if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+      }
+    }
+  }
+  if constexpr ((DBG & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    GRS_STAMP(5);
+  }
+}
+
+// gstart for the look-back lanes of wave 0: exclusive scan of the pass histogram
+template <int RADIX>
+__device__ __forceinline__ void pass_starts(const uint32_t* __restrict__ pass_hist, uint32_t lane,
+                                            uint32_t (&gs)[LbCfg<RADIX>::DPL]) {
+  constexpr int DPL = LbCfg<RADIX>::DPL;
+  uint32_t h[DPL], s = 0;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) {
+    h[e] = lane * DPL + e < static_cast<uint32_t>(RADIX) ? pass_hist[lane * DPL + e] : 0u;
+    s += h[e];
+  }
+  uint32_t incl = s;
+#pragma unroll
+  for (int o = 1; o < GRS_WAVE; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
+  }
+  uint32_t run = incl - s;
+#pragma unroll
+  for (int e = 0; e < DPL; ++e) {
+    gs[e] = run;
+    run += h[e];
+  }
+}
+
+// One tile per workgroup (grid = number of tiles).  Status buffer layout per pass:
+// [tiles][RADIX] tile words, then [ceil(tiles / G)][RADIX] group accumulators.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK) void grs_onesweep_ar2(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  using SM = Ar2Smem<K, PAIRS, RB, BLOCK, ITEMS>;
+  constexpr int RADIX = SM::RADIX;
+  constexpr int DPL = LbCfg<RADIX>::DPL;
+  __shared__ SM sm;
+  const uint64_t t_begin = (DBG & 8) ? __builtin_amdgcn_s_memtime() : 0;
+  const uint32_t t = threadIdx.x;
+  const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
+  const uint32_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
+  if (t == 0) sm.ticket[0] = atomicAdd(ticket, 1u);
+  for (uint32_t i = t; i < static_cast<uint32_t>(SM::WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
+  uint32_t gs[DPL];
+  if (t < GRS_WAVE) pass_starts<RADIX>(pass_hist, t, gs);
+  const lb_rsrc st_r = make_rsrc(status, (tiles + groups) * RADIX * 4u);
+  const lb_rsrc ga_r = make_rsrc(status + static_cast<size_t>(tiles) * RADIX, groups * RADIX * 4u);
+  __syncthreads();
+  const uint32_t tile = sm.ticket[0];
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  load_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, n, tile, key, val);
+  ar2_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out, n, dig, gs,
+                                            st_r, ga_r, status + static_cast<size_t>(tiles) * RADIX,
+                                            status_next, tiles, error_word, NoHook(), t_begin);
 }
 
 // ----------------------------------------------------------------------------------------

@@ -89,6 +89,68 @@ int lab_pass2(int kb, int pairs, int block, int items, int dbg, const void* in, 
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// atomic-rank pass: grid 0 = one tile per workgroup, grid > 0 = persistent with that grid
+int lab_ar(int kb, int pairs, int block, int items, int dbg, int grid, const void* in, void* out,
+           const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist, uint32_t* ticket,
+           uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = ((((long)kb * 2 + pairs) * 10000 + block) * 100 + items) * 100 + dbg;
+  switch (code) {
+#define A(KB, P, B, I, D)                                                                     \
+  case ((((long)KB * 2 + P) * 10000 + B) * 100 + I) * 100 + D: {                                \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                              \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                         \
+    if (grid > 0)                                                                             \
+      hipLaunchKernelGGL((grs::grs_onesweep_ar_persist<KT, P != 0, 8, B, I, D>), dim3(grid),   \
+                         dim3(B), 0, s, (const KT*)in, (KT*)out, vin, vout, n,                \
+                         grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);       \
+    else                                                                                      \
+      hipLaunchKernelGGL((grs::grs_onesweep_ar<KT, P != 0, 8, B, I, D>), dim3(tiles), dim3(B), \
+                         0, s, (const KT*)in, (KT*)out, vin, vout, n,                         \
+                         grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);       \
+  } break;
+    A(32, 0, 512, 24, 0) A(32, 0, 512, 16, 0) A(32, 0, 512, 20, 0) A(32, 0, 512, 32, 0)
+    A(32, 0, 256, 16, 0) A(32, 0, 256, 24, 0) A(32, 0, 256, 32, 0) A(32, 0, 1024, 16, 0)
+    A(32, 0, 512, 12, 0) A(32, 0, 1024, 12, 0) A(32, 0, 512, 8, 0)
+    A(32, 1, 512, 16, 0) A(32, 1, 512, 12, 0) A(32, 1, 256, 16, 0) A(32, 1, 512, 8, 0)
+    A(64, 0, 512, 16, 0) A(64, 0, 512, 12, 0) A(64, 0, 256, 16, 0) A(64, 0, 512, 8, 0)
+    A(64, 1, 512, 8, 0) A(64, 1, 512, 12, 0) A(64, 1, 256, 12, 0)
+    A(32, 0, 512, 24, 8192) A(32, 0, 512, 16, 8192) A(32, 0, 1024, 16, 8192)
+    A(32, 0, 512, 24, 8) A(32, 0, 512, 16, 8) A(32, 0, 1024, 16, 8)
+    A(32, 0, 512, 24, 16) A(32, 0, 1024, 16, 16)
+    A(32, 0, 512, 24, 48) A(32, 0, 512, 24, 64) A(32, 0, 512, 24, 72) A(32, 0, 512, 24, 80)
+    A(32, 0, 512, 16, 64) A(32, 0, 1024, 16, 64) A(32, 0, 512, 20, 64) A(32, 0, 512, 24, 32) A(32, 0, 512, 24, 40) A(32, 0, 1024, 16, 32) A(32, 0, 512, 16, 32) A(32, 0, 512, 16, 40)
+#undef A
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ar2 (one-wave vectorised two-level look-back), one tile per workgroup
+int lab_ar2(int kb, int pairs, int block, int items, int dbg, const void* in, void* out,
+            const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist, uint32_t* ticket,
+            uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = ((((long)kb * 2 + pairs) * 10000 + block) * 100 + items) * 100 + dbg;
+  switch (code) {
+#define A(KB, P, B, I, D)                                                                     \
+  case ((((long)KB * 2 + P) * 10000 + B) * 100 + I) * 100 + D: {                                \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                              \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                         \
+    hipLaunchKernelGGL((grs::grs_onesweep_ar2<KT, P != 0, 8, B, I, D>), dim3(tiles), dim3(B),  \
+                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                           \
+                       grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);         \
+  } break;
+    A(32, 0, 512, 24, 0) A(32, 0, 512, 16, 0) A(32, 0, 512, 20, 0) A(32, 0, 1024, 16, 0)
+    A(32, 0, 512, 24, 8) A(32, 0, 512, 16, 8) A(32, 0, 256, 24, 0) A(32, 0, 256, 32, 0)
+    A(32, 1, 512, 16, 0) A(32, 1, 512, 12, 0) A(64, 0, 512, 16, 0) A(64, 0, 512, 12, 0)
+    A(64, 1, 512, 8, 0) A(64, 1, 512, 12, 0)
+#undef A
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int lab_hist(int kb, const void* in, uint32_t n, uint32_t* hist, uint32_t* clear, uint32_t cw,
              void* stream) {
   if (kb == 32)

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="32:0:512:24:0")
     ap.add_argument("--copy", action="store_true")
+    ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, a.lib))
     vp = ctypes.c_void_p
@@ -36,8 +37,10 @@ def main():
 
     variants = []
     for v in a.variants.split(","):
-        parts = [int(x) for x in v.split(":")]
-        variants.append(tuple(parts + [0] * (6 - len(parts))))
+        # "a32:..." = atomic-rank kernel (lab_ar), grid 0 = one tile per WG; "b32:..." = ar2
+        ar = 2 if v.startswith("b") else (1 if v.startswith("a") else 0)
+        parts = [int(x) for x in v.lstrip("ab").split(":")]
+        variants.append(tuple(parts + [0] * (6 - len(parts))) + (int(ar),))
     bufs = {}
     for kb in sorted({v[0] for v in variants}):
         dt = torch.uint32 if kb == 32 else torch.uint64
@@ -58,11 +61,18 @@ def main():
     torch.cuda.synchronize()
 
     def run(v):
-        kb, pairs, block, items, dbg, grid = v
+        kb, pairs, block, items, dbg, grid, ar = v
         keys, out, hist = bufs[kb]
-        L.lab_set_persistent(grid)
-        rc = L.lab_pass2(kb, pairs, block, items, dbg, P(keys), P(out), P(vin), P(vout),
-                         ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
+        if ar == 2:
+            rc = L.lab_ar2(kb, pairs, block, items, dbg, P(keys), P(out), P(vin), P(vout),
+                           ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
+        elif ar:
+            rc = L.lab_ar(kb, pairs, block, items, dbg, grid, P(keys), P(out), P(vin), P(vout),
+                          ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
+        else:
+            L.lab_set_persistent(grid)
+            rc = L.lab_pass2(kb, pairs, block, items, dbg, P(keys), P(out), P(vin), P(vout),
+                             ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
         assert rc == 0, (v, rc)
 
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -86,6 +96,28 @@ def main():
             torch.cuda.synchronize()
             copy_t.append(e0.elapsed_time(e1))
     print(f"n={n}  error word={int(err[0].item())}")
+    if a.check:
+        # one pass = stable partition by the low 8 bits: compare with torch's stable sort
+        for v in variants:
+            if v[4] & ~96:
+                continue
+            kb, pairs = v[0], v[1]
+            keys, out, hist = bufs[kb]
+            st.zero_()
+            ticket.zero_()
+            err.zero_()
+            run(v)
+            torch.cuda.synchronize()
+            k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
+            dig = k64 & 255
+            _, idx = torch.sort(dig, stable=True)
+            ok = torch.equal(out.view(k64.dtype if kb == 64 else torch.int32).to(torch.int64)
+                             if kb == 32 else out.view(torch.int64), k64[idx])
+            okv = (not pairs) or torch.equal(vout.to(torch.int64) if False else
+                                            vout.view(torch.int32).to(torch.int64) & 0xFFFFFFFF,
+                                            idx)
+            print(f"check {v}: keys {'OK' if ok else 'MISMATCH'} vals {'OK' if okv else 'MISMATCH'}"
+                  f" err={int(err[0].item())}")
     if copy_t:
         med = statistics.median(copy_t)
         print(f"copy x4 of n u32: median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s")
@@ -93,10 +125,27 @@ def main():
         kb, pairs = v[0], v[1]
         alg = n * 2 * (kb // 8 + (4 if pairs else 0))
         med, mn = statistics.median(times[v]), min(times[v])
-        print(f"kb={kb} pairs={pairs} block={v[2]:4d} items={v[3]:2d} dbg={v[4]:2d} grid={v[5]:4d}"
+        print(f"{['  ', 'AR', 'A2'][v[6]]} kb={kb} pairs={pairs} block={v[2]:4d} items={v[3]:2d} dbg={v[4]:2d} grid={v[5]:4d}"
               f"  median {med:8.4f} ms  min {mn:8.4f}  {alg / med / 1e6:8.1f} GB/s")
     names = ["ticket+issue", "load+hist", "p2", "p3", "p4", "reorder", "store"]
     for v in variants:
+        if v[4] & 16:
+            err.zero_()
+            st.zero_()
+            ticket.zero_()
+            run(v)
+            torch.cuda.synchronize()
+            tiles = (n + v[2] * v[3] - 1) // (v[2] * v[3])
+            a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+            if v[4] & 96:
+                print(f"lookback2 stats {v}: tile rounds mean {a_[:,0].mean():.2f} p90 {np.percentile(a_[:,0],90):.0f} max {a_[:,0].max():.0f}; "
+                      f"spins mean {a_[:,1].mean():.2f} p90 {np.percentile(a_[:,1],90):.0f}; group rounds mean {a_[:,2].mean():.2f} "
+                      f"p90 {np.percentile(a_[:,2],90):.0f} max {a_[:,2].max():.0f}; fallbacks mean {a_[:,3].mean():.2f} p90 {np.percentile(a_[:,3],90):.0f}")
+                continue
+            print(f"lookback stats {v}: rounds mean {a_[:,0].mean():.2f} p90 {np.percentile(a_[:,0],90):.0f} "
+                  f"max {a_[:,0].max():.0f}; spins mean {a_[:,1].mean():.2f} p90 {np.percentile(a_[:,1],90):.0f}; "
+                  f"walk mean {a_[:,2].mean():.1f} p90 {np.percentile(a_[:,2],90):.0f}; "
+                  f"first RT cycles mean {a_[1:,3].mean():.0f} p10 {np.percentile(a_[1:,3],10):.0f} p90 {np.percentile(a_[1:,3],90):.0f}")
         if not (v[4] & 8):
             continue
         err.zero_()
@@ -106,6 +155,12 @@ def main():
         torch.cuda.synchronize()
         tiles = (n + v[2] * v[3] - 1) // (v[2] * v[3])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+        if v[6]:
+            m = a_[:, :7].mean(0)
+            print(f"stamps {v}: ticket+load={m[6]:.0f} rank+B1={m[1]-m[0]:.0f} scan+B2={m[2]-m[1]:.0f} "
+                  f"lookback+B3={m[3]-m[2]:.0f} reorder+B4={m[4]-m[3]:.0f} store+drain={m[5]-m[4]:.0f} "
+                  f"total={m[5]:.0f}  (p90 lookback {np.percentile(a_[:, 3] - a_[:, 2], 90):.0f})")
+            continue
         ph = a_[:, :7]
         d = np.diff(np.concatenate([np.zeros((tiles, 1)), ph], axis=1), axis=1)
         print(f"stamps {v}: mean cycles per phase "
