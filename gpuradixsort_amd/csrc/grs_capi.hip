@@ -11,7 +11,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/grs.h"
@@ -34,16 +36,100 @@ grs_status set_err(grs_status s, const std::string& msg) {
       return set_err(GRS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
-// Tile geometry per (key type, payload, radix).  ITEMS keys per thread, GRS_BLOCK threads.
+// Tile geometry per (key type, payload, radix) of the one-tile-per-workgroup passes (the
+// atomic-rank pass grs_onesweep_ar and the ballot-match fallback grs_onesweep_pass).
+// ITEMS keys per thread, GRS_BLOCK threads; measured on MI355X (tools/lab.py).
 template <typename K, bool PAIRS, int RB>
 struct TileCfg {
-  // measured on MI355X, 2^27 uniform keys (tools/lab.py)
   static constexpr int BLOCK = GRS_BLOCK;
   static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 8 : 16) : (PAIRS ? 16 : 24);
   static constexpr int TILE = BLOCK * ITEMS;
 };
 
+// The persistent pass grs_onesweep_v3 (u32 keys without payload): 16 waves x 16 keys, one
+// workgroup per CU (double-buffered 64 KB tiles in LDS).  Smaller v3 tiles, or v3 with a
+// payload or u64 keys (8K- or 4K-key tiles), measured 2-6x slower: a workgroup holds the
+// ticket of the tile it prefetches for a whole iteration, and with more, shorter tiles in
+// flight later tiles' look-backs wait on those held tiles.
+struct V3Cfg {
+  static constexpr int BLOCK = 1024;
+  static constexpr int ITEMS = 16;
+  static constexpr int TILE = BLOCK * ITEMS;
+};
+
 constexpr int max_tile_min() { return 2048; }  // smallest TILE over configs (sizes status)
+
+// Status words of one look-back buffer for `tiles` tiles: the larger of the one-tile passes'
+// layout (tile words + group accumulators + group INCLUSIVE words) and v3's (tile words +
+// group + 2 x supergroup words).
+size_t status_words_for(size_t tiles, size_t radix) {
+  const size_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
+  return std::max((tiles + 2 * groups) * radix, grs::hier_status_words(tiles, radix));
+}
+
+// Probe of the property the atomic-rank passes rely on: the lanes of ONE returning ds_add
+// wave-instruction that hit one LDS address get their old values in ascending lane order
+// (tools/ldsorder.hip checks it at scale).  out[0] += number of mismatching lanes.
+__global__ void grs_probe_lds_order(uint32_t* out) {
+  __shared__ uint32_t cnt[256];
+  const uint32_t lane = threadIdx.x;  // one wave
+  uint32_t bad = 0;
+  for (int pattern = 0; pattern < 6; ++pattern) {
+    for (uint32_t i = lane; i < 256; i += 64) cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t round = 0; round < 4; ++round) {
+      uint32_t d;
+      switch (pattern) {
+        case 0: d = 7; break;                                   // all lanes, one address
+        case 1: d = lane % 3; break;
+        case 2: d = (lane * 37u + round * 11u) & 255u; break;
+        case 3: d = (lane & 1) ? 5u : 37u; break;                // two addresses, one bank
+        case 4: d = (grs::splitmix64(lane * 131u + round) >> 7) & 15u; break;
+        default: d = 255u - lane / 4; break;
+      }
+      const uint32_t before = cnt[d];
+      __syncthreads();
+      uint32_t below = 0;
+      for (uint32_t l2 = 0; l2 < 64; ++l2) {
+        const uint32_t d2 = __shfl(d, l2, 64);
+        below += (l2 < lane && d2 == d) ? 1u : 0u;
+      }
+      const uint32_t old = atomicAdd(&cnt[d], 1u);
+      bad += old != before + below;
+      __syncthreads();
+    }
+  }
+  if (bad) atomicAdd(out, bad);
+}
+
+// Rank mode per device: 0 = atomic ranking (probe passed), 1 = ballot-match fallback.
+// GRS_RANK=match in the environment forces the fallback (tests cover both paths).
+int device_rank_mode(int device) {
+  static std::mutex mu;
+  static int mode[64];
+  static bool known[64];
+  const char* env = std::getenv("GRS_RANK");
+  if (env && std::strcmp(env, "match") == 0) return 1;
+  std::lock_guard<std::mutex> lock(mu);
+  if (device >= 0 && device < 64 && known[device]) return mode[device];
+  int m = 1;
+  uint32_t* d = nullptr;
+  if (hipMalloc(&d, 4) == hipSuccess) {
+    uint32_t h = 1;
+    if (hipMemset(d, 0, 4) == hipSuccess) {
+      hipLaunchKernelGGL(grs_probe_lds_order, dim3(1), dim3(64), 0, 0, d);
+      if (hipGetLastError() == hipSuccess && hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost) == hipSuccess)
+        m = h == 0 ? 0 : 1;
+    }
+    (void)hipFree(d);
+  }
+  (void)hipGetLastError();
+  if (device >= 0 && device < 64) {
+    mode[device] = m;
+    known[device] = true;
+  }
+  return m;
+}
 
 }  // namespace
 
@@ -52,6 +138,8 @@ struct grs_sorter {
   grs_key_type key_type = GRS_KEY_U32;
   int pairs = 0;
   int radix_bits = 8;
+  int rank_mode = 0;               // 0: atomic ranking (v3 / ar passes), 1: ballot-match fallback
+  int v3_grid = 0;                 // resident v3 workgroups (CUs x blocks per CU)
   size_t capacity = 0;
   void* alt_keys = nullptr;
   uint32_t* alt_vals = nullptr;
@@ -132,7 +220,22 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(capacity, 1);
   const size_t tiles = (cap + max_tile_min() - 1) / max_tile_min();
-  s->status_words = tiles * (size_t(1) << radix_bits);
+  s->status_words = status_words_for(tiles, size_t(1) << radix_bits);
+  s->rank_mode = device_rank_mode(device);
+  {
+    int cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (radix_bits == 8)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(&grs::grs_onesweep_v3<uint32_t, false, 8, V3Cfg::BLOCK, V3Cfg::ITEMS>),
+          V3Cfg::BLOCK, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(&grs::grs_onesweep_v3<uint32_t, false, 4, V3Cfg::BLOCK, V3Cfg::ITEMS>),
+          V3Cfg::BLOCK, 0);
+    (void)hipGetLastError();
+    s->v3_grid = std::max(1, cus) * std::max(1, per_cu);
+  }
   grs_status st = GRS_OK;
   auto alloc = [&](void** p, size_t bytes) {
     if (st != GRS_OK) return;
@@ -159,6 +262,8 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
 }
 
 size_t grs_scratch_bytes(const grs_sorter* s) { return s ? s->scratch_bytes : 0; }
+
+int grs_rank_mode(const grs_sorter* s) { return s ? s->rank_mode : -1; }
 
 grs_status grs_set_profiling(grs_sorter* s, int ring) {
   if (!s) return set_err(GRS_EINVAL, "grs_set_profiling: NULL sorter");
@@ -191,14 +296,27 @@ grs_status grs_set_profiling(grs_sorter* s, int ring) {
 
 namespace {
 
+// Which pass kernel a sort call launches: the persistent v3 pass for u32 keys without payload,
+// the one-tile-per-workgroup atomic-rank pass otherwise, the ballot-match pass if the LDS
+// order probe failed (or GRS_RANK=match).
+enum class PassKind { V3, AR, MATCH };
+
+template <typename K, bool PAIRS>
+PassKind pass_kind(const grs_sorter* s) {
+  if (s->rank_mode != 0) return PassKind::MATCH;
+  return (!PAIRS && sizeof(K) == 4) ? PassKind::V3 : PassKind::AR;
+}
+
 template <typename K, bool PAIRS, int RB>
 grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begin_bit,
                     int end_bit, hipStream_t stream) {
   using Cfg = TileCfg<K, PAIRS, RB>;
   constexpr int RADIX = 1 << RB;
+  const PassKind kind = pass_kind<K, PAIRS>(s);
   const int passes = (end_bit - begin_bit + RB - 1) / RB;
-  const uint32_t tiles = (n + Cfg::TILE - 1) / Cfg::TILE;
-  const size_t words = static_cast<size_t>(tiles) * RADIX;
+  const uint32_t tile = kind == PassKind::V3 ? V3Cfg::TILE : Cfg::TILE;
+  const uint32_t tiles = (n + tile - 1) / tile;
+  const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
   uint32_t* st1 = s->status + s->status_words;
@@ -235,10 +353,23 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     const int bits = std::min(RB, end_bit - shift);
     uint32_t* st_cur = (p & 1) ? st1 : st0;
     uint32_t* st_nxt = (p & 1) ? st0 : st1;
-    hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
-                       dim3(Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n,
-                       grs::RadixDigit<K>{shift, (1u << bits) - 1u}, hist + p * RADIX, tickets + p,
-                       st_cur, st_nxt, err);
+    const grs::RadixDigit<K> dig{shift, (1u << bits) - 1u};
+    if (kind == PassKind::V3) {
+      if constexpr (!PAIRS && sizeof(K) == 4) {
+        const uint32_t grid = std::min<uint32_t>(tiles, static_cast<uint32_t>(s->v3_grid));
+        hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS>),
+                           dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
+                           hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+      }
+    } else if (kind == PassKind::AR) {
+      hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
+                         dim3(Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
+                         tickets + p, st_cur, st_nxt, err);
+    } else {
+      hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
+                         dim3(Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
+                         tickets + p, st_cur, st_nxt, err);
+    }
     GRS_HIP(hipGetLastError());
     if ((r = mark()) != GRS_OK) return r;
     std::swap(src, dst);
@@ -260,9 +391,9 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   return GRS_OK;
 }
 
-// Stable key-range partition: one histogram launch + one onesweep launch with a splitter
-// digit (4-bit slot, up to 16 buckets).  Buckets land contiguously in keys_out/vals_out in
-// bucket order; bucket sizes are copied to d_counts[0..count].
+// Stable key-range partition: one histogram launch + one pass with a splitter digit (4-bit
+// slot, up to 16 buckets).  Buckets land contiguously in keys_out/vals_out in bucket order;
+// bucket sizes are copied to d_counts[0..count].
 template <typename K, bool PAIRS>
 grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
                          uint32_t* vals_out, uint32_t n, const K* splitters, int count,
@@ -273,7 +404,7 @@ grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* 
   dig.count = static_cast<uint32_t>(count);
   for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) dig.s[i] = i < count ? splitters[i] : K(0);
   const uint32_t tiles = (n + Cfg::TILE - 1) / Cfg::TILE;
-  const size_t words = static_cast<size_t>(tiles) * (1u << RB);
+  const size_t words = status_words_for(tiles, 1u << RB);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* hist = s->ctrl;
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
@@ -282,11 +413,18 @@ grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* 
                      dim3(GRS_HIST_BLOCK), 0, stream, keys, n, dig, hist, s->status,
                      static_cast<uint32_t>(words));
   GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
+  if (s->rank_mode == 0)
+    hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
                                              grs::SplitterDigit<K>>),
-                     dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
-                     dig, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
-                     s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
+                       dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
+                       dig, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
+                       s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
+  else
+    hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
+                                               grs::SplitterDigit<K>>),
+                       dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
+                       dig, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
+                       s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
   GRS_HIP(hipGetLastError());
   GRS_HIP(hipMemcpyAsync(d_counts, hist, (count + 1) * 4, hipMemcpyDeviceToDevice, stream));
   return GRS_OK;

@@ -41,7 +41,7 @@
 #define GRS_LB_GROUP 8
 #endif
 #ifndef GRS_LB_GWIN
-#define GRS_LB_GWIN 4
+#define GRS_LB_GWIN 8
 #endif
 
 // Layout of the per-sorter control block (uint32 words), zeroed once per sort call.

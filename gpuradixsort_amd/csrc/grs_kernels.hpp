@@ -921,12 +921,16 @@ struct StreamSmem {
 // does not track the DMA, so it inserts no vmcnt(0) in front of unrelated LDS reads (which
 // would drain the prefetch); the kernel retires it with its own counted s_waitcnt.
 __device__ __forceinline__ void lds_dma16(const void* gsrc, void* lds) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+  // M0 is compiler-reserved: set and restore it inside the statement that uses it
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-               :
-               : "s"(m0), "v"(gsrc)
-               : "memory", "m0");
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(dst)
+      : "memory");
 }
 
 // HBM -> LDS copy of one full tile (keys, and payload), 1 KiB per wave instruction.
@@ -1192,7 +1196,10 @@ __device__ __forceinline__ void ar_tile(ArSmem<K, PAIRS, RB, BLOCK, ITEMS>& sm,
   const uint32_t tile_base = tile * TILE;
   const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
   const uint32_t pad = TILE - valid;
-  constexpr bool LB3 = (DBG & 64) != 0;
+  // look-back: LB3 (group accumulators + group INCLUSIVE words published by the tile that
+  // completes a group) by default; lab ablations: DBG & 32 = two-level with tile INCLUSIVE
+  // chain (LB2), DBG & 2048 = the plain windowed look-back
+  constexpr bool LB3 = (DBG & (32 | 2048)) == 0;
   constexpr bool LB2 = (DBG & 32) != 0 || LB3;
   const uint32_t tiles = (n + TILE - 1) / TILE;
   const uint32_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
@@ -1819,6 +1826,420 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_ar2(
   ar2_tile<K, PAIRS, RB, BLOCK, ITEMS, DBG>(sm, key, val, tile, keys_out, vals_out, n, dig, gs,
                                             st_r, ga_r, status + static_cast<size_t>(tiles) * RADIX,
                                             status_next, tiles, error_word, NoHook(), t_begin);
+}
+
+// ----------------------------------------------------------------------------------------
+// v3 onesweep pass (the library's default): persistent workgroups, LDS-DMA double-buffered
+// tiles, ranking by lane-ordered LDS atomics, hierarchical look-back overlapped with the
+// LDS reorder
+// ----------------------------------------------------------------------------------------
+//
+// Why (tools/lab.py on MI355X, 2^27 uniform u32 keys):
+//  * ballot-match ranking costs ~40 VALU per item.  ONE returning LDS atomic per item on the
+//    wave's digit counter replaces it: the LDS serialises the lanes of one wave-instruction
+//    that hit one address in ascending lane order, so the returned count IS the stable rank
+//    (probed by tools/ldsorder.hip, and at sorter creation by grs_capi.hip, which falls back
+//    to the ballot-match pass above if the probe fails);
+//  * a tile's keys arrive ~3 us after they are requested under full streaming: the next tile
+//    is DMA'd (global_load_lds) into the second LDS buffer while the current one is processed;
+//  * a plain decoupled look-back walked 100+ predecessor words per digit: a poll round trip
+//    is 1-3 us under streaming (it queues behind the CU's own traffic) while hundreds of tiles
+//    start per round trip, so the inclusive frontier lags far behind.  HierLookback below
+//    reads < 2G + 2SW words per digit in one round.
+//
+// Status buffer of one pass (uint32 words, all zero at pass start):
+//   [tiles][R] tile AGGREGATE words, [groups][R] group accumulators,
+//   [supers][R] supergroup accumulators, [supers][R] supergroup INCLUSIVE words
+// A pass zeroes its tiles' and groups' words of the OTHER buffer for the next pass; the
+// histogram kernel zeroes the first pass's buffer.
+
+// bounded spin step: sleeps and returns true, or raises the error word and returns false
+__device__ __forceinline__ bool spin_ok(uint32_t& spins, uint32_t* error_word) {
+  if (++spins > GRS_SPIN_LIMIT) {
+    atomicOr(error_word, 1u);
+    return false;
+  }
+  __builtin_amdgcn_s_sleep(1);
+  return true;
+}
+
+// Words of one status buffer: tile words + group + 2 x supergroup words (per digit).
+__host__ __device__ constexpr size_t hier_status_words(size_t tiles, size_t radix) {
+  return (tiles + (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP +
+          2 * ((tiles + GRS_LB_GROUP * GRS_LB_GROUP - 1) / (GRS_LB_GROUP * GRS_LB_GROUP))) *
+         radix;
+}
+
+// Hierarchical look-back of one digit.  Levels: tile -> group (G tiles) -> supergroup (G*G
+// tiles).  Every tile publishes its AGGREGATE word and adds (1 << 24) | count into its
+// group's and its supergroup's accumulator (a word whose top byte reads the level's size is
+// complete; sums stay < 2^24); the add that completes a supergroup (its returned arrival
+// count = tiles in it - 1) publishes the supergroup's INCLUSIVE prefix.  The exclusive prefix
+// of tile T = (supergroups before T's: the newest published INCLUSIVE plus the complete
+// accumulators after it) + (groups of T's supergroup before T's group) + (tiles of T's
+// group before T).  Every word is one 32-bit value written atomically, so no release /
+// acquire is needed: a poll that reads an old state polls again.  `issue` sends every load of
+// the first round at once; `finish` consumes them (re-polling what is not ready yet).
+template <int RADIX>
+struct HierLookback {
+  static constexpr int G = GRS_LB_GROUP;
+  static constexpr int S = G * G;         // tiles per supergroup
+  static constexpr int SW = GRS_LB_GWIN;  // supergroups per poll window
+  // All polls are agent-coherent (sc1) buffer loads of one status buffer addressed by 32-bit
+  // word offsets: base words of each level are wave-uniform, so no 64-bit address per load
+  // stays live across the reorder that runs between `issue` and `finish`.
+  uint32_t tw[G - 1];                     // own group's earlier tile words, nearest first
+  uint32_t gw[G - 1];                     // own supergroup's earlier group accumulators
+  uint32_t si[SW], sa[SW];                // supergroup INCLUSIVE words / accumulators
+  int32_t ph;                             // next supergroup to consume
+  uint32_t ntw, ngw;
+
+  static __device__ __forceinline__ uint32_t ld(lb_rsrc r, uint32_t word) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, word * 4u, 0, 16);
+  }
+  // word offsets of the levels inside the status buffer (uniform)
+  struct Layout {
+    uint32_t gacc, sacc, sinc;
+  };
+  __device__ __forceinline__ void load_supers(lb_rsrc r, const Layout& L, uint32_t d) {
+#pragma unroll
+    for (int k = 0; k < SW; ++k) {
+      const int32_t h = ph - k;
+      si[k] = h >= 0 ? ld(r, L.sinc + static_cast<uint32_t>(h) * RADIX + d) : 0u;
+      sa[k] = h >= 0 ? ld(r, L.sacc + static_cast<uint32_t>(h) * RADIX + d) : 0u;
+    }
+  }
+  __device__ __forceinline__ void issue(lb_rsrc r, const Layout& L, uint32_t tile, uint32_t d) {
+    const uint32_t g = tile / G, s = tile / S;
+    ntw = tile - g * G;
+    ngw = g - s * G;
+#pragma unroll
+    for (int k = 0; k < G - 1; ++k) {
+      tw[k] = static_cast<uint32_t>(k) < ntw ? ld(r, (tile - 1 - k) * RADIX + d) : 0u;
+      gw[k] = static_cast<uint32_t>(k) < ngw ? ld(r, L.gacc + (g - 1 - k) * RADIX + d) : 0u;
+    }
+    ph = static_cast<int32_t>(s) - 1;
+    load_supers(r, L, d);
+  }
+  // Exclusive prefix of digit d over tiles [0, tile).  sold: the value this tile's returning
+  // add to its supergroup accumulator saw; publish: this tile's count of digit d.
+  __device__ __forceinline__ uint32_t finish(lb_rsrc r, const Layout& L, uint32_t* sinc,
+                                             uint32_t tile, uint32_t tiles, uint32_t d,
+                                             uint32_t sold, uint32_t publish,
+                                             uint32_t* error_word, uint32_t* stats = nullptr) {
+    uint32_t spins = 0, low = 0, rounds = 1;
+    const uint32_t g = tile / G;
+#pragma unroll
+    for (int k = 0; k < G - 1; ++k) {
+      if (static_cast<uint32_t>(k) < ntw) {
+        uint32_t v = tw[k];
+        while ((v >> GRS_FLAG_SHIFT) == GRS_FLAG_NOT_READY && spin_ok(spins, error_word))
+          v = ld(r, (tile - 1 - k) * RADIX + d);
+        low += v & GRS_VALUE_MASK;
+      }
+      if (static_cast<uint32_t>(k) < ngw) {
+        uint32_t v = gw[k];
+        while ((v >> 24) != static_cast<uint32_t>(G) && spin_ok(spins, error_word))
+          v = ld(r, L.gacc + (g - 1 - k) * RADIX + d);
+        low += v & 0xFFFFFFu;
+      }
+    }
+    uint32_t hi = 0;
+    while (ph >= 0) {
+      int consumed = 0;
+      bool done = false, blocked = false;
+#pragma unroll
+      for (int k = 0; k < SW; ++k) {
+        if (!done && !blocked && ph - k >= 0) {
+          if ((si[k] >> GRS_FLAG_SHIFT) == GRS_FLAG_INCLUSIVE) {
+            hi += si[k] & GRS_VALUE_MASK;
+            done = true;
+          } else if ((sa[k] >> 24) == static_cast<uint32_t>(S)) {
+            hi += sa[k] & 0xFFFFFFu;
+            ++consumed;
+          } else {
+            blocked = true;
+          }
+        }
+      }
+      if (done) break;
+      ph -= consumed;
+      if (ph < 0) break;
+      if (consumed == 0 && !spin_ok(spins, error_word)) break;
+      ++rounds;
+      load_supers(r, L, d);
+    }
+    const uint32_t s = tile / S;
+    const uint32_t in_super = min(static_cast<uint32_t>(S), tiles - s * S);
+    if ((sold >> 24) == in_super - 1)
+      st_status(sinc + static_cast<size_t>(s) * RADIX + d,
+                (GRS_FLAG_INCLUSIVE << GRS_FLAG_SHIFT) |
+                    ((hi + (sold & 0xFFFFFFu) + publish) & GRS_VALUE_MASK));
+    if (stats) {  // lab only: per tile max over digits of poll rounds / spins
+      atomicMax(stats + 0, rounds);
+      atomicMax(stats + 1, spins);
+    }
+    return hi + low;
+  }
+};
+
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS>
+struct V3Smem {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int TILE = BLOCK * ITEMS;
+  uint32_t cnt[WAVES * RADIX];  // per-wave digit counters -> tile positions
+  uint32_t base[RADIX];         // global destination of tile position 0 of digit d
+  uint32_t wsum[WAVES];
+  uint32_t ticket[2];
+  alignas(16) K kbuf[2][TILE];
+  alignas(16) uint32_t vbuf[PAIRS ? 2 : 1][PAIRS ? TILE : 4];
+};
+
+// Persistent grid (one or two workgroups per CU).  Per iteration on tile `cur` (LDS buffer b):
+//   L0   wait for this wave's DMA of `cur` (a counted vmcnt that skips the previous tile's
+//        stores), barrier; keys -> registers, wave-striped: item j of lane l of wave w is key
+//        w*64*ITEMS + j*64 + l, so ranking items in (j, lane) order is input order
+//   rank one returning ds_add per key on the wave's digit counter; take the next ticket
+//   B1   digit threads: wave starts + tile count, AGGREGATE word, group / supergroup adds,
+//        scan over digits
+//   B2   digit threads: fold the tile-local starts into the counters, issue the first
+//        look-back round; the ticket of the next tile lands
+//   B2.5 waves without a digit start the DMA of `nxt` into buffer b^1; all waves reorder the
+//        tile into buffer b by (digit, input order); digit threads finish the look-back and
+//        write the digit bases, then their waves start their part of the DMA
+//   B3   stores: consecutive threads write consecutive slots of each digit run
+// A workgroup takes tickets in increasing order and only ever waits on smaller tiles, and
+// every tile publishes its counts before waiting on anything, so the grid always progresses.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int DBG = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  using SM = V3Smem<K, PAIRS, RB, BLOCK, ITEMS>;
+  constexpr int RADIX = SM::RADIX;
+  constexpr int WAVES = SM::WAVES;
+  constexpr int TILE = SM::TILE;
+  constexpr int WAVE_TILE = GRS_WAVE * ITEMS;
+  constexpr int LB_WAVES = (RADIX + GRS_WAVE - 1) / GRS_WAVE;
+  constexpr int G = GRS_LB_GROUP;
+  constexpr int S = G * G;
+  constexpr int NST = ITEMS * (PAIRS ? 2 : 1);  // global stores a wave issues after its DMA
+  static_assert(NST <= 63, "vmcnt field");
+  static_assert(RADIX <= BLOCK && LB_WAVES < WAVES, "digit waves plus a ticket wave");
+  static_assert(S <= 255 && static_cast<long>(S) * TILE < (1l << 24), "accumulator fields");
+  __shared__ SM sm;
+
+  const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t dmask = dig.max_digit();
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  const uint32_t full_tiles = n / TILE;
+  const uint32_t groups = (tiles + G - 1) / G;
+  const uint32_t supers = (tiles + S - 1) / S;
+  uint32_t* gacc = status + static_cast<size_t>(tiles) * RADIX;
+  uint32_t* sacc = gacc + static_cast<size_t>(groups) * RADIX;
+  uint32_t* sinc = sacc + static_cast<size_t>(supers) * RADIX;
+  uint32_t* gacc_next = status_next + static_cast<size_t>(tiles) * RADIX;
+  uint32_t* sacc_next = gacc_next + static_cast<size_t>(groups) * RADIX;
+  uint32_t* sinc_next = sacc_next + static_cast<size_t>(supers) * RADIX;
+  const lb_rsrc st_r = make_rsrc(status, (tiles + groups + 2 * supers) * RADIX * 4u);
+  const typename HierLookback<RADIX>::Layout lay{tiles * RADIX, (tiles + groups) * RADIX,
+                                                 (tiles + groups + supers) * RADIX};
+  constexpr uint32_t TK_THREAD = BLOCK - GRS_WAVE;  // lane 0 of the last wave (no digit)
+
+  uint32_t tk = 0;  // TK_THREAD: ticket of the next tile (taken after ranking, lands at B2)
+  if (t == TK_THREAD) sm.ticket[0] = (DBG & 64) ? blockIdx.x : atomicAdd(ticket, 1u);
+  for (uint32_t i = t; i < static_cast<uint32_t>(WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
+  // global start of digit t in this pass: exclusive scan of the pass histogram
+  uint32_t gstart = 0;
+  {
+    const uint32_t h = t < static_cast<uint32_t>(RADIX) ? pass_hist[t] : 0u;
+    uint32_t incl = h;
+#pragma unroll
+    for (int o = 1; o < GRS_WAVE; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
+      if (lane >= static_cast<uint32_t>(o)) incl += y;
+    }
+    if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
+    __syncthreads();
+    gstart = incl - h;
+    for (uint32_t ww = 0; ww < w; ++ww) gstart += sm.wsum[ww];
+  }
+  __syncthreads();
+  uint32_t cur = sm.ticket[0];
+  if (cur < full_tiles) dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, cur, sm.kbuf[0], sm.vbuf[0]);
+  bool prev_full_stores = false;  // previous iteration issued NST stores after its DMA
+  int b = 0;
+
+#define V3_STAMP(k)                                                                        \
+  do {                                                                                     \
+    if constexpr ((DBG & 8) != 0) {                                                        \
+      if (t == 0)                                                                          \
+        error_word[64 + static_cast<size_t>(cur) * 8 + (k)] =                              \
+            static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_it);                    \
+    }                                                                                      \
+  } while (0)
+  while (cur < tiles) {
+    const uint64_t t_it = (DBG & 8) ? __builtin_amdgcn_s_memtime() : 0;
+    // ---- L0 ----
+    if (prev_full_stores)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    V3_STAMP(0);
+    const uint32_t tile_base = cur * TILE;
+    const bool full = cur < full_tiles;
+    const uint32_t valid = full ? TILE : n - tile_base;
+    const uint32_t pad = TILE - valid;
+    K* kr = sm.kbuf[b];
+    uint32_t* vr = sm.vbuf[PAIRS ? b : 0];
+    if (!full) {  // the ragged last tile: staged with plain loads, padding = all-ones keys
+      for (uint32_t i = t; i < static_cast<uint32_t>(TILE); i += BLOCK) {
+        kr[i] = i < valid ? keys_in[tile_base + i] : static_cast<K>(~static_cast<K>(0));
+        if constexpr (PAIRS) vr[i] = i < valid ? vals_in[tile_base + i] : 0u;
+      }
+      lds_barrier();
+    }
+    K key[ITEMS];
+    uint32_t val[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) key[j] = kr[w * WAVE_TILE + j * GRS_WAVE + lane];
+    if constexpr (PAIRS) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) val[j] = vr[w * WAVE_TILE + j * GRS_WAVE + lane];
+    }
+
+    // ---- rank: one returning LDS atomic per item (lane-ordered) ----
+    uint32_t rank[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t d = dig(key[j]);
+      rank[j] = (d << 16) | atomicAdd(&sm.cnt[w * RADIX + d], 1u);
+    }
+    // zero this tile's (and its group's / supergroup's) words for the next pass
+    for (uint32_t i = t; i < static_cast<uint32_t>(RADIX); i += BLOCK) {
+      status_next[static_cast<size_t>(cur) * RADIX + i] = 0;
+      if (cur % G == 0) gacc_next[static_cast<size_t>(cur / G) * RADIX + i] = 0;
+      if (cur % S == 0) {
+        sacc_next[static_cast<size_t>(cur / S) * RADIX + i] = 0;
+        sinc_next[static_cast<size_t>(cur / S) * RADIX + i] = 0;
+      }
+    }
+    // The next tile's ticket is taken only now, one iteration before that tile is counted: a
+    // tile whose ticket is held but whose counts are not published yet stalls every later
+    // tile's look-back, so tickets are never taken further ahead.
+    if (t == TK_THREAD) tk = (DBG & 64) ? cur + gridDim.x : atomicAdd(ticket, 1u);
+    lds_barrier();  // B1
+    V3_STAMP(1);
+
+    // ---- digit threads: wave starts, tile count, publish, scan over digits ----
+    uint32_t tile_cnt = 0, publish = 0, sold = 0, excl = 0;
+    if (t < static_cast<uint32_t>(RADIX)) {
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) {
+        const uint32_t c = sm.cnt[ww * RADIX + t];
+        sm.cnt[ww * RADIX + t] = tile_cnt;
+        tile_cnt += c;
+      }
+      publish = (t == dmask) ? tile_cnt - pad : tile_cnt;  // padding is ranked, never counted
+      st_status(status + static_cast<size_t>(cur) * RADIX + t,
+                (GRS_FLAG_AGGREGATE << GRS_FLAG_SHIFT) | publish);
+      __hip_atomic_fetch_add(gacc + static_cast<size_t>(cur / G) * RADIX + t, (1u << 24) | publish,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sold = __hip_atomic_fetch_add(sacc + static_cast<size_t>(cur / S) * RADIX + t,
+                                    (1u << 24) | publish, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (w < static_cast<uint32_t>(LB_WAVES)) {
+      uint32_t incl = tile_cnt;
+#pragma unroll
+      for (int o = 1; o < GRS_WAVE; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
+        if (lane >= static_cast<uint32_t>(o)) incl += y;
+      }
+      if (lane == GRS_WAVE - 1) sm.wsum[w] = incl;
+      excl = incl - tile_cnt;
+    }
+    lds_barrier();  // B2
+    V3_STAMP(2);
+
+    HierLookback<RADIX> lb;
+    uint32_t local_start = 0;
+    if (t < static_cast<uint32_t>(RADIX)) {
+      for (uint32_t ww = 0; ww < w; ++ww) excl += sm.wsum[ww];
+      local_start = excl;
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) sm.cnt[ww * RADIX + t] += local_start;
+      if constexpr ((DBG & 32) != 0) lb.issue(st_r, lay, cur, t);  // lab: in flight during the reorder
+    }
+    if (t == TK_THREAD) sm.ticket[1] = tk;  // before this wave's DMA (vmcnt accounting)
+    lds_barrier();  // B2.5
+    V3_STAMP(3);
+
+    const uint32_t nxt = sm.ticket[1];
+    const bool nxt_full = nxt < full_tiles;
+    if (w >= static_cast<uint32_t>(LB_WAVES) && nxt_full)
+      dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
+    // ---- reorder into the current buffer (its keys are in registers) ----
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t d = rank[j] >> 16;
+      const uint32_t pos = sm.cnt[w * RADIX + d] + (rank[j] & 0xFFFFu);
+      kr[pos] = key[j];
+      if constexpr (PAIRS) vr[pos] = val[j];
+    }
+    if (t < static_cast<uint32_t>(RADIX)) {
+      // issued after the reorder: overlapping it (DBG & 32) keeps 30 more VGPRs live through
+      // the reorder and spills at 4 waves per SIMD
+      if constexpr ((DBG & 32) == 0) lb.issue(st_r, lay, cur, t);
+      uint32_t* stats = (DBG & 16) ? error_word + 64 + static_cast<size_t>(cur) * 8 : nullptr;
+      const uint32_t prefix =
+          lb.finish(st_r, lay, sinc, cur, tiles, t, sold, publish, error_word, stats);
+      sm.base[t] = gstart + prefix - local_start;
+    }
+    if (w < static_cast<uint32_t>(LB_WAVES) && nxt_full)
+      dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
+    lds_barrier();  // B3
+    V3_STAMP(4);
+    for (uint32_t i = t; i < static_cast<uint32_t>(WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
+
+    // ---- store ----
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t i = k * BLOCK + t;
+        const K kk = kr[i];
+        const uint32_t dst = sm.base[dig(kk)] + i;
+        keys_out[dst] = kk;
+        if constexpr (PAIRS) vals_out[dst] = vr[i];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const uint32_t i = k * BLOCK + t;
+        if (i < valid) {
+          const K kk = kr[i];
+          const uint32_t dst = sm.base[dig(kk)] + i;
+          keys_out[dst] = kk;
+          if constexpr (PAIRS) vals_out[dst] = vr[i];
+        }
+      }
+    }
+    if constexpr ((DBG & 8) != 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      V3_STAMP(5);
+    }
+    prev_full_stores = full && nxt_full;
+    cur = nxt;
+    b ^= 1;
+  }
+#undef V3_STAMP
 }
 
 // ----------------------------------------------------------------------------------------

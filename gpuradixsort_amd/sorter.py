@@ -66,6 +66,18 @@ class RadixSorter:
     def scratch_bytes(self) -> int:
         return int(lib().grs_scratch_bytes(self._h))
 
+    @property
+    def rank_mode(self) -> str:
+        """'atomic' (lane-ordered LDS atomics, the default) or 'match' (ballot fallback)."""
+        return {0: "atomic", 1: "match"}[int(lib().grs_rank_mode(self._h))]
+
+    @property
+    def pass_kernel(self) -> str:
+        """Name of the pass kernel a sort() call launches (profiling / roofline reports)."""
+        if self.rank_mode == "match":
+            return "grs_onesweep_pass"
+        return "grs_onesweep_v3" if (self.key_bits == 32 and not self.pairs) else "grs_onesweep_ar"
+
     def _check_keys(self, keys: torch.Tensor, vals: Optional[torch.Tensor]) -> None:
         if not keys.is_cuda or not keys.is_contiguous():
             raise ValueError("keys must be a contiguous device tensor")

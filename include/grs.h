@@ -84,6 +84,11 @@ void grs_destroy(grs_sorter* s);
 /* Bytes of device scratch the sorter holds (ping-pong + look-back status + control). */
 size_t grs_scratch_bytes(const grs_sorter* s);
 
+/* Ranking used by this sorter's passes: 0 = lane-ordered LDS atomics (the default; probed on
+ * the device at grs_create), 1 = wave64 ballot-match fallback (probe failed, or the
+ * environment variable GRS_RANK=match was set at grs_create).  -1 for a NULL sorter. */
+int grs_rank_mode(const grs_sorter* s);
+
 /* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a
  * payload, d_vals[0..n) is permuted with its keys (d_vals may be NULL otherwise).
  * Replaces ParallelSort::Sort() (ParallelSort.cpp:168-422). */

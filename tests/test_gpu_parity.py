@@ -67,7 +67,10 @@ def distributions(n, kb, rng):
                           & rng.integers(0, top, n, dtype=dt, endpoint=True))
 
 
-SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 12289, 65536, 1 << 20]
+# tile edges of every pass kernel: 4096 / 8192 / 12288 (one-tile passes), 16384 (v3), and the
+# look-back group / supergroup edges (8 and 64 tiles)
+SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 12289, 16383, 16385, 65536,
+         131073, 1 << 20]
 
 
 @pytest.mark.parametrize("radix_bits", [4, 8])
@@ -99,6 +102,54 @@ def test_u64_matches_stable_sort(gpu, n, pairs, radix_bits):
         assert np.array_equal(gk, keys[perm]), f"{name}: keys differ"
         if pairs:
             assert np.array_equal(gv, perm), f"{name}: permutation differs"
+
+
+def test_rank_mode_is_atomic_on_gfx950(gpu):
+    """The LDS lane-order probe passes on MI355X, so the atomic-rank passes (v3 / ar) run."""
+    s = sorter(32, False, 8, 1 << 20)
+    assert s.rank_mode == "atomic"
+    assert s.pass_kernel == "grs_onesweep_v3"
+    assert sorter(32, True, 8, 1 << 20).pass_kernel == "grs_onesweep_ar"
+
+
+@pytest.mark.parametrize("kb,pairs", [(32, False), (32, True), (64, False), (64, True)])
+def test_group_and_supergroup_edges(gpu, kb, pairs):
+    """Sizes around the hierarchical look-back's group (8 tiles) and supergroup (64 tiles)
+    edges of every tile size; ragged last groups."""
+    rng = np.random.default_rng(kb * 10 + pairs)
+    dt = np.uint32 if kb == 32 else np.uint64
+    for n in (64 * 16384 - 1, 64 * 16384 + 16384 + 5, 8 * 12288 * 9 + 3, 8 * 8192 * 65 + 1):
+        keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        keys[::31] = keys[5]   # ties across tiles
+        perm = oracle.stable_argsort(keys)
+        gk, gv = gpu_sort(keys, pairs, 8, gpu)
+        assert np.array_equal(gk, keys[perm]), n
+        if pairs:
+            assert np.array_equal(gv, perm), n
+
+
+def test_ballot_match_fallback(gpu, monkeypatch):
+    """GRS_RANK=match forces the ballot-match pass (the path taken if the LDS order probe
+    ever fails): same bit-exact results."""
+    import gpuradixsort_amd as grs
+
+    monkeypatch.setenv("GRS_RANK", "match")
+    rng = np.random.default_rng(5)
+    for kb, pairs, rb in ((32, False, 8), (32, True, 4), (64, True, 8)):
+        dt = np.uint32 if kb == 32 else np.uint64
+        keys = rng.integers(0, np.iinfo(dt).max, 300_007, dtype=dt, endpoint=True)
+        perm = oracle.stable_argsort(keys)
+        s = grs.RadixSorter(keys.size, key_bits=kb, pairs=pairs, radix_bits=rb)
+        assert s.rank_mode == "match" and s.pass_kernel == "grs_onesweep_pass"
+        k = to_dev(keys, gpu)
+        v = to_dev(np.arange(keys.size, dtype=np.uint32), gpu) if pairs else None
+        s.sort(k, v)
+        torch.cuda.synchronize()
+        s.check_error()
+        assert np.array_equal(k.cpu().numpy(), keys[perm])
+        if pairs:
+            assert np.array_equal(v.cpu().numpy(), perm)
+        s.close()
 
 
 def test_golden_16key_kat(gpu):

@@ -2,6 +2,7 @@
 // Built by tools/Makefile into tools/liblab*.so; driven by tools/lab.py on the GPU box.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "../gpuradixsort_amd/csrc/grs_kernels.hpp"
@@ -56,6 +57,11 @@ int lab_pass2(int kb, int pairs, int block, int items, int dbg, const void* in, 
               uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   const long code = ((((long)kb * 2 + pairs) * 10000 + block) * 100 + items) * 100 + dbg;
+#ifdef LAB_MIN
+  (void)s; (void)code; (void)in; (void)out; (void)vin; (void)vout; (void)n; (void)hist;
+  (void)ticket; (void)st; (void)st2; (void)err; (void)shift;
+  return -1;
+#else
   switch (code) {
 #define V(KB, P, B, I, D)                                                                     \
   case ((((long)KB * 2 + P) * 10000 + B) * 100 + I) * 100 + D:                                  \
@@ -87,6 +93,7 @@ int lab_pass2(int kb, int pairs, int block, int items, int dbg, const void* in, 
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
+#endif
 }
 
 // atomic-rank pass: grid 0 = one tile per workgroup, grid > 0 = persistent with that grid
@@ -109,6 +116,10 @@ int lab_ar(int kb, int pairs, int block, int items, int dbg, int grid, const voi
                          0, s, (const KT*)in, (KT*)out, vin, vout, n,                         \
                          grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);       \
   } break;
+#ifdef LAB_MIN
+    A(32, 0, 512, 24, 64) A(32, 1, 512, 16, 64) A(32, 1, 512, 12, 64) A(64, 0, 512, 16, 64)
+    A(64, 0, 512, 12, 64) A(64, 1, 512, 8, 64) A(64, 1, 512, 12, 64) A(32, 0, 1024, 16, 64)
+#else
     A(32, 0, 512, 24, 0) A(32, 0, 512, 16, 0) A(32, 0, 512, 20, 0) A(32, 0, 512, 32, 0)
     A(32, 0, 256, 16, 0) A(32, 0, 256, 24, 0) A(32, 0, 256, 32, 0) A(32, 0, 1024, 16, 0)
     A(32, 0, 512, 12, 0) A(32, 0, 1024, 12, 0) A(32, 0, 512, 8, 0)
@@ -120,6 +131,7 @@ int lab_ar(int kb, int pairs, int block, int items, int dbg, int grid, const voi
     A(32, 0, 512, 24, 16) A(32, 0, 1024, 16, 16)
     A(32, 0, 512, 24, 48) A(32, 0, 512, 24, 64) A(32, 0, 512, 24, 72) A(32, 0, 512, 24, 80)
     A(32, 0, 512, 16, 64) A(32, 0, 1024, 16, 64) A(32, 0, 512, 20, 64) A(32, 0, 512, 24, 32) A(32, 0, 512, 24, 40) A(32, 0, 1024, 16, 32) A(32, 0, 512, 16, 32) A(32, 0, 512, 16, 40)
+#endif
 #undef A
     default: return -1;
   }
@@ -141,11 +153,43 @@ int lab_ar2(int kb, int pairs, int block, int items, int dbg, const void* in, vo
                        0, s, (const KT*)in, (KT*)out, vin, vout, n,                           \
                        grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);         \
   } break;
+#ifdef LAB_MIN
+    A(32, 0, 512, 24, 0)
+#else
     A(32, 0, 512, 24, 0) A(32, 0, 512, 16, 0) A(32, 0, 512, 20, 0) A(32, 0, 1024, 16, 0)
     A(32, 0, 512, 24, 8) A(32, 0, 512, 16, 8) A(32, 0, 256, 24, 0) A(32, 0, 256, 32, 0)
     A(32, 1, 512, 16, 0) A(32, 1, 512, 12, 0) A(64, 0, 512, 16, 0) A(64, 0, 512, 12, 0)
     A(64, 1, 512, 8, 0) A(64, 1, 512, 12, 0)
+#endif
 #undef A
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// v3 (library default pass): persistent grid of `grid` workgroups (0 = one per tile)
+int lab_v3(int kb, int pairs, int block, int items, int dbg, int grid, const void* in, void* out,
+           const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist, uint32_t* ticket,
+           uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = ((((long)kb * 2 + pairs) * 10000 + block) * 100 + items) * 100 + dbg;
+  switch (code) {
+#define C3(KB, P, B, I, D)                                                                    \
+  case ((((long)KB * 2 + P) * 10000 + B) * 100 + I) * 100 + D: {                               \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                             \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                        \
+    const uint32_t g = grid > 0 ? std::min<uint32_t>(grid, tiles) : tiles;                   \
+    hipLaunchKernelGGL((grs::grs_onesweep_v3<KT, P != 0, 8, B, I, D>), dim3(g), dim3(B), 0, s, \
+                       (const KT*)in, (KT*)out, vin, vout, n, grs::RadixDigit<KT>{shift, 255u}, \
+                       hist, ticket, st, st2, err);                                          \
+  } break;
+    C3(32, 0, 512, 16, 0) C3(32, 0, 512, 16, 16) C3(32, 0, 512, 12, 0) C3(32, 0, 512, 16, 32)
+    C3(32, 0, 512, 16, 48) C3(32, 0, 1024, 16, 32) C3(32, 0, 1024, 16, 8) C3(32, 0, 512, 16, 8)
+    C3(32, 0, 1024, 16, 64) C3(32, 0, 512, 16, 64) C3(32, 0, 1024, 16, 72)
+    C3(32, 0, 1024, 16, 0) C3(32, 0, 1024, 16, 16) C3(32, 0, 1024, 12, 0) C3(32, 0, 512, 8, 0)
+    C3(32, 1, 512, 8, 0) C3(32, 1, 1024, 8, 0) C3(64, 0, 512, 8, 0) C3(64, 0, 1024, 8, 0)
+    C3(64, 1, 512, 4, 0) C3(64, 1, 1024, 4, 0)
+#undef C3
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -38,8 +38,9 @@ def main():
     variants = []
     for v in a.variants.split(","):
         # "a32:..." = atomic-rank kernel (lab_ar), grid 0 = one tile per WG; "b32:..." = ar2
-        ar = 2 if v.startswith("b") else (1 if v.startswith("a") else 0)
-        parts = [int(x) for x in v.lstrip("ab").split(":")]
+        # "c32:..." = v3 (lab_v3, grid = persistent workgroups)
+        ar = {"a": 1, "b": 2, "c": 3}.get(v[0], 0)
+        parts = [int(x) for x in v.lstrip("abc").split(":")]
         variants.append(tuple(parts + [0] * (6 - len(parts))) + (int(ar),))
     bufs = {}
     for kb in sorted({v[0] for v in variants}):
@@ -63,7 +64,10 @@ def main():
     def run(v):
         kb, pairs, block, items, dbg, grid, ar = v
         keys, out, hist = bufs[kb]
-        if ar == 2:
+        if ar == 3:
+            rc = L.lab_v3(kb, pairs, block, items, dbg, grid, P(keys), P(out), P(vin), P(vout),
+                          ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
+        elif ar == 2:
             rc = L.lab_ar2(kb, pairs, block, items, dbg, P(keys), P(out), P(vin), P(vout),
                            ctypes.c_uint32(n), P(hist), P(ticket), P(st), P(st2), P(err), 0, sp)
         elif ar:
@@ -125,7 +129,7 @@ def main():
         kb, pairs = v[0], v[1]
         alg = n * 2 * (kb // 8 + (4 if pairs else 0))
         med, mn = statistics.median(times[v]), min(times[v])
-        print(f"{['  ', 'AR', 'A2'][v[6]]} kb={kb} pairs={pairs} block={v[2]:4d} items={v[3]:2d} dbg={v[4]:2d} grid={v[5]:4d}"
+        print(f"{['  ', 'AR', 'A2', 'V3'][v[6]]} kb={kb} pairs={pairs} block={v[2]:4d} items={v[3]:2d} dbg={v[4]:2d} grid={v[5]:4d}"
               f"  median {med:8.4f} ms  min {mn:8.4f}  {alg / med / 1e6:8.1f} GB/s")
     names = ["ticket+issue", "load+hist", "p2", "p3", "p4", "reorder", "store"]
     for v in variants:
@@ -137,6 +141,9 @@ def main():
             torch.cuda.synchronize()
             tiles = (n + v[2] * v[3] - 1) // (v[2] * v[3])
             a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+            if v[6] == 3:
+                print(f"v3 look-back stats {v}: rounds mean {a_[:,0].mean():.2f} p90 {np.percentile(a_[:,0],90):.0f} max {a_[:,0].max():.0f}; spins mean {a_[:,1].mean():.2f} p90 {np.percentile(a_[:,1],90):.0f} max {a_[:,1].max():.0f}")
+                continue
             if v[4] & 96:
                 print(f"lookback2 stats {v}: tile rounds mean {a_[:,0].mean():.2f} p90 {np.percentile(a_[:,0],90):.0f} max {a_[:,0].max():.0f}; "
                       f"spins mean {a_[:,1].mean():.2f} p90 {np.percentile(a_[:,1],90):.0f}; group rounds mean {a_[:,2].mean():.2f} "
@@ -155,6 +162,13 @@ def main():
         torch.cuda.synchronize()
         tiles = (n + v[2] * v[3] - 1) // (v[2] * v[3])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+        if v[6] == 3:
+            m = a_[1:, :6].mean(0)   # cycles since the iteration start at each phase end
+            d = np.diff(np.concatenate([[0.0], m]))
+            print(f"v3 stamps {v}: L0-wait={d[0]:.0f} rank+B1={d[1]:.0f} digits+B2={d[2]:.0f} "
+                  f"fold+B2.5={d[3]:.0f} reorder+lookback+B3={d[4]:.0f} store+drain={d[5]:.0f} "
+                  f"total={m[5]:.0f}")
+            continue
         if v[6]:
             m = a_[:, :7].mean(0)
             print(f"stamps {v}: ticket+load={m[6]:.0f} rank+B1={m[1]-m[0]:.0f} scan+B2={m[2]-m[1]:.0f} "
