@@ -1,8 +1,10 @@
 #!/bin/bash
-# One GPU-box session: parity tests, bench lines for every config, rocprof summary.
-# usage (via gpurun): bash tools/gpu_session.sh [tag]
+# One GPU-box session: parity tests, smoke, bench lines for every config, rocprof kernel
+# stats and PMC traffic of the headline config.
+# usage (via gpurun): bash tools/gpu_session.sh TAG [quick]
 set -u
 TAG=${1:-s}
+MODE=${2:-full}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 run() {  # name, timeout, command...
@@ -12,11 +14,16 @@ run() {  # name, timeout, command...
   echo "$name rc=$rc"
   return $rc
 }
-run pytest 900 python -m pytest tests -m gpu -q -p no:cacheprovider
-rc=$?
-[ $rc -gt 1 ] && exit $rc
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-run bench 300 python bench.py || exit $?
-for c in c2 c3 c5; do run bench_$c 300 python bench.py --config $c --steps 10 --no-cpu-baseline || exit $?; done
+if [ "$MODE" = full ]; then
+  run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 -p no:cacheprovider || exit $?
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+fi
 run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline || exit $?
+run pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o p --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline || exit $?
+run pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o p --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline || exit $?
+python3 tools/bench_pmc.py ${TAG} c4 134217728 > gpurun_out/${TAG}_pmc.log 2>&1; echo "pmc parse rc=$?"
+run bench 300 python bench.py || exit $?
+if [ "$MODE" = full ]; then
+  for c in c2 c3 c5; do run bench_$c 300 python bench.py --config $c --steps 10 --no-cpu-baseline || exit $?; done
+fi
 exit 0
