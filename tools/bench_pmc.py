@@ -45,6 +45,9 @@ def main():
         "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py --config {config} ({tag})",
     }
     json.dump(db, open(out_path, "w"), indent=1)
+    # the box's profiles/ does not travel back: a copy under gpurun_out/ is merged home
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    json.dump(db, open(os.path.join(REPO, "gpurun_out", "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(db[f"{config}:{n}"]))
 
 
