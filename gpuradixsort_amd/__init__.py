@@ -5,13 +5,18 @@ ParallelSort controller surface (amdreallyfast/GpuRadixSort).
   OriginalDataSsbo,
   ParallelSort         the reference's names and call pattern (ParallelSort.h:46-48)
   RecordSort           sort whole records by a key (K1 key hook + pair sort + K5 gather)
+  key_transform        order-preserving signed / float key bits (sort them as unsigned)
+  exclusive_scan_u32   stand-alone device-wide scan (the reference's K3a + K3b)
+  RadixSorter.sort_segmented   batched sort of independent segments
   sharded_sort         multi-GPU key-range sort: one RCCL all-to-all-v over xGMI
 
 All compute runs in libgrs.so's HIP kernels; there is no CPU fallback.
 """
 from ._lib import GRS_MAX_N, GrsError, lib
 from .parallel_sort import OriginalDataSsbo, ParallelSort, RecordSort
-from .sorter import RadixSorter, count_inversions, fill_splitmix, gather_records, iota_u32
+from .sorter import (KEYS_FLOAT, KEYS_SIGNED, KEYS_UNSIGNED, RadixSorter, count_inversions,
+                     exclusive_scan_u32, fill_splitmix, gather_records, iota_u32, key_transform)
 
 __all__ = ["GRS_MAX_N", "GrsError", "lib", "OriginalDataSsbo", "ParallelSort", "RecordSort",
-           "RadixSorter", "count_inversions", "fill_splitmix", "gather_records", "iota_u32"]
+           "RadixSorter", "count_inversions", "fill_splitmix", "gather_records", "iota_u32",
+           "key_transform", "exclusive_scan_u32", "KEYS_UNSIGNED", "KEYS_SIGNED", "KEYS_FLOAT"]

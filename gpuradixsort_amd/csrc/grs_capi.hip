@@ -154,6 +154,9 @@ struct grs_sorter {
   hipEvent_t* ev = nullptr;        // ring * EV_PER_CALL events
   struct CallInfo { int ev_used; int passes; bool copy; };
   CallInfo* info = nullptr;        // ring entries
+  // grs_sort_segmented scratch (allocated on first use, grown on demand)
+  void* seg_buf = nullptr;
+  size_t seg_bytes = 0;
 };
 
 extern "C" {
@@ -184,6 +187,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->alt_vals) (void)hipFree(s->alt_vals);
   if (s->status) (void)hipFree(s->status);
   if (s->ctrl) (void)hipFree(s->ctrl);
+  if (s->seg_buf) (void)hipFree(s->seg_buf);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   delete[] s->ev;
@@ -633,6 +637,140 @@ grs_status grs_count_inversions(const void* d_keys, size_t n, int key_bytes, uin
   if (r != GRS_OK) return set_err(r, "grs_count_inversions: HIP failure");
   *out_count = h;
   return GRS_OK;
+}
+
+grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, int inverse,
+                             void* stream) {
+  if ((key_bytes != 4 && key_bytes != 8) || kind < 0 || kind > 2)
+    return set_err(GRS_EINVAL, "grs_key_transform: bad key_bytes or kind");
+  if (n == 0 || kind == GRS_KEYS_UNSIGNED) return GRS_OK;
+  if (!d_keys) return set_err(GRS_EINVAL, "grs_key_transform: NULL keys");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (key_bytes == 4)
+    hipLaunchKernelGGL(grs::grs_key_transform<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<uint32_t*>(d_keys), static_cast<uint64_t>(n), kind, inverse);
+  else
+    hipLaunchKernelGGL(grs::grs_key_transform<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<uint64_t*>(d_keys), static_cast<uint64_t>(n), kind, inverse);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
+// Scan scratch: [0] tile ticket, [1] error word, [2..3] pad, then one 64-bit status word per
+// tile.
+static constexpr size_t kScanTile = GRS_SCAN_BLOCK * GRS_SCAN_ITEMS;
+
+size_t grs_scan_scratch_bytes(size_t n) { return 16 + 8 * ((n + kScanTile - 1) / kScanTile); }
+
+grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                  uint32_t* d_total, void* d_scratch, size_t scratch_bytes,
+                                  void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (n > GRS_SCAN_MAX_N) return set_err(GRS_ECAPACITY, "grs_exclusive_scan_u32: n too large");
+  if (n == 0) {
+    if (d_total) GRS_HIP(hipMemsetAsync(d_total, 0, 4, st));
+    return GRS_OK;
+  }
+  if (!d_in || !d_out || !d_scratch)
+    return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: NULL argument");
+  const size_t need = grs_scan_scratch_bytes(n);
+  if (scratch_bytes < need) return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: scratch too small");
+  uint32_t* ctl = static_cast<uint32_t*>(d_scratch);
+  GRS_HIP(hipMemsetAsync(ctl, 0, need, st));
+  const uint32_t tiles = static_cast<uint32_t>((n + kScanTile - 1) / kScanTile);
+  hipLaunchKernelGGL(grs::grs_scan_u32, dim3(tiles), dim3(GRS_SCAN_BLOCK), 0, st, d_in, d_out,
+                     static_cast<uint32_t>(n), reinterpret_cast<uint64_t*>(ctl + 4), ctl, d_total,
+                     ctl + 1);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
+grs_status grs_scan_check_error(const void* d_scratch, void* stream) {
+  if (!d_scratch) return set_err(GRS_EINVAL, "grs_scan_check_error: NULL scratch");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  uint32_t e = 0;
+  GRS_HIP(hipMemcpyAsync(&e, static_cast<const uint32_t*>(d_scratch) + 1, 4,
+                         hipMemcpyDeviceToHost, st));
+  GRS_HIP(hipStreamSynchronize(st));
+  return e ? set_err(GRS_ETIMEOUT, "a scan look-back spin exceeded its bound") : GRS_OK;
+}
+
+grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
+                              const uint32_t* d_offsets, int num_segments, void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL sorter");
+  if (!s->pairs)
+    return set_err(GRS_EINVAL, "grs_sort_segmented: needs a sorter created with a payload");
+  if (num_segments < 1 || !d_offsets)
+    return set_err(GRS_EINVAL, "grs_sort_segmented: bad segments");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_segmented: n exceeds capacity");
+  if (n == 0) return GRS_OK;
+  if (!d_keys) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL keys");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool u64 = s->key_type == GRS_KEY_U64;
+  const size_t kb = u64 ? 8 : 4;
+  // perm | pos | vals_out | segment keys (reused for the gathered keys), 256-B aligned parts
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t need = 3 * al(n * 4) + al(n * kb);
+  grs_status r = GRS_OK;
+  if (s->seg_bytes < need) {
+    if (s->seg_buf) (void)hipFree(s->seg_buf);
+    s->seg_buf = nullptr;
+    s->seg_bytes = 0;
+    if (hipMalloc(&s->seg_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      r = set_err(GRS_ENOMEM, "grs_sort_segmented: scratch allocation failed");
+    } else {
+      s->seg_bytes = need;
+    }
+  }
+  char* b = static_cast<char*>(s->seg_buf);
+  uint32_t* perm = reinterpret_cast<uint32_t*>(b);
+  uint32_t* pos = reinterpret_cast<uint32_t*>(b + al(n * 4));
+  uint32_t* vout = reinterpret_cast<uint32_t*>(b + 2 * al(n * 4));
+  void* segk = b + 3 * al(n * 4);
+  int segbits = 1;
+  while ((1ll << segbits) < num_segments) ++segbits;
+  const int kbits = u64 ? 64 : 32;
+  // 1. stable sort of the keys, carrying each key's input index
+  if (r == GRS_OK) r = grs_iota_u32(perm, n, 0, stream);
+  if (r == GRS_OK) r = grs_sort_bits(s, d_keys, perm, n, 0, kbits, stream);
+  // 2. segment of each sorted element; 3. stable sort by segment (key order kept inside one)
+  if (r == GRS_OK) {
+    if (u64)
+      hipLaunchKernelGGL(grs::grs_segment_ids<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                         perm, d_offsets, static_cast<uint32_t>(num_segments),
+                         static_cast<uint64_t*>(segk), static_cast<uint64_t>(n));
+    else
+      hipLaunchKernelGGL(grs::grs_segment_ids<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                         perm, d_offsets, static_cast<uint32_t>(num_segments),
+                         static_cast<uint32_t*>(segk), static_cast<uint64_t>(n));
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+  }
+  if (r == GRS_OK) r = grs_iota_u32(pos, n, 0, stream);
+  if (r == GRS_OK && num_segments > 1)
+    r = grs_sort_bits(s, segk, pos, n, 0, std::min(segbits, kbits), stream);
+  // 4. gather keys (into the segment-key buffer) and payload, then copy back
+  if (r == GRS_OK) {
+    if (u64)
+      hipLaunchKernelGGL(grs::grs_segment_gather<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0,
+                         st, static_cast<const uint64_t*>(d_keys), static_cast<uint64_t*>(segk),
+                         pos, perm, d_vals, vout, static_cast<uint64_t>(n));
+    else
+      hipLaunchKernelGGL(grs::grs_segment_gather<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0,
+                         st, static_cast<const uint32_t*>(d_keys), static_cast<uint32_t*>(segk),
+                         pos, perm, d_vals, vout, static_cast<uint64_t>(n));
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+  }
+  if (r == GRS_OK && hipMemcpyAsync(d_keys, segk, n * kb, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_segmented: copy");
+  if (r == GRS_OK && d_vals &&
+      hipMemcpyAsync(d_vals, vout, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_segmented: copy");
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
 }
 
 }  // extern "C"

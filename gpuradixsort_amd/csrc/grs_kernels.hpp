@@ -920,21 +920,30 @@ struct StreamSmem {
 // `lds` + 16 * lane (lds wave-uniform).  Written as inline asm on purpose: the compiler
 // does not track the DMA, so it inserts no vmcnt(0) in front of unrelated LDS reads (which
 // would drain the prefetch); the kernel retires it with its own counted s_waitcnt.
+template <bool NT = false>
 __device__ __forceinline__ void lds_dma16(const void* gsrc, void* lds) {
   // M0 is compiler-reserved: set and restore it inside the statement that uses it
   const uint32_t dst = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
   uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(dst)
-      : "memory");
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(dst)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(dst)
+        : "memory");
 }
 
 // HBM -> LDS copy of one full tile (keys, and payload), 1 KiB per wave instruction.
-template <typename K, bool PAIRS, int BLOCK, int ITEMS>
+template <typename K, bool PAIRS, int BLOCK, int ITEMS, bool NT = false>
 __device__ __forceinline__ void dma_tile(const K* __restrict__ keys_in,
                                          const uint32_t* __restrict__ vals_in, uint32_t tile,
                                          K* kdst, uint32_t* vdst) {
@@ -949,14 +958,14 @@ __device__ __forceinline__ void dma_tile(const K* __restrict__ keys_in,
 #pragma unroll
   for (int c = 0; c < KCH / WAVES; ++c) {
     const int ch = c * WAVES + w;
-    lds_dma16(ks + ch * 1024 + lane * 16, reinterpret_cast<char*>(kdst) + ch * 1024);
+    lds_dma16<NT>(ks + ch * 1024 + lane * 16, reinterpret_cast<char*>(kdst) + ch * 1024);
   }
   if constexpr (PAIRS) {
     const char* vs = reinterpret_cast<const char*>(vals_in + static_cast<size_t>(tile) * TILE);
 #pragma unroll
     for (int c = 0; c < VCH / WAVES; ++c) {
       const int ch = c * WAVES + w;
-      lds_dma16(vs + ch * 1024 + lane * 16, reinterpret_cast<char*>(vdst) + ch * 1024);
+      lds_dma16<NT>(vs + ch * 1024 + lane * 16, reinterpret_cast<char*>(vdst) + ch * 1024);
     }
   }
 }
@@ -1113,7 +1122,7 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_stream(
       for (int k = 0; k < ITEMS; ++k) {
         const uint32_t i = k * BLOCK + t;
         const K kk = kr[i];
-        const uint32_t dst = sm.base[dig(kk)] + i;
+        uint32_t dst = sm.base[dig(kk)] + i;
         keys_out[dst] = kk;
         if constexpr (PAIRS) vals_out[dst] = vr[i];
       }
@@ -1997,6 +2006,9 @@ struct V3Smem {
 };
 
 // Persistent grid (one or two workgroups per CU).  Per iteration on tile `cur` (LDS buffer b):
+// Tiles are DMA'd with the nontemporal policy (read once per pass; lab: 3-4 % faster pass
+// than the default policy, DBG & 128 restores it); the scatter stores keep the default
+// policy, since partial lines of neighbouring digit runs merge in L2 (nt stores: 1.8x slower).
 //   L0   wait for this wave's DMA of `cur` (a counted vmcnt that skips the previous tile's
 //        stores), barrier; keys -> registers, wave-striped: item j of lane l of wave w is key
 //        w*64*ITEMS + j*64 + l, so ranking items in (j, lane) order is input order
@@ -2053,7 +2065,13 @@ __global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
   constexpr uint32_t TK_THREAD = BLOCK - GRS_WAVE;  // lane 0 of the last wave (no digit)
 
   uint32_t tk = 0;  // TK_THREAD: ticket of the next tile (taken after ranking, lands at B2)
-  if (t == TK_THREAD) sm.ticket[0] = (DBG & 64) ? blockIdx.x : atomicAdd(ticket, 1u);
+  // lab: DBG & 512 = static XCD-chunked order (needs DBG & 1): block b of label x = b % 8
+  // walks tiles x * tpc + b / 8, + gridDim / 8, ... so consecutive tiles share an XCD
+  const uint32_t tpc = (((n + TILE - 1) / TILE) + 7) / 8;
+  const uint32_t chunk_end = min((blockIdx.x % 8 + 1) * tpc, (n + TILE - 1) / TILE);
+  if (t == TK_THREAD)
+    sm.ticket[0] = (DBG & 512) ? (blockIdx.x % 8) * tpc + blockIdx.x / 8
+                   : (DBG & 64) ? blockIdx.x : atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < static_cast<uint32_t>(WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
   // global start of digit t in this pass: exclusive scan of the pass histogram
   uint32_t gstart = 0;
@@ -2072,7 +2090,7 @@ __global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
   }
   __syncthreads();
   uint32_t cur = sm.ticket[0];
-  if (cur < full_tiles) dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, cur, sm.kbuf[0], sm.vbuf[0]);
+  if (cur < full_tiles) dma_tile<K, PAIRS, BLOCK, ITEMS, (DBG & 128) == 0>(keys_in, vals_in, cur, sm.kbuf[0], sm.vbuf[0]);
   bool prev_full_stores = false;  // previous iteration issued NST stores after its DMA
   int b = 0;
 
@@ -2134,7 +2152,9 @@ __global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
     // The next tile's ticket is taken only now, one iteration before that tile is counted: a
     // tile whose ticket is held but whose counts are not published yet stalls every later
     // tile's look-back, so tickets are never taken further ahead.
-    if (t == TK_THREAD) tk = (DBG & 64) ? cur + gridDim.x : atomicAdd(ticket, 1u);
+    if (t == TK_THREAD)
+      tk = (DBG & 512)  ? (cur + gridDim.x / 8 < chunk_end ? cur + gridDim.x / 8 : tiles)
+           : (DBG & 64) ? cur + gridDim.x : atomicAdd(ticket, 1u);
     lds_barrier();  // B1
     V3_STAMP(1);
 
@@ -2185,7 +2205,7 @@ __global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
     const uint32_t nxt = sm.ticket[1];
     const bool nxt_full = nxt < full_tiles;
     if (w >= static_cast<uint32_t>(LB_WAVES) && nxt_full)
-      dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
+      dma_tile<K, PAIRS, BLOCK, ITEMS, (DBG & 128) == 0>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
     // ---- reorder into the current buffer (its keys are in registers) ----
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
@@ -2197,14 +2217,18 @@ __global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
     if (t < static_cast<uint32_t>(RADIX)) {
       // issued after the reorder: overlapping it (DBG & 32) keeps 30 more VGPRs live through
       // the reorder and spills at 4 waves per SIMD
-      if constexpr ((DBG & 32) == 0) lb.issue(st_r, lay, cur, t);
-      uint32_t* stats = (DBG & 16) ? error_word + 64 + static_cast<size_t>(cur) * 8 : nullptr;
-      const uint32_t prefix =
-          lb.finish(st_r, lay, sinc, cur, tiles, t, sold, publish, error_word, stats);
+      uint32_t prefix;
+      if constexpr ((DBG & 1) != 0) {  // lab: no look-back (uniform-data estimate)
+        prefix = cur * static_cast<uint32_t>(TILE / RADIX);
+      } else {
+        if constexpr ((DBG & 32) == 0) lb.issue(st_r, lay, cur, t);
+        uint32_t* stats = (DBG & 16) ? error_word + 64 + static_cast<size_t>(cur) * 8 : nullptr;
+        prefix = lb.finish(st_r, lay, sinc, cur, tiles, t, sold, publish, error_word, stats);
+      }
       sm.base[t] = gstart + prefix - local_start;
     }
     if (w < static_cast<uint32_t>(LB_WAVES) && nxt_full)
-      dma_tile<K, PAIRS, BLOCK, ITEMS>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
+      dma_tile<K, PAIRS, BLOCK, ITEMS, (DBG & 128) == 0>(keys_in, vals_in, nxt, sm.kbuf[b ^ 1], sm.vbuf[PAIRS ? (b ^ 1) : 0]);
     lds_barrier();  // B3
     V3_STAMP(4);
     for (uint32_t i = t; i < static_cast<uint32_t>(WAVES * RADIX); i += BLOCK) sm.cnt[i] = 0;
@@ -2215,8 +2239,14 @@ __global__ __launch_bounds__(BLOCK, 4) void grs_onesweep_v3(
       for (int k = 0; k < ITEMS; ++k) {
         const uint32_t i = k * BLOCK + t;
         const K kk = kr[i];
-        const uint32_t dst = sm.base[dig(kk)] + i;
-        keys_out[dst] = kk;
+        uint32_t dst = sm.base[dig(kk)] + i;
+        if constexpr ((DBG & 1) != 0) dst = min(dst, n - 1);   // lab: estimated bases
+        if constexpr ((DBG & 2) != 0) dst = tile_base + i;     // lab: contiguous stores
+        if constexpr ((DBG & 256) != 0) {                       // lab: nontemporal stores
+          __builtin_nontemporal_store(kk, &keys_out[dst]);
+        } else {
+          keys_out[dst] = kk;
+        }
         if constexpr (PAIRS) vals_out[dst] = vr[i];
       }
     } else {
@@ -2288,6 +2318,190 @@ __global__ void grs_gather_records(const uint8_t* __restrict__ src, uint8_t* __r
       const uint64_t r = e / rb, c = e - r * rb;
       dst[e] = src[static_cast<uint64_t>(idx[r]) * rb + c];
     }
+  }
+}
+
+// Order-preserving key transforms (the reference supports unsigned keys
+// only, ReadMeRadixSort.txt:71-80).  kind 1 = two's-complement signed: flip the sign bit;
+// kind 2 = IEEE-754 float: negative values flip every bit, others only the sign bit, so
+// -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN as unsigned integers.  `inverse` undoes it.
+template <typename K>
+__global__ void grs_key_transform(K* __restrict__ keys, uint64_t n, int kind, int inverse) {
+  constexpr K SIGN = static_cast<K>(1) << (8 * sizeof(K) - 1);
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const K x = keys[i];
+    K y;
+    if (kind == 1) {
+      y = x ^ SIGN;
+    } else if (!inverse) {
+      y = (x & SIGN) ? static_cast<K>(~x) : static_cast<K>(x | SIGN);
+    } else {
+      y = (x & SIGN) ? static_cast<K>(x & ~SIGN) : static_cast<K>(~x);
+    }
+    keys[i] = y;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// stand-alone device-wide exclusive scan of uint32 (the reference's K3a + K3b,
+// ParallelPrefixScan.comp:41-196, as one single-pass launch)
+// ----------------------------------------------------------------------------------------
+//
+// The reference scans 1024-item groups with a Blelloch tree in shared memory (K3a) and then
+// the <= 1024 group totals in one work group (K3b), with sums wrapping mod 2^32.  Here: one
+// launch, tiles of SCAN_BLOCK x SCAN_ITEMS items taken by ticket (so a tile only waits on
+// tiles that already started); a tile publishes its aggregate, one wave looks back over up to
+// 64 predecessors per step (nearest INCLUSIVE word ends the walk), publishes its inclusive
+// prefix and writes its items.  Status words are 64-bit: [63:62] flag, [31:0] value (mod 2^32).
+// In place (in == out) is allowed: a tile reads only its own items, before writing them.
+#define GRS_SCAN_BLOCK 256
+#define GRS_SCAN_ITEMS 16
+
+__device__ __forceinline__ uint64_t ld_status64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_u32(
+    const uint32_t* in, uint32_t* out, uint32_t n,   // may alias (in place)
+    uint64_t* __restrict__ status, uint32_t* __restrict__ ticket, uint32_t* __restrict__ total,
+    uint32_t* __restrict__ error_word) {
+  constexpr int B = GRS_SCAN_BLOCK, I = GRS_SCAN_ITEMS, TILE = B * I, W = B / GRS_WAVE;
+  // items pass through LDS with one pad word per 32 (position i -> i + i / 32): the coalesced
+  // stripes (item k*B + t) and the per-thread runs (items t*I .. t*I + I-1) are both
+  // bank-conflict-free
+  __shared__ uint32_t s_tile[TILE + TILE / 32];
+  __shared__ uint32_t s_wsum[W];
+  __shared__ uint32_t s_ticket, s_excl;
+  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+  if (t == 0) s_ticket = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = s_ticket;
+  const uint32_t base = tile * TILE;
+  auto pad = [](uint32_t i) { return i + (i >> 5); };
+#pragma unroll
+  for (int k = 0; k < I; ++k) {
+    const uint32_t i = base + k * B + t;
+    s_tile[pad(k * B + t)] = i < n ? in[i] : 0u;
+  }
+  __syncthreads();
+  uint32_t x[I], sum = 0;
+#pragma unroll
+  for (int k = 0; k < I; ++k) {
+    x[k] = s_tile[pad(t * I + k)];
+    sum += x[k];
+  }
+  // block exclusive scan of the thread sums
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < GRS_WAVE; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
+  }
+  if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0, agg = 0;
+#pragma unroll
+  for (int ww = 0; ww < W; ++ww) {
+    const uint32_t ws = s_wsum[ww];
+    if (static_cast<uint32_t>(ww) < w) wbase += ws;
+    agg += ws;
+  }
+  const uint32_t thread_excl = wbase + incl - sum;
+  // publish, look back, publish the inclusive prefix
+  constexpr uint64_t AGG = static_cast<uint64_t>(GRS_FLAG_AGGREGATE) << 62;
+  constexpr uint64_t INC = static_cast<uint64_t>(GRS_FLAG_INCLUSIVE) << 62;
+  if (w == 0) {
+    uint32_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0) st_status64(&status[0], INC | agg);
+    } else {
+      if (lane == 0) st_status64(&status[tile], AGG | agg);
+      int64_t hi = static_cast<int64_t>(tile) - 1;   // newest predecessor of this window
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t p = hi - static_cast<int64_t>(lane);
+        uint64_t sw = p >= 0 ? ld_status64(&status[p]) : (INC | 0u);
+        const uint64_t incl_mask = __builtin_amdgcn_ballot_w64((sw >> 62) == GRS_FLAG_INCLUSIVE);
+        // lanes up to (and including) the nearest INCLUSIVE word, or the whole window
+        const uint32_t stop = incl_mask ? static_cast<uint32_t>(__builtin_ctzll(incl_mask)) : 63u;
+        const uint64_t not_ready = __builtin_amdgcn_ballot_w64((sw >> 62) == GRS_FLAG_NOT_READY);
+        const uint64_t need = stop == 63u ? ~0ull : ((2ull << stop) - 1ull);
+        if (not_ready & need) {
+          if (++spins > GRS_SPIN_LIMIT) {
+            if (lane == 0) atomicOr(error_word, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint32_t c = lane <= stop ? static_cast<uint32_t>(sw) : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, GRS_WAVE);
+        excl += c;
+        if (incl_mask) break;
+        hi -= GRS_WAVE;
+      }
+      if (lane == 0) st_status64(&status[tile], INC | static_cast<uint32_t>(excl + agg));
+    }
+    if (lane == 0) s_excl = excl;
+    if (lane == 0 && total != nullptr && base + TILE >= n) *total = excl + agg;
+  }
+  __syncthreads();
+  uint32_t run = s_excl + thread_excl;
+#pragma unroll
+  for (int k = 0; k < I; ++k) {
+    const uint32_t xi = x[k];
+    x[k] = run;
+    run += xi;
+  }
+  // back through LDS for coalesced stores (every thread's loads of s_tile are done: the
+  // barrier above)
+#pragma unroll
+  for (int k = 0; k < I; ++k) s_tile[pad(t * I + k)] = x[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < I; ++k) {
+    const uint32_t i = base + k * B + t;
+    if (i < n) out[i] = s_tile[pad(k * B + t)];
+  }
+}
+
+// Segmented sort helpers.  After a stable sort of the keys carrying
+// their input index perm[j], segk[j] = the segment of input element perm[j]: the largest s
+// in [0, nseg) with offsets[s] <= perm[j] (offsets: nseg + 1 non-decreasing device words,
+// offsets[0] = 0, offsets[nseg] = n).
+template <typename K>
+__global__ void grs_segment_ids(const uint32_t* __restrict__ perm,
+                                const uint32_t* __restrict__ offsets, uint32_t nseg,
+                                K* __restrict__ segk, uint64_t n) {
+  for (uint64_t j = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; j < n;
+       j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t x = perm[j];
+    uint32_t lo = 0, hi = nseg;   // invariant: offsets[lo] <= x (offsets[0] = 0), answer < hi
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (offsets[mid] <= x) lo = mid; else hi = mid;
+    }
+    segk[j] = static_cast<K>(lo);
+  }
+}
+
+// out_keys[j] = keys[pos[j]]; out_vals[j] = vals[perm[pos[j]]] (vals may be null).
+template <typename K>
+__global__ void grs_segment_gather(const K* __restrict__ keys, K* __restrict__ out_keys,
+                                   const uint32_t* __restrict__ pos,
+                                   const uint32_t* __restrict__ perm,
+                                   const uint32_t* __restrict__ vals,
+                                   uint32_t* __restrict__ out_vals, uint64_t n) {
+  for (uint64_t j = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; j < n;
+       j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t p = pos[j];
+    out_keys[j] = keys[p];
+    if (vals) out_vals[j] = vals[perm[p]];
   }
 }
 

@@ -118,6 +118,28 @@ class RadixSorter:
                                   ctypes.c_void_p(sp.ctypes.data), int(sp.size), _ptr(counts),
                                   _stream_ptr(stream)), "grs_partition")
 
+    def sort_segmented(self, keys: torch.Tensor, offsets: torch.Tensor,
+                       vals: Optional[torch.Tensor] = None, n: Optional[int] = None,
+                       stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Sort every segment [offsets[s], offsets[s+1]) of keys[:n] (and vals) on its own,
+        stably, in place (grs_sort_segmented).  offsets: device u32/i32 tensor of
+        num_segments + 1 non-decreasing entries, offsets[0] = 0, offsets[-1] = n.  Needs a
+        sorter built with pairs=True (the payload slot carries the input index)."""
+        if not self.pairs:
+            raise ValueError("sort_segmented needs a sorter created with pairs=True")
+        if not keys.is_cuda or not keys.is_contiguous() or keys.element_size() * 8 != self.key_bits:
+            raise ValueError(f"keys must be a contiguous {self.key_bits}-bit device tensor")
+        if not offsets.is_cuda or not offsets.is_contiguous() or offsets.element_size() != 4:
+            raise ValueError("offsets must be a contiguous 32-bit device tensor")
+        if vals is not None and (not vals.is_cuda or not vals.is_contiguous()
+                                 or vals.element_size() != 4):
+            raise ValueError("vals must be a contiguous 32-bit device tensor")
+        n = keys.numel() if n is None else int(n)
+        vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
+        check(lib().grs_sort_segmented(self._h, _ptr(keys), vp, n, _ptr(offsets),
+                                       offsets.numel() - 1, _stream_ptr(stream)),
+              "grs_sort_segmented")
+
     def set_profiling(self, ring: int) -> None:
         """Keep per-phase hipEvent timings of the last `ring` sort calls (0 = off)."""
         check(lib().grs_set_profiling(self._h, int(ring)), "grs_set_profiling")
@@ -162,3 +184,37 @@ def count_inversions(keys: torch.Tensor, n: Optional[int] = None, stream=None) -
     check(lib().grs_count_inversions(_ptr(keys), n, keys.element_size(), ctypes.byref(out),
                                      _stream_ptr(stream)), "grs_count_inversions")
     return int(out.value)
+
+
+KEYS_UNSIGNED, KEYS_SIGNED, KEYS_FLOAT = 0, 1, 2
+_KINDS = {torch.int32: KEYS_SIGNED, torch.int64: KEYS_SIGNED, torch.float32: KEYS_FLOAT,
+          torch.float64: KEYS_FLOAT, torch.uint32: KEYS_UNSIGNED, torch.uint64: KEYS_UNSIGNED}
+
+
+def key_transform(keys: torch.Tensor, inverse: bool = False, kind: Optional[int] = None,
+                  stream=None) -> torch.Tensor:
+    """Order-preserving bit transform in place (grs_key_transform) so signed / float keys sort
+    as unsigned: kind defaults from keys.dtype (int -> signed, float -> IEEE-754)."""
+    k = _KINDS[keys.dtype] if kind is None else int(kind)
+    check(lib().grs_key_transform(_ptr(keys), keys.numel(), keys.element_size(), k, int(inverse),
+                                  _stream_ptr(stream)), "grs_key_transform")
+    return keys
+
+
+def exclusive_scan_u32(inp: torch.Tensor, out: Optional[torch.Tensor] = None,
+                       total: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """Device-wide exclusive prefix sum of uint32 (mod 2^32), one launch (grs_exclusive_scan_u32);
+    out may be inp (in place); total (device, >= 1 word) receives the sum of all items."""
+    if inp.element_size() != 4 or not inp.is_cuda or not inp.is_contiguous():
+        raise ValueError("scan input must be a contiguous 32-bit device tensor")
+    out = torch.empty_like(inp) if out is None else out
+    n = inp.numel()
+    L = lib()
+    scratch = torch.empty(max(1, (L.grs_scan_scratch_bytes(n) + 3) // 4), dtype=torch.int32,
+                          device=inp.device)
+    tp = _ptr(total) if total is not None else ctypes.c_void_p(0)
+    check(L.grs_exclusive_scan_u32(_ptr(inp), _ptr(out), n, tp, _ptr(scratch),
+                                   scratch.numel() * 4, _stream_ptr(stream)),
+          "grs_exclusive_scan_u32")
+    check(L.grs_scan_check_error(_ptr(scratch), _stream_ptr(stream)), "grs_scan_check_error")
+    return out

@@ -140,6 +140,40 @@ grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t see
 grs_status grs_count_inversions(const void* d_keys, size_t n, int key_bytes,
                                 uint64_t* out_count, void* stream);
 
+/* ---- beyond the reference's path ---- */
+
+/* Order-preserving key transforms, so that signed and floating-point keys sort with the
+ * unsigned radix sort (the reference sorts unsigned keys only, ReadMeRadixSort.txt:71-80;
+ * its K1 key hook is OriginalDataToIntermediateData.comp:12-19,42).  kind: 0 unsigned
+ * (no-op), 1 two's-complement signed, 2 IEEE-754 (f32 / f64; -NaN < -inf < -0 < +0 < +inf <
+ * +NaN).  inverse = 0 before the sort, 1 after it.  In place, asynchronous. */
+#define GRS_KEYS_UNSIGNED 0
+#define GRS_KEYS_SIGNED 1
+#define GRS_KEYS_FLOAT 2
+grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, int inverse,
+                             void* stream);
+
+/* Stand-alone device-wide exclusive prefix sum of uint32 (sums wrap mod 2^32), the
+ * reference's K3a + K3b (ParallelPrefixScan.comp:41-196, ParallelSort.cpp:253-274) as one
+ * single-pass launch.  d_out may equal d_in.  d_total (nullable) receives the sum of all
+ * items (the reference's totalNumberOfOnes, PrefixScanBuffer.comp:37).  Scratch: device
+ * memory of grs_scan_scratch_bytes(n) bytes, owned by the caller, one call at a time. */
+#define GRS_SCAN_MAX_N 0xFFFFF000u
+size_t grs_scan_scratch_bytes(size_t n);
+grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                  uint32_t* d_total, void* d_scratch, size_t scratch_bytes,
+                                  void* stream);
+/* Synchronises on `stream`; GRS_ETIMEOUT if the last scan's look-back spin gave up. */
+grs_status grs_scan_check_error(const void* d_scratch, void* stream);
+
+/* Segmented (batched) stable sort: every segment [off[s], off[s+1]) of d_keys[0..n) is
+ * sorted on its own, with d_vals (nullable) permuted alike; d_offsets: num_segments + 1
+ * non-decreasing DEVICE words, off[0] = 0, off[num_segments] = n.  Needs a sorter created
+ * with a payload (it carries the input index); two sorts (keys, then segment ids) and one
+ * gather; scratch of 12 + key-size bytes per item is allocated on first use and kept. */
+grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
+                              const uint32_t* d_offsets, int num_segments, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,10 @@ Contents (each restates the reference, amdreallyfast/GpuRadixSort, file:line cit
   * stable_sort            independent C merge sort (small N) / numpy stable argsort (any N)
   * splitmix keys          SURVEY.md §8(d) generator, numpy and C twins
   * cpu_sort               std::sort / __gnu_parallel::sort (BASELINE.md §4 CPU baseline)
+  * ref_device_scan        K3a + K3b composed as ParallelSort.cpp:253-274 drives them
+  * key_transform_np,
+    segmented_sort_np      checkers for the §8f extensions (order-preserving key bits,
+                           segmented sort): numpy restatements, no reference counterpart
 """
 from __future__ import annotations
 
@@ -86,6 +90,62 @@ def ref_parallel_sort(keys) -> tuple[np.ndarray, np.ndarray]:
     if r != 0:
         raise MemoryError("ref_parallel_sort: allocation failed")
     return a, perm[: a.size]
+
+
+def ref_device_scan(values) -> tuple[np.ndarray, int]:
+    """The reference's device-wide exclusive scan: K3a scans each 1024-item group of the
+    zero-padded input (ParallelPrefixScan.comp:56-141, PrefixSumSsbo.cpp:125-127), K3b scans
+    the group totals in one 1024-wide group (ParallelPrefixScan.comp:151-196), and the
+    group's prefix is added to each item (SortIntermediateData.comp:46-48 reads them so).
+    uint32 arithmetic wraps mod 2^32 as in GLSL.  Valid for N <= 1,048,576."""
+    a = np.ascontiguousarray(values, dtype=np.uint32)
+    n = a.size
+    if n > REF_CAPACITY:
+        raise ValueError("beyond the reference's capacity")
+    if n == 0:
+        return a.copy(), 0
+    p = padded_count(n)
+    padded = np.zeros(p, dtype=np.uint32)
+    padded[:n] = a
+    groups = p // 1024
+    sums = np.zeros(1024, dtype=np.uint32)
+    for g in range(groups):
+        out, tot = blelloch_scan(padded[g * 1024:(g + 1) * 1024])
+        padded[g * 1024:(g + 1) * 1024] = out
+        sums[g] = tot
+    gscan, total = blelloch_scan(sums)
+    with np.errstate(over="ignore"):
+        padded += np.repeat(gscan[:groups], 1024)
+    return padded[:n], int(total)
+
+
+# ---- §8f extensions: checkers -------------------------------------------------------------
+
+def key_transform_np(a: np.ndarray) -> np.ndarray:
+    """Order-preserving unsigned image of signed / IEEE-754 keys (grs_key_transform)."""
+    bits = a.dtype.itemsize * 8
+    ut = np.uint32 if bits == 32 else np.uint64
+    u = a.view(ut).copy()
+    sign = ut(1) << ut(bits - 1)
+    if a.dtype.kind == "i":
+        return u ^ sign
+    if a.dtype.kind == "f":
+        neg = (u & sign) != 0
+        return np.where(neg, ~u, u | sign).astype(ut)
+    return u
+
+
+def segmented_sort_np(keys: np.ndarray, offsets: np.ndarray, vals=None):
+    """Every segment [off[s], off[s+1]) stably sorted on its own."""
+    k = keys.copy()
+    v = None if vals is None else vals.copy()
+    for s in range(len(offsets) - 1):
+        lo, hi = int(offsets[s]), int(offsets[s + 1])
+        o = np.argsort(keys[lo:hi], kind="stable")
+        k[lo:hi] = keys[lo:hi][o]
+        if v is not None:
+            v[lo:hi] = vals[lo:hi][o]
+    return k, v
 
 
 # ---- independent stable sorts -------------------------------------------------------------

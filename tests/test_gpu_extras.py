@@ -1,0 +1,185 @@
+"""GPU parity of the §8f extensions, through the C-ABI:
+
+  * grs_exclusive_scan_u32  vs the restated reference scan (K3a + K3b, oracle.ref_device_scan)
+                            for N <= 2^20, the PrefixScan.xlsx KAT, and numpy cumsum mod 2^32
+                            beyond the reference's capacity
+  * grs_key_transform       signed / float keys sorted through the unsigned sort vs numpy's
+                            order of the original values (parity unpinned: the reference has
+                            no signed or float keys, ReadMeRadixSort.txt:71-80)
+  * grs_sort_segmented      vs per-segment numpy stable argsort (parity unpinned: the
+                            reference has no segmented sort)
+Bit-exact throughout (integer work).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def cumsum_excl(a: np.ndarray):
+    c = np.cumsum(a.astype(np.uint64)) - a.astype(np.uint64)
+    return (c & 0xFFFFFFFF).astype(np.uint32), int(a.astype(np.uint64).sum() & 0xFFFFFFFF)
+
+
+def gpu_scan(a: np.ndarray, dev, in_place=False):
+    import gpuradixsort_amd as grs
+
+    x = torch.from_numpy(a.view(np.int32).copy()).to(dev)
+    total = torch.full((1,), -1, dtype=torch.int32, device=dev)
+    out = grs.exclusive_scan_u32(x, x if in_place else None, total=total)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32), int(total.cpu().numpy().view(np.uint32)[0])
+
+
+def test_scan_xlsx_kat(gpu):
+    kat = json.load(open(os.path.join(GOLDEN, "prefix_scan_xlsx.json")))
+    out, total = gpu_scan(np.asarray(kat["input"], dtype=np.uint32), gpu)
+    assert out.tolist() == kat["exclusive_scan"]
+    assert total == kat["total"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 1023, 1024, 1025, 4095, 4096, 4097, 65537, 1 << 20])
+def test_scan_vs_reference_restatement(gpu, n):
+    rng = np.random.default_rng(n)
+    for a in (rng.integers(0, 2, n, dtype=np.uint32),                 # the reference's 0/1 bits
+              rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)):  # wraps mod 2^32
+        want, wtot = oracle.ref_device_scan(a)
+        out, total = gpu_scan(a, gpu)
+        assert np.array_equal(out, want)
+        assert total == wtot
+
+
+@pytest.mark.parametrize("n", [(1 << 24) + 5, 100_000_007])
+def test_scan_large_in_place(gpu, n):
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want, wtot = cumsum_excl(a)
+    out, total = gpu_scan(a, gpu, in_place=True)
+    assert np.array_equal(out, want)
+    assert total == wtot
+
+
+def test_scan_empty_and_all_max(gpu):
+    out, total = gpu_scan(np.zeros(0, dtype=np.uint32), gpu)
+    assert out.size == 0 and total == 0
+    a = np.full(300_001, 0xFFFFFFFF, dtype=np.uint32)
+    out, total = gpu_scan(a, gpu)
+    want, wtot = cumsum_excl(a)
+    assert np.array_equal(out, want) and total == wtot
+
+
+# ---- key transforms ----------------------------------------------------------------------
+
+def sort_transformed(a: np.ndarray, dev):
+    """a (signed / float numpy array) -> sorted through transform + unsigned sort + inverse,
+    plus the stable permutation."""
+    import gpuradixsort_amd as grs
+
+    bits = a.dtype.itemsize * 8
+    t = torch.from_numpy(a.copy()).to(dev)
+    u = t.view(torch.int32 if bits == 32 else torch.int64)
+    grs.key_transform(t)
+    s = grs.RadixSorter(max(a.size, 1), key_bits=bits, pairs=True)
+    v = torch.arange(a.size, dtype=torch.int32, device=dev)
+    s.sort(u, v)
+    grs.key_transform(t, inverse=True)
+    torch.cuda.synchronize()
+    s.check_error()
+    s.close()
+    return t.cpu().numpy(), v.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.int64, np.float32, np.float64])
+def test_key_transform_sort(gpu, dtype):
+    rng = np.random.default_rng(3)
+    n = 300_017
+    if np.dtype(dtype).kind == "i":
+        info = np.iinfo(dtype)
+        a = rng.integers(info.min, info.max, n, dtype=dtype, endpoint=True)
+        a[:5] = [info.min, info.max, 0, -1, 1]
+    else:
+        a = (rng.standard_normal(n) * 1e6).astype(dtype)
+        a[::97] = a[::97].round()          # ties
+        a[:6] = [np.inf, -np.inf, 0.0, -0.0, np.finfo(dtype).tiny, -np.finfo(dtype).max]
+    out, perm = sort_transformed(a, gpu)
+    order = np.argsort(oracle.key_transform_np(a), kind="stable")
+    assert np.array_equal(out.view(np.uint8), a[order].view(np.uint8))   # bit-exact
+    assert np.array_equal(perm, order.astype(np.uint32))
+    # and the values are in numpy's numeric order (no NaNs here; -0 sorts before +0)
+    assert np.array_equal(out, np.sort(a, kind="stable"))
+
+
+def test_key_transform_nan_and_roundtrip(gpu):
+    import gpuradixsort_amd as grs
+
+    a = np.array([1.0, np.nan, -np.nan, -np.inf, np.inf, -0.0, 0.0, -2.5], dtype=np.float32)
+    out, _ = sort_transformed(a, gpu)
+    bits = out.view(np.uint32)
+    assert np.isnan(out[0]) and np.signbit(out[0])       # -NaN first
+    assert np.isnan(out[-1]) and not np.signbit(out[-1])  # +NaN last
+    assert out[1] == -np.inf and out[-2] == np.inf
+    assert out[2] == -2.5 and bits[3] == 0x80000000 and bits[4] == 0   # -0 before +0
+    # transform + inverse is the identity on every bit pattern
+    x = torch.from_numpy(np.random.default_rng(1).integers(0, 2**32, 1 << 16, dtype=np.uint64)
+                         .astype(np.uint32).view(np.float32)).to(gpu)
+    y = x.clone()
+    grs.key_transform(y)
+    grs.key_transform(y, inverse=True)
+    assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
+# ---- segmented sort ------------------------------------------------------------------------
+
+def random_offsets(n, nseg, rng, empty=True):
+    cuts = np.sort(rng.integers(0, n + 1, nseg - 1))
+    off = np.concatenate([[0], cuts, [n]]).astype(np.uint32)
+    if empty and nseg > 3:
+        off[2] = off[1]                  # an empty segment
+    return off
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+@pytest.mark.parametrize("n,nseg", [(1, 1), (1000, 1), (100_003, 7), (300_000, 4096),
+                                    (1 << 20, 100_000)])
+def test_segmented_sort(gpu, kb, n, nseg):
+    import gpuradixsort_amd as grs
+
+    rng = np.random.default_rng(n + nseg + kb)
+    dt = np.uint32 if kb == 32 else np.uint64
+    keys = rng.integers(0, 1 << 12, n, dtype=dt)       # many ties: stability matters
+    vals = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    off = random_offsets(n, nseg, rng)
+    want_k, want_v = oracle.segmented_sort_np(keys, off, vals)
+    s = grs.RadixSorter(n, key_bits=kb, pairs=True)
+    k = torch.from_numpy(keys.view(np.int32 if kb == 32 else np.int64).copy()).to(gpu)
+    v = torch.from_numpy(vals.view(np.int32).copy()).to(gpu)
+    o = torch.from_numpy(off.view(np.int32)).to(gpu)
+    s.sort_segmented(k, o, v)
+    torch.cuda.synchronize()
+    s.check_error()
+    assert np.array_equal(k.cpu().numpy().view(dt), want_k)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), want_v)
+    # keys only (no payload pointer) gives the same keys
+    k2 = torch.from_numpy(keys.view(np.int32 if kb == 32 else np.int64).copy()).to(gpu)
+    s.sort_segmented(k2, o)
+    torch.cuda.synchronize()
+    assert np.array_equal(k2.cpu().numpy().view(dt), want_k)
+    s.close()
+
+
+def test_segmented_sort_needs_payload_sorter(gpu):
+    import gpuradixsort_amd as grs
+
+    s = grs.RadixSorter(16, key_bits=32, pairs=False)
+    k = torch.zeros(16, dtype=torch.int32, device=gpu)
+    o = torch.tensor([0, 16], dtype=torch.int32, device=gpu)
+    with pytest.raises(ValueError):
+        s.sort_segmented(k, o)
+    s.close()

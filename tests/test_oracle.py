@@ -138,3 +138,31 @@ def test_cpu_sort_wrappers():
     v = np.arange(k.size, dtype=np.uint32)
     oracle.cpu_stable_sort_pairs(k, v, 2)
     assert hashlib.sha256(v.tobytes()).hexdigest() == rec["sha256_perm"]
+
+
+def test_ref_device_scan_pinned_by_xlsx_and_cumsum():
+    """K3a + K3b composed (oracle.ref_device_scan) == the PrefixScan.xlsx hand trace, and ==
+    an independent cumsum (mod 2^32) across group boundaries."""
+    kat = load("prefix_scan_xlsx.json")
+    out, total = oracle.ref_device_scan(kat["input"])
+    assert out.tolist() == kat["exclusive_scan"] and total == kat["total"]
+    rng = np.random.default_rng(5)
+    for n in (1, 1023, 1024, 1025, 3000, 1 << 16):
+        a = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        out, total = oracle.ref_device_scan(a)
+        c = (np.cumsum(a.astype(np.uint64)) - a.astype(np.uint64)) & 0xFFFFFFFF
+        assert np.array_equal(out, c.astype(np.uint32))
+        assert total == int(a.astype(np.uint64).sum() & 0xFFFFFFFF)
+
+
+def test_key_transform_np_orders_like_numpy():
+    rng = np.random.default_rng(2)
+    for dt in (np.int32, np.int64):
+        a = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, 5000, dtype=dt)
+        assert np.array_equal(a[np.argsort(oracle.key_transform_np(a), kind="stable")],
+                              np.sort(a, kind="stable"))
+    for dt in (np.float32, np.float64):
+        a = (rng.standard_normal(5000) * 1e3).astype(dt)
+        a[:4] = [np.inf, -np.inf, 0.0, -0.0]
+        assert np.array_equal(a[np.argsort(oracle.key_transform_np(a), kind="stable")],
+                              np.sort(a, kind="stable"))

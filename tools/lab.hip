@@ -186,7 +186,10 @@ int lab_v3(int kb, int pairs, int block, int items, int dbg, int grid, const voi
     C3(32, 0, 512, 16, 0) C3(32, 0, 512, 16, 16) C3(32, 0, 512, 12, 0) C3(32, 0, 512, 16, 32)
     C3(32, 0, 512, 16, 48) C3(32, 0, 1024, 16, 32) C3(32, 0, 1024, 16, 8) C3(32, 0, 512, 16, 8)
     C3(32, 0, 1024, 16, 64) C3(32, 0, 512, 16, 64) C3(32, 0, 1024, 16, 72)
-    C3(32, 0, 1024, 16, 0) C3(32, 0, 1024, 16, 16) C3(32, 0, 1024, 12, 0) C3(32, 0, 512, 8, 0)
+    C3(32, 0, 1024, 16, 0) C3(32, 0, 1024, 16, 16) C3(32, 0, 1024, 16, 1) C3(32, 0, 1024, 16, 2)
+    C3(32, 0, 1024, 16, 3) C3(32, 0, 1024, 16, 9) C3(32, 0, 1024, 16, 128)
+    C3(32, 0, 1024, 16, 256) C3(32, 0, 1024, 16, 384) C3(32, 0, 1024, 16, 130)
+    C3(32, 0, 1024, 16, 65) C3(32, 0, 1024, 16, 577) C3(32, 0, 1024, 16, 705) C3(32, 0, 1024, 16, 193) C3(32, 0, 1024, 12, 0) C3(32, 0, 512, 8, 0)
     C3(32, 1, 512, 8, 0) C3(32, 1, 1024, 8, 0) C3(64, 0, 512, 8, 0) C3(64, 0, 1024, 8, 0)
     C3(64, 1, 512, 4, 0) C3(64, 1, 1024, 4, 0)
 #undef C3
