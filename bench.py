@@ -77,9 +77,22 @@ def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
         oracle.cpu_sort(keys, 1)
         what = "std::sort"
     dt = time.perf_counter() - t
-    return {"value": round(n_sample / dt / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
-            "sample": f"{n_sample} keys of the same splitmix64 uniform workload, {what}, "
-                      f"1 thread, {dt:.2f} s (oracle/cpu_sort.cpp)"}
+    out = {"value": round(n_sample / dt / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
+           "sample": f"{n_sample} keys of the same splitmix64 uniform workload, {what}, "
+                     f"1 thread, {dt:.2f} s (oracle/cpu_sort.cpp)"}
+    # __gnu_parallel::sort on this process's share of the host, beside it
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                       else (os.cpu_count() or 1)))
+    keys = oracle.splitmix_keys(n_sample, key_bits, seed)
+    t = time.perf_counter()
+    if pairs:
+        oracle.cpu_stable_sort_pairs(keys, np.arange(n_sample, dtype=np.uint32), cores)
+    else:
+        oracle.cpu_sort(keys, cores)
+    dt = time.perf_counter() - t
+    out["parallel"] = {"value": round(n_sample / dt / 1e9, 5), "cores": cores,
+                       "what": f"__gnu_parallel::sort, {cores} threads, {dt:.2f} s"}
+    return out
 
 
 def main():
@@ -185,6 +198,7 @@ def main():
         if rec:
             traffic = rec.get("hbm_bytes_per_launch")
 
+    sort_alg = n_local * 2 * tims[0]["passes"] * (kb // 8 + (4 if pairs else 0))
     if rank == 0:
         value = n_total * a.steps / elapsed / 1e9
         out = {
@@ -202,6 +216,11 @@ def main():
                          "traffic": traffic, "kernel": kernel_name,
                          "kernel_mean_ms": round(mean_pass_ms, 5),
                          "alg_bytes_per_launch": alg_bytes},
+            # whole-sort view of SURVEY.md §8d: B_alg = N x 2 x passes x (key + value bytes)
+            # over the whole step (histogram and exchange included)
+            "sort_roofline": {"achieved": round(sort_alg / (elapsed / a.steps) / 1e9, 1),
+                              "frac": round(sort_alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBPS, 4),
+                              "alg_bytes_per_step": sort_alg, "unit": "GB/s"},
             "cpu_baseline": cpu,
             "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
                           "sort_total_gpu": round(sort_ms, 5)},

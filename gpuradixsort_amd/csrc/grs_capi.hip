@@ -340,7 +340,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
   {
     // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout)
-    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(2048, (n + 4095) / 4096));
+    // (1024 blocks: lab 0.119 ms vs 0.125 at 2048 on 2^27 keys, tools/histlab.py)
+    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(1024, (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
                        stream, keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words));

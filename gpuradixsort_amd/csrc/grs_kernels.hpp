@@ -2355,8 +2355,8 @@ __global__ void grs_key_transform(K* __restrict__ keys, uint64_t n, int kind, in
 // 64 predecessors per step (nearest INCLUSIVE word ends the walk), publishes its inclusive
 // prefix and writes its items.  Status words are 64-bit: [63:62] flag, [31:0] value (mod 2^32).
 // In place (in == out) is allowed: a tile reads only its own items, before writing them.
-#define GRS_SCAN_BLOCK 256
-#define GRS_SCAN_ITEMS 16
+#define GRS_SCAN_BLOCK 512
+#define GRS_SCAN_ITEMS 32
 
 __device__ __forceinline__ uint64_t ld_status64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1,0 +1,95 @@
+"""Throughput of the §8f extensions on one MI355X (hipEvents on torch's current stream).
+
+python tools/bench_extras.py [--n N] [--reps R]
+Prints one JSON line per operation with its algorithmic bytes per item, GB/s and the fraction
+of the 8 TB/s HBM peak:
+  scan            grs_exclusive_scan_u32, 2^28 items: 8 B/item (read + write)
+  key_transform   grs_key_transform f32, 2^28 items: 8 B/item
+  segmented_sort  grs_sort_segmented u32 key + u32 payload, 2^26 items in 2^16 segments
+                  (Gkeys/s; two sorts + a gather by construction)
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import gpuradixsort_amd as grs  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 28)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    n = a.n
+    L = grs.lib()
+
+    x = torch.empty(n, dtype=torch.int32, device=dev)
+    grs.fill_splitmix(x, 1)
+    y = torch.empty_like(x)
+    scratch = torch.empty((L.grs_scan_scratch_bytes(n) + 3) // 4, dtype=torch.int32, device=dev)
+    tot = torch.empty(1, dtype=torch.int32, device=dev)
+    import ctypes
+    vp = ctypes.c_void_p
+    sp = vp(torch.cuda.current_stream().cuda_stream)
+
+    def scan():
+        assert L.grs_exclusive_scan_u32(vp(x.data_ptr()), vp(y.data_ptr()), n, vp(tot.data_ptr()),
+                                        vp(scratch.data_ptr()), scratch.numel() * 4, sp) == 0
+    ms = timed(scan, a.reps)
+    gbs = n * 8 / ms / 1e6
+    print(json.dumps({"op": "exclusive_scan_u32", "n": n, "ms": round(ms, 4),
+                      "GB/s": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                      "bytes_per_item": 8}), flush=True)
+
+    f = x.view(torch.float32)
+    ms = timed(lambda: grs.key_transform(f), a.reps)
+    gbs = n * 8 / ms / 1e6
+    print(json.dumps({"op": "key_transform_f32", "n": n, "ms": round(ms, 4),
+                      "GB/s": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                      "bytes_per_item": 8}), flush=True)
+    del x, y, f
+
+    m = 1 << 26
+    segs = 1 << 16
+    s = grs.RadixSorter(m, key_bits=32, pairs=True)
+    k0 = torch.empty(m, dtype=torch.int32, device=dev)
+    grs.fill_splitmix(k0, 2)
+    k = torch.empty_like(k0)
+    v = torch.empty_like(k0)
+    off = torch.arange(0, m + 1, m // segs, dtype=torch.int32, device=dev)
+
+    def seg():
+        k.copy_(k0)
+        s.sort_segmented(k, off, v)
+    ms_copy = timed(lambda: k.copy_(k0), a.reps)
+    ms = timed(seg, a.reps) - ms_copy
+    print(json.dumps({"op": "sort_segmented_u32_pairs", "n": m, "segments": segs,
+                      "ms": round(ms, 4), "Gkeys/s": round(m / ms / 1e6, 2),
+                      "note": "restore copy of the keys subtracted"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
