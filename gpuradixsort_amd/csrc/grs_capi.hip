@@ -157,6 +157,7 @@ struct grs_sorter {
   // grs_sort_segmented scratch (allocated on first use, grown on demand)
   void* seg_buf = nullptr;
   size_t seg_bytes = 0;
+  grs_sorter* seg64 = nullptr;     // u64 pair sorter of (segment << 32 | key), u32 keys only
 };
 
 extern "C" {
@@ -188,6 +189,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->status) (void)hipFree(s->status);
   if (s->ctrl) (void)hipFree(s->ctrl);
   if (s->seg_buf) (void)hipFree(s->seg_buf);
+  if (s->seg64) grs_destroy(s->seg64);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   delete[] s->ev;
@@ -657,11 +659,11 @@ grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, in
   return GRS_OK;
 }
 
-// Scan scratch: [0] tile ticket, [1] error word, [2..3] pad, then one 64-bit status word per
-// tile.
+// Scan scratch: [0] error word (kept for the ABI; reduce-then-scan never spins), [1..3]
+// pad, then one uint32 prefix per 16K-item tile.
 static constexpr size_t kScanTile = GRS_SCAN_BLOCK * GRS_SCAN_ITEMS;
 
-size_t grs_scan_scratch_bytes(size_t n) { return 16 + 8 * ((n + kScanTile - 1) / kScanTile); }
+size_t grs_scan_scratch_bytes(size_t n) { return 16 + 4 * ((n + kScanTile - 1) / kScanTile); }
 
 grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
                                   uint32_t* d_total, void* d_scratch, size_t scratch_bytes,
@@ -674,14 +676,23 @@ grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t 
   }
   if (!d_in || !d_out || !d_scratch)
     return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: NULL argument");
-  const size_t need = grs_scan_scratch_bytes(n);
-  if (scratch_bytes < need) return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: scratch too small");
+  if (scratch_bytes < grs_scan_scratch_bytes(n))
+    return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: scratch too small");
+  if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15u)
+    return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: d_in and d_out must be 16-byte aligned");
   uint32_t* ctl = static_cast<uint32_t*>(d_scratch);
-  GRS_HIP(hipMemsetAsync(ctl, 0, need, st));
+  uint32_t* sums = ctl + 4;
   const uint32_t tiles = static_cast<uint32_t>((n + kScanTile - 1) / kScanTile);
-  hipLaunchKernelGGL(grs::grs_scan_u32, dim3(tiles), dim3(GRS_SCAN_BLOCK), 0, st, d_in, d_out,
-                     static_cast<uint32_t>(n), reinterpret_cast<uint64_t*>(ctl + 4), ctl, d_total,
-                     ctl + 1);
+  const uint32_t n32 = static_cast<uint32_t>(n);
+  GRS_HIP(hipMemsetAsync(ctl, 0, 16, st));
+  hipLaunchKernelGGL(grs::grs_scan_reduce, dim3(tiles), dim3(GRS_SCAN_BLOCK), 0, st, d_in, n32,
+                     sums);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(grs::grs_scan_spine, dim3(1), dim3(GRS_SCAN_SPINE_BLOCK), 0, st, sums, tiles,
+                     d_total);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL(grs::grs_scan_downsweep, dim3(tiles), dim3(GRS_SCAN_BLOCK), 0, st, d_in,
+                     d_out, n32, sums);
   GRS_HIP(hipGetLastError());
   return GRS_OK;
 }
@@ -690,10 +701,72 @@ grs_status grs_scan_check_error(const void* d_scratch, void* stream) {
   if (!d_scratch) return set_err(GRS_EINVAL, "grs_scan_check_error: NULL scratch");
   hipStream_t st = static_cast<hipStream_t>(stream);
   uint32_t e = 0;
-  GRS_HIP(hipMemcpyAsync(&e, static_cast<const uint32_t*>(d_scratch) + 1, 4,
+  GRS_HIP(hipMemcpyAsync(&e, static_cast<const uint32_t*>(d_scratch), 4,
                          hipMemcpyDeviceToHost, st));
   GRS_HIP(hipStreamSynchronize(st));
   return e ? set_err(GRS_ETIMEOUT, "a scan look-back spin exceeded its bound") : GRS_OK;
+}
+
+// u32 keys: one sort of u64 keys (segment << 32 | key) by bits [0, 32 + ceil(log2 S)), the
+// payload riding along; no random gathers (grs_segment_marks / _compose / _split).
+// Scratch (seg_buf): comp u64[n] | marks u32[n] | marks_excl u32[n] | scan scratch.
+static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
+                                     const uint32_t* d_offsets, int num_segments, void* stream) {
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t scan_bytes = grs_scan_scratch_bytes(n);
+  const size_t need = al(n * 8) + 2 * al(n * 4) + al(scan_bytes);
+  grs_status r = GRS_OK;
+  if (s->seg_bytes < need) {
+    if (s->seg_buf) (void)hipFree(s->seg_buf);
+    s->seg_buf = nullptr;
+    s->seg_bytes = 0;
+    if (hipMalloc(&s->seg_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      r = set_err(GRS_ENOMEM, "grs_sort_segmented: scratch allocation failed");
+    } else {
+      s->seg_bytes = need;
+    }
+  }
+  if (r == GRS_OK && (!s->seg64 || s->seg64->capacity < n)) {
+    if (s->seg64) grs_destroy(s->seg64);
+    s->seg64 = nullptr;
+    r = grs_create(&s->seg64, s->capacity, GRS_KEY_U64, 1, 8, s->device);
+  }
+  char* b = static_cast<char*>(s->seg_buf);
+  uint64_t* comp = reinterpret_cast<uint64_t*>(b);
+  uint32_t* marks = reinterpret_cast<uint32_t*>(b + al(n * 8));
+  uint32_t* excl = reinterpret_cast<uint32_t*>(b + al(n * 8) + al(n * 4));
+  void* scan_scratch = b + al(n * 8) + 2 * al(n * 4);
+  int segbits = 0;
+  while ((1ll << segbits) < num_segments) ++segbits;
+  if (r == GRS_OK && hipMemsetAsync(marks, 0, n * 4, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_segmented: memset");
+  if (r == GRS_OK && num_segments > 1) {
+    hipLaunchKernelGGL(grs::grs_segment_marks, dim3(grid_for(num_segments, 256)), dim3(256), 0, st,
+                       d_offsets, static_cast<uint32_t>(num_segments) , static_cast<uint32_t>(n),
+                       marks);
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+  }
+  if (r == GRS_OK) r = grs_exclusive_scan_u32(marks, excl, n, nullptr, scan_scratch, scan_bytes, stream);
+  if (r == GRS_OK) {
+    hipLaunchKernelGGL(grs::grs_segment_compose, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<const uint32_t*>(d_keys), marks, excl, comp,
+                       static_cast<uint64_t>(n));
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+  }
+  // payload: the caller's values, or the marks buffer as a don't-care rider
+  if (r == GRS_OK) r = grs_sort_bits(s->seg64, comp, d_vals ? d_vals : marks, n, 0, 32 + segbits, stream);
+  if (r == GRS_OK) {
+    hipLaunchKernelGGL(grs::grs_segment_split, dim3(grid_for(n, 256)), dim3(256), 0, st, comp,
+                       static_cast<uint32_t*>(d_keys), static_cast<uint64_t>(n));
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+  }
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
 }
 
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
@@ -706,6 +779,8 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_segmented: n exceeds capacity");
   if (n == 0) return GRS_OK;
   if (!d_keys) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL keys");
+  if (s->key_type == GRS_KEY_U32) return sort_segmented_u32(s, d_keys, d_vals, n, d_offsets,
+                                                            num_segments, stream);
   int prev = 0;
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
@@ -718,6 +793,7 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   grs_status r = GRS_OK;
   if (s->seg_bytes < need) {
     if (s->seg_buf) (void)hipFree(s->seg_buf);
+  if (s->seg64) grs_destroy(s->seg64);
     s->seg_buf = nullptr;
     s->seg_bytes = 0;
     if (hipMalloc(&s->seg_buf, need) != hipSuccess) {

@@ -2345,47 +2345,115 @@ __global__ void grs_key_transform(K* __restrict__ keys, uint64_t n, int kind, in
 
 // ----------------------------------------------------------------------------------------
 // stand-alone device-wide exclusive scan of uint32 (the reference's K3a + K3b,
-// ParallelPrefixScan.comp:41-196, as one single-pass launch)
+// ParallelPrefixScan.comp:41-196), reduce-then-scan
 // ----------------------------------------------------------------------------------------
 //
-// The reference scans 1024-item groups with a Blelloch tree in shared memory (K3a) and then
-// the <= 1024 group totals in one work group (K3b), with sums wrapping mod 2^32.  Here: one
-// launch, tiles of SCAN_BLOCK x SCAN_ITEMS items taken by ticket (so a tile only waits on
-// tiles that already started); a tile publishes its aggregate, one wave looks back over up to
-// 64 predecessors per step (nearest INCLUSIVE word ends the walk), publishes its inclusive
-// prefix and writes its items.  Status words are 64-bit: [63:62] flag, [31:0] value (mod 2^32).
-// In place (in == out) is allowed: a tile reads only its own items, before writing them.
+// The reference scans 1024-item groups with a Blelloch tree in shared memory (K3a), then the
+// <= 1024 group totals in one work group (K3b); sums wrap mod 2^32.  Here the groups are
+// 16K-item tiles and there are three launches:
+//   grs_scan_reduce     tile sums (one read of the input)
+//   grs_scan_spine      exclusive scan of the tile sums in one workgroup (+ the total)
+//   grs_scan_downsweep  re-read each tile, scan it, add its tile prefix, write it
+// 12 B of HBM traffic per item.  (Measured against single-pass decoupled look-back variants
+// of 8 B/item, flat and two-level: the look-back chain made those 1.6-2.3x slower, DESIGN.md
+// §3.5.)  In place (in == out) is allowed: only the downsweep writes, a tile after reading it.
 #define GRS_SCAN_BLOCK 512
 #define GRS_SCAN_ITEMS 32
+#define GRS_SCAN_SPINE_BLOCK 1024
 
-__device__ __forceinline__ uint64_t ld_status64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status64(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_reduce(const uint32_t* __restrict__ in,
+                                                                 uint32_t n,
+                                                                 uint32_t* __restrict__ tile_sums) {
+  constexpr int B = GRS_SCAN_BLOCK, I = GRS_SCAN_ITEMS, TILE = B * I, W = B / GRS_WAVE;
+  __shared__ uint32_t s_wsum[W];
+  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+  const uint32_t base = blockIdx.x * TILE;
+  uint32_t sum = 0;
+  if (base + TILE <= n) {
+    const uint4* v = reinterpret_cast<const uint4*>(in + base);
+#pragma unroll
+    for (int k = 0; k < I / 4; ++k) {
+      const uint4 x = v[k * B + t];
+      sum += x.x + x.y + x.z + x.w;
+    }
+  } else {
+    for (uint32_t i = base + t; i < n; i += B) sum += in[i];
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, GRS_WAVE);
+  if (lane == 0) s_wsum[w] = sum;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) tot += s_wsum[ww];
+    tile_sums[blockIdx.x] = tot;
+  }
 }
 
-__global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_u32(
+// One workgroup: tile_sums[0..m) -> exclusive prefix in place; *total = sum (nullable).
+__global__ __launch_bounds__(GRS_SCAN_SPINE_BLOCK) void grs_scan_spine(uint32_t* __restrict__ sums,
+                                                                      uint32_t m,
+                                                                      uint32_t* __restrict__ total) {
+  constexpr int B = GRS_SCAN_SPINE_BLOCK, W = B / GRS_WAVE;
+  __shared__ uint32_t s_wsum[W];
+  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < m; base += B) {
+    const uint32_t i = base + t;
+    const uint32_t x = i < m ? sums[i] : 0u;
+    uint32_t incl = x;
+#pragma unroll
+    for (int o = 1; o < GRS_WAVE; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
+      if (lane >= static_cast<uint32_t>(o)) incl += y;
+    }
+    if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, blk = 0;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) {
+      const uint32_t ws = s_wsum[ww];
+      if (static_cast<uint32_t>(ww) < w) wbase += ws;
+      blk += ws;
+    }
+    if (i < m) sums[i] = carry + wbase + incl - x;
+    carry += blk;
+    __syncthreads();   // s_wsum is rewritten by the next chunk
+  }
+  if (t == 0 && total != nullptr) *total = carry;
+}
+
+__global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_downsweep(
     const uint32_t* in, uint32_t* out, uint32_t n,   // may alias (in place)
-    uint64_t* __restrict__ status, uint32_t* __restrict__ ticket, uint32_t* __restrict__ total,
-    uint32_t* __restrict__ error_word) {
+    const uint32_t* __restrict__ tile_prefix) {
   constexpr int B = GRS_SCAN_BLOCK, I = GRS_SCAN_ITEMS, TILE = B * I, W = B / GRS_WAVE;
   // items pass through LDS with one pad word per 32 (position i -> i + i / 32): the coalesced
   // stripes (item k*B + t) and the per-thread runs (items t*I .. t*I + I-1) are both
   // bank-conflict-free
   __shared__ uint32_t s_tile[TILE + TILE / 32];
   __shared__ uint32_t s_wsum[W];
-  __shared__ uint32_t s_ticket, s_excl;
   const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-  if (t == 0) s_ticket = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const uint32_t tile = s_ticket;
-  const uint32_t base = tile * TILE;
+  const uint32_t base = blockIdx.x * TILE;
   auto pad = [](uint32_t i) { return i + (i >> 5); };
+  const bool full = base + TILE <= n;
+  if (full) {   // 16-byte loads: chunk k*B + t = items 4(k*B + t) .. +3
+    const uint4* v = reinterpret_cast<const uint4*>(in + base);
 #pragma unroll
-  for (int k = 0; k < I; ++k) {
-    const uint32_t i = base + k * B + t;
-    s_tile[pad(k * B + t)] = i < n ? in[i] : 0u;
+    for (int k = 0; k < I / 4; ++k) {
+      const uint4 q = v[k * B + t];
+      const uint32_t o = pad(4 * (k * B + t));   // 4 words never straddle a pad
+      s_tile[o] = q.x;
+      s_tile[o + 1] = q.y;
+      s_tile[o + 2] = q.z;
+      s_tile[o + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      const uint32_t i = base + k * B + t;
+      s_tile[pad(k * B + t)] = i < n ? in[i] : 0u;
+    }
   }
   __syncthreads();
   uint32_t x[I], sum = 0;
@@ -2394,7 +2462,6 @@ __global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_u32(
     x[k] = s_tile[pad(t * I + k)];
     sum += x[k];
   }
-  // block exclusive scan of the thread sums
   uint32_t incl = sum;
 #pragma unroll
   for (int o = 1; o < GRS_WAVE; o <<= 1) {
@@ -2402,71 +2469,31 @@ __global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_u32(
     if (lane >= static_cast<uint32_t>(o)) incl += y;
   }
   if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
-  __syncthreads();
-  uint32_t wbase = 0, agg = 0;
+  __syncthreads();   // also: every thread's reads of s_tile are done
+  uint32_t run = tile_prefix[blockIdx.x] + incl - sum;
 #pragma unroll
-  for (int ww = 0; ww < W; ++ww) {
-    const uint32_t ws = s_wsum[ww];
-    if (static_cast<uint32_t>(ww) < w) wbase += ws;
-    agg += ws;
-  }
-  const uint32_t thread_excl = wbase + incl - sum;
-  // publish, look back, publish the inclusive prefix
-  constexpr uint64_t AGG = static_cast<uint64_t>(GRS_FLAG_AGGREGATE) << 62;
-  constexpr uint64_t INC = static_cast<uint64_t>(GRS_FLAG_INCLUSIVE) << 62;
-  if (w == 0) {
-    uint32_t excl = 0;
-    if (tile == 0) {
-      if (lane == 0) st_status64(&status[0], INC | agg);
-    } else {
-      if (lane == 0) st_status64(&status[tile], AGG | agg);
-      int64_t hi = static_cast<int64_t>(tile) - 1;   // newest predecessor of this window
-      uint32_t spins = 0;
-      for (;;) {
-        const int64_t p = hi - static_cast<int64_t>(lane);
-        uint64_t sw = p >= 0 ? ld_status64(&status[p]) : (INC | 0u);
-        const uint64_t incl_mask = __builtin_amdgcn_ballot_w64((sw >> 62) == GRS_FLAG_INCLUSIVE);
-        // lanes up to (and including) the nearest INCLUSIVE word, or the whole window
-        const uint32_t stop = incl_mask ? static_cast<uint32_t>(__builtin_ctzll(incl_mask)) : 63u;
-        const uint64_t not_ready = __builtin_amdgcn_ballot_w64((sw >> 62) == GRS_FLAG_NOT_READY);
-        const uint64_t need = stop == 63u ? ~0ull : ((2ull << stop) - 1ull);
-        if (not_ready & need) {
-          if (++spins > GRS_SPIN_LIMIT) {
-            if (lane == 0) atomicOr(error_word, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        uint32_t c = lane <= stop ? static_cast<uint32_t>(sw) : 0u;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, GRS_WAVE);
-        excl += c;
-        if (incl_mask) break;
-        hi -= GRS_WAVE;
-      }
-      if (lane == 0) st_status64(&status[tile], INC | static_cast<uint32_t>(excl + agg));
-    }
-    if (lane == 0) s_excl = excl;
-    if (lane == 0 && total != nullptr && base + TILE >= n) *total = excl + agg;
-  }
-  __syncthreads();
-  uint32_t run = s_excl + thread_excl;
+  for (int ww = 0; ww < W; ++ww)
+    if (static_cast<uint32_t>(ww) < w) run += s_wsum[ww];
 #pragma unroll
   for (int k = 0; k < I; ++k) {
     const uint32_t xi = x[k];
-    x[k] = run;
+    s_tile[pad(t * I + k)] = run;
     run += xi;
   }
-  // back through LDS for coalesced stores (every thread's loads of s_tile are done: the
-  // barrier above)
-#pragma unroll
-  for (int k = 0; k < I; ++k) s_tile[pad(t * I + k)] = x[k];
   __syncthreads();
+  if (full) {
+    uint4* v = reinterpret_cast<uint4*>(out + base);
 #pragma unroll
-  for (int k = 0; k < I; ++k) {
-    const uint32_t i = base + k * B + t;
-    if (i < n) out[i] = s_tile[pad(k * B + t)];
+    for (int k = 0; k < I / 4; ++k) {
+      const uint32_t o = pad(4 * (k * B + t));
+      v[k * B + t] = make_uint4(s_tile[o], s_tile[o + 1], s_tile[o + 2], s_tile[o + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      const uint32_t i = base + k * B + t;
+      if (i < n) out[i] = s_tile[pad(k * B + t)];
+    }
   }
 }
 
@@ -2503,6 +2530,34 @@ __global__ void grs_segment_gather(const K* __restrict__ keys, K* __restrict__ o
     out_keys[j] = keys[p];
     if (vals) out_vals[j] = vals[perm[p]];
   }
+}
+
+// Segmented sort of u32 keys without gathers: segment ids in input order by marking each
+// segment start (atomic: empty segments stack on one position) and a scan, then one u64 key
+// (segment << 32 | key) per item, sorted once and split back.
+__global__ void grs_segment_marks(const uint32_t* __restrict__ offsets, uint32_t nseg, uint32_t n,
+                                  uint32_t* __restrict__ marks) {
+  for (uint32_t s = 1 + blockIdx.x * blockDim.x + threadIdx.x; s < nseg;
+       s += gridDim.x * blockDim.x) {
+    const uint32_t o = offsets[s];
+    if (o < n) atomicAdd(&marks[o], 1u);
+  }
+}
+
+__global__ void grs_segment_compose(const uint32_t* __restrict__ keys,
+                                    const uint32_t* __restrict__ marks,
+                                    const uint32_t* __restrict__ marks_excl,
+                                    uint64_t* __restrict__ comp, uint64_t n) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    comp[i] = (static_cast<uint64_t>(marks_excl[i] + marks[i]) << 32) | keys[i];
+}
+
+__global__ void grs_segment_split(const uint64_t* __restrict__ comp, uint32_t* __restrict__ keys,
+                                  uint64_t n) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    keys[i] = static_cast<uint32_t>(comp[i]);
 }
 
 // Adjacent-order check of the reference (ParallelSort.cpp:336-352), strengthened: counts

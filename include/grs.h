@@ -155,7 +155,7 @@ grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, in
 
 /* Stand-alone device-wide exclusive prefix sum of uint32 (sums wrap mod 2^32), the
  * reference's K3a + K3b (ParallelPrefixScan.comp:41-196, ParallelSort.cpp:253-274) as one
- * single-pass launch.  d_out may equal d_in.  d_total (nullable) receives the sum of all
+ * reduce-then-scan (three launches).  d_out may equal d_in; both 16-byte aligned.  d_total (nullable) receives the sum of all
  * items (the reference's totalNumberOfOnes, PrefixScanBuffer.comp:37).  Scratch: device
  * memory of grs_scan_scratch_bytes(n) bytes, owned by the caller, one call at a time. */
 #define GRS_SCAN_MAX_N 0xFFFFF000u
