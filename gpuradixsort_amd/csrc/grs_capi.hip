@@ -158,6 +158,11 @@ struct grs_sorter {
   void* seg_buf = nullptr;
   size_t seg_bytes = 0;
   grs_sorter* seg64 = nullptr;     // u64 pair sorter of (segment << 32 | key), u32 keys only
+  // tuning knobs read from the environment at grs_create (A/B measurements on one box)
+  // GRS_V3_DMA=nt: nontemporal tile DMA.  One box, same process (tools/ab_v3_dma.sh): nt made
+  // the pass 1 % faster but the next histogram 20 % slower (106.5 vs 104.2 Gkeys/s), so off.
+  bool v3_dma_nt = false;
+  int hist_grid_cap = 1024;             // GRS_HIST_GRID: cap of the upfront histogram grid
 };
 
 extern "C" {
@@ -242,6 +247,8 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
     (void)hipGetLastError();
     s->v3_grid = std::max(1, cus) * std::max(1, per_cu);
   }
+  if (const char* e = std::getenv("GRS_V3_DMA")) s->v3_dma_nt = std::strcmp(e, "nt") == 0;
+  if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
   grs_status st = GRS_OK;
   auto alloc = [&](void** p, size_t bytes) {
     if (st != GRS_OK) return;
@@ -342,8 +349,9 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
   {
     // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout)
-    // (1024 blocks: lab 0.119 ms vs 0.125 at 2048 on 2^27 keys, tools/histlab.py)
-    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(1024, (n + 4095) / 4096));
+    // 1024 blocks: 5 % faster than 2048 alone (tools/histlab.py) and 0.008 ms faster inside
+    // the sort (tools/ab_v3_dma.sh); GRS_HIST_GRID overrides the cap
+    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(s->hist_grid_cap, (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
                        stream, keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words));
@@ -364,9 +372,14 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     if (kind == PassKind::V3) {
       if constexpr (!PAIRS && sizeof(K) == 4) {
         const uint32_t grid = std::min<uint32_t>(tiles, static_cast<uint32_t>(s->v3_grid));
-        hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS>),
-                           dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
-                           hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+        if (!s->v3_dma_nt)   // default cache policy for the tile DMA (see grs_create)
+          hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS, 128>),
+                             dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
+                             hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+        else
+          hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS>),
+                             dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
+                             hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
       }
     } else if (kind == PassKind::AR) {
       hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),

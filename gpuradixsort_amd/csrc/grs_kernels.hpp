@@ -2006,9 +2006,11 @@ struct V3Smem {
 };
 
 // Persistent grid (one or two workgroups per CU).  Per iteration on tile `cur` (LDS buffer b):
-// Tiles are DMA'd with the nontemporal policy (read once per pass; lab: 3-4 % faster pass
-// than the default policy, DBG & 128 restores it); the scatter stores keep the default
-// policy, since partial lines of neighbouring digit runs merge in L2 (nt stores: 1.8x slower).
+// Tile DMA cache policy: nontemporal unless DBG & 128.  nt made the pass alone 1-3 % faster
+// (tools/lab.py) but the sort slower (the next histogram launch absorbs more dirty lines:
+// tools/ab_v3_dma.sh), so the library launches the DBG = 128 instance unless GRS_V3_DMA=nt.
+// The scatter stores keep the default policy: partial lines of neighbouring digit runs merge
+// in L2 (nt stores measured 1.8x slower).
 //   L0   wait for this wave's DMA of `cur` (a counted vmcnt that skips the previous tile's
 //        stores), barrier; keys -> registers, wave-striped: item j of lane l of wave w is key
 //        w*64*ITEMS + j*64 + l, so ranking items in (j, lane) order is input order
