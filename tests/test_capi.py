@@ -63,3 +63,25 @@ def test_python_errors_are_loud():
 
     with pytest.raises(GrsError):
         _lib.check(_lib.GRS_EINVAL, "probe")
+
+
+def test_extension_entry_points_validate_without_a_device():
+    """§8f entry points reject bad arguments before any HIP call (no device needed)."""
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    # key transform: key width and kind are checked; n = 0 and kind 0 are no-ops
+    assert L.grs_key_transform(None, 10, 2, 1, 0, None) == _lib.GRS_EINVAL
+    assert L.grs_key_transform(None, 10, 4, 3, 0, None) == _lib.GRS_EINVAL
+    assert L.grs_key_transform(None, 10, 4, 1, 0, None) == _lib.GRS_EINVAL   # NULL keys
+    assert L.grs_key_transform(None, 0, 4, 1, 0, None) == _lib.GRS_OK
+    assert L.grs_key_transform(None, 10, 8, 0, 0, None) == _lib.GRS_OK
+    # scan: scratch size grows with n; capacity, NULL and short-scratch checks
+    assert L.grs_scan_scratch_bytes(0) == 16
+    assert L.grs_scan_scratch_bytes(1) < L.grs_scan_scratch_bytes(1 << 24)
+    assert L.grs_exclusive_scan_u32(None, None, 1 << 33, None, None, 0, None) == _lib.GRS_ECAPACITY
+    assert L.grs_exclusive_scan_u32(None, None, 100, None, None, 0, None) == _lib.GRS_EINVAL
+    fake = ctypes.c_void_p(1 << 20)   # never dereferenced: the size check fails first
+    assert L.grs_exclusive_scan_u32(fake, fake, 100, None, fake, 4, None) == _lib.GRS_EINVAL
+    # segmented sort: a sorter is required
+    assert L.grs_sort_segmented(None, None, None, 10, None, 1, None) == _lib.GRS_EINVAL
