@@ -58,6 +58,8 @@ SIGNATURES = [
     ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),
     ("grs_count_inversions", c_int, [c_void_p, c_size_t, c_int, POINTER(c_uint64), c_void_p]),
+    ("grs_sort_host", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                              c_void_p]),
     ("grs_key_transform", c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p]),
     ("grs_scan_scratch_bytes", c_size_t, [c_size_t]),
     ("grs_exclusive_scan_u32", c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_size_t,

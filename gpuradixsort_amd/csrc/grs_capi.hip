@@ -158,6 +158,8 @@ struct grs_sorter {
   void* seg_buf = nullptr;
   size_t seg_bytes = 0;
   grs_sorter* seg64 = nullptr;     // u64 pair sorter of (segment << 32 | key), u32 keys only
+  void* host_stage = nullptr;      // grs_sort_host device staging (keys | payload), on first use
+  size_t host_stage_bytes = 0;
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
   // GRS_V3_DMA=nt: nontemporal tile DMA.  One box, same process (tools/ab_v3_dma.sh): nt made
   // the pass 1 % faster but the next histogram 20 % slower (106.5 vs 104.2 Gkeys/s), so off.
@@ -195,6 +197,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->ctrl) (void)hipFree(s->ctrl);
   if (s->seg_buf) (void)hipFree(s->seg_buf);
   if (s->seg64) grs_destroy(s->seg64);
+  if (s->host_stage) (void)hipFree(s->host_stage);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   delete[] s->ev;
@@ -746,6 +749,7 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
   }
   if (r == GRS_OK && (!s->seg64 || s->seg64->capacity < n)) {
     if (s->seg64) grs_destroy(s->seg64);
+  if (s->host_stage) (void)hipFree(s->host_stage);
     s->seg64 = nullptr;
     r = grs_create(&s->seg64, s->capacity, GRS_KEY_U64, 1, 8, s->device);
   }
@@ -807,6 +811,7 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   if (s->seg_bytes < need) {
     if (s->seg_buf) (void)hipFree(s->seg_buf);
   if (s->seg64) grs_destroy(s->seg64);
+  if (s->host_stage) (void)hipFree(s->host_stage);
     s->seg_buf = nullptr;
     s->seg_bytes = 0;
     if (hipMalloc(&s->seg_buf, need) != hipSuccess) {
@@ -859,6 +864,50 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   if (r == GRS_OK && d_vals &&
       hipMemcpyAsync(d_vals, vout, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
     r = set_err(GRS_EHIP, "grs_sort_segmented: copy");
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
+                         const uint32_t* h_vals_in, uint32_t* h_vals_out, size_t n, void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_sort_host: NULL sorter");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_host: n exceeds capacity");
+  if (n == 0) return GRS_OK;
+  if (!h_keys_in || !h_keys_out) return set_err(GRS_EINVAL, "grs_sort_host: NULL keys");
+  if (s->pairs != (h_vals_in != nullptr) || (h_vals_in != nullptr) != (h_vals_out != nullptr))
+    return set_err(GRS_EINVAL, "grs_sort_host: payload pointers must match the sorter");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  const size_t kbytes = (n * kb + 255) & ~static_cast<size_t>(255);
+  const size_t need = kbytes + (s->pairs ? n * 4 : 0);
+  grs_status r = GRS_OK;
+  if (s->host_stage_bytes < need) {
+    if (s->host_stage) (void)hipFree(s->host_stage);
+    s->host_stage = nullptr;
+    s->host_stage_bytes = 0;
+    if (hipMalloc(&s->host_stage, need) != hipSuccess) {
+      (void)hipGetLastError();
+      r = set_err(GRS_ENOMEM, "grs_sort_host: staging allocation failed");
+    } else {
+      s->host_stage_bytes = need;
+    }
+  }
+  char* dk = static_cast<char*>(s->host_stage);
+  uint32_t* dv = s->pairs ? reinterpret_cast<uint32_t*>(dk + kbytes) : nullptr;
+  if (r == GRS_OK && hipMemcpyAsync(dk, h_keys_in, n * kb, hipMemcpyHostToDevice, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_host: upload");
+  if (r == GRS_OK && dv && hipMemcpyAsync(dv, h_vals_in, n * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_host: upload");
+  if (r == GRS_OK) r = grs_sort(s, dk, dv, n, stream);
+  if (r == GRS_OK && hipMemcpyAsync(h_keys_out, dk, n * kb, hipMemcpyDeviceToHost, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_host: download");
+  if (r == GRS_OK && dv && hipMemcpyAsync(h_vals_out, dv, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_host: download");
+  if (r == GRS_OK && hipStreamSynchronize(st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_host: synchronize");
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
 }

@@ -118,6 +118,24 @@ class RadixSorter:
                                   ctypes.c_void_p(sp.ctypes.data), int(sp.size), _ptr(counts),
                                   _stream_ptr(stream)), "grs_partition")
 
+    def sort_host(self, keys, vals=None, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Sort host numpy arrays in place through device staging (grs_sort_host; BASELINE C1
+        plumbing, PCIe both ways).  keys: uint32/uint64 numpy array; vals: uint32 or None."""
+        import numpy as np
+
+        if not isinstance(keys, np.ndarray) or not keys.flags.c_contiguous \
+                or keys.dtype.itemsize * 8 != self.key_bits:
+            raise ValueError(f"keys must be a contiguous {self.key_bits}-bit numpy array")
+        if (vals is not None) != self.pairs:
+            raise ValueError("payload presence must match the sorter")
+        if vals is not None and (vals.dtype.itemsize != 4 or vals.size < keys.size
+                                 or not vals.flags.c_contiguous):
+            raise ValueError("vals must be a contiguous 32-bit numpy array")
+        kp = ctypes.c_void_p(keys.ctypes.data)
+        vp = ctypes.c_void_p(vals.ctypes.data) if vals is not None else ctypes.c_void_p(0)
+        check(lib().grs_sort_host(self._h, kp, kp, vp, vp, keys.size, _stream_ptr(stream)),
+              "grs_sort_host")
+
     def sort_segmented(self, keys: torch.Tensor, offsets: torch.Tensor,
                        vals: Optional[torch.Tensor] = None, n: Optional[int] = None,
                        stream: Optional[torch.cuda.Stream] = None) -> None:

@@ -140,6 +140,14 @@ grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t see
 grs_status grs_count_inversions(const void* d_keys, size_t n, int key_bytes,
                                 uint64_t* out_count, void* stream);
 
+/* Host-buffer sort (BASELINE config C1's plumbing path; the reference's glBufferSubData
+ * upload + Sort() + readback, main.cpp:146-160): copies h_keys_in (and h_vals_in) to device
+ * staging owned by the sorter, sorts, copies the result to h_keys_out (and h_vals_out), and
+ * synchronises `stream`.  In-place (h_keys_out == h_keys_in) is allowed.  Its rate includes
+ * PCIe both ways; bench.py's headline value never does. */
+grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
+                         const uint32_t* h_vals_in, uint32_t* h_vals_out, size_t n, void* stream);
+
 /* ---- beyond the reference's path ---- */
 
 /* Order-preserving key transforms, so that signed and floating-point keys sort with the

@@ -183,3 +183,38 @@ def test_segmented_sort_needs_payload_sorter(gpu):
     with pytest.raises(ValueError):
         s.sort_segmented(k, o)
     s.close()
+
+
+# ---- host-buffer sort (BASELINE C1 plumbing) ------------------------------------------------
+
+def test_sort_host_c1_matches_reference_path(gpu):
+    """C1: 64K uniform u32 keys through grs_sort_host == the restated reference path."""
+    import gpuradixsort_amd as grs
+
+    keys = oracle.splitmix_keys(65536, 32, oracle.config_seed(1))
+    want_k, want_p = oracle.ref_parallel_sort(keys)
+    s = grs.RadixSorter(65536, key_bits=32, pairs=True)
+    k = keys.copy()
+    v = np.arange(k.size, dtype=np.uint32)
+    s.sort_host(k, v)
+    assert np.array_equal(k, want_k) and np.array_equal(v, want_p)
+    s.close()
+    s = grs.RadixSorter(65536, key_bits=32)
+    k = keys.copy()
+    s.sort_host(k)
+    assert np.array_equal(k, want_k)
+    with pytest.raises(ValueError):
+        s.sort_host(k, v)          # payload on a keys-only sorter
+    s.close()
+
+
+def test_sort_host_u64_and_empty(gpu):
+    import gpuradixsort_amd as grs
+
+    keys = oracle.splitmix_keys(300_001, 64, oracle.config_seed(5))
+    s = grs.RadixSorter(keys.size, key_bits=64)
+    k = keys.copy()
+    s.sort_host(k)
+    assert np.array_equal(k, np.sort(keys))
+    s.sort_host(np.zeros(0, dtype=np.uint64))
+    s.close()
