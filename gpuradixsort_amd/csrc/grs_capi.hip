@@ -42,7 +42,12 @@ grs_status set_err(grs_status s, const std::string& msg) {
 template <typename K, bool PAIRS, int RB>
 struct TileCfg {
   static constexpr int BLOCK = GRS_BLOCK;
-  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 8 : 16) : (PAIRS ? 16 : 24);
+  // The largest tiles that fit one workgroup's LDS (128-144 KB of keys + payload): longer
+  // digit runs per tile, fewer look-back steps.  Lab (2^27, ms per pass, two sweeps):
+  // u32 pairs 16 / 24 / 32 items 0.55 / 0.53-0.60 / 0.56; u64 keys 16 / 24 / 32 items
+  // 0.56 / 0.53-0.56 / 0.51; u64 pairs 8 / 12 / 16 / 24 items 1.02 / 0.90-0.96 / 0.81-0.87 /
+  // 0.80; bench C3 48 -> 55 Gkeys/s and C5 28.5 -> 30 going to 24 / 24 / 16 items.
+  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 24 : 32) : (PAIRS ? 32 : 24);
   static constexpr int TILE = BLOCK * ITEMS;
 };
 
