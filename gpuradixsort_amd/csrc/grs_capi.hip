@@ -62,6 +62,17 @@ struct V3Cfg {
   static constexpr int TILE = BLOCK * ITEMS;
 };
 
+// One-tile-per-workgroup atomic-rank pass with 32K-36K-key tiles for u32 keys without payload
+// (the default, 512 x 72; GRS_U32_PASS=ar1024 / ar512 select 1024 x 32 / 512 x 64): longer
+// digit runs per tile beat v3's prefetching of 16K-key tiles (lab 0.276 vs 0.285 ms per pass,
+// in the sort 109.8 vs 105.4 Gkeys/s).
+template <int B, int I>
+struct BigCfg {
+  static constexpr int BLOCK = B;
+  static constexpr int ITEMS = I;
+  static constexpr int TILE = B * I;
+};
+
 constexpr int max_tile_min() { return 2048; }  // smallest TILE over configs (sizes status)
 
 // Status words of one look-back buffer for `tiles` tiles: the larger of the one-tile passes'
@@ -170,6 +181,11 @@ struct grs_sorter {
   // the pass 1 % faster but the next histogram 20 % slower (106.5 vs 104.2 Gkeys/s), so off.
   bool v3_dma_nt = false;
   int hist_grid_cap = 1024;             // GRS_HIST_GRID: cap of the upfront histogram grid
+  // GRS_U32_PASS (u32 keys without payload): 3 = ar512x72 (default), 0 = v3, 1 = ar1024,
+  // 2 = ar512.  Same box, same process, 2^27 keys (tools/ab_u32_pass.sh): v3 105.4, ar1024
+  // 109.5, ar512x72 109.8 Gkeys/s (pass 0.273 / 0.266 / 0.266 ms; the histogram after a
+  // one-tile-per-workgroup pass also runs 0.02 ms faster).
+  int u32_pass = 3;
 };
 
 extern "C" {
@@ -257,6 +273,11 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   }
   if (const char* e = std::getenv("GRS_V3_DMA")) s->v3_dma_nt = std::strcmp(e, "nt") == 0;
   if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("GRS_U32_PASS"))
+    s->u32_pass = std::strcmp(e, "v3") == 0       ? 0
+                  : std::strcmp(e, "ar1024") == 0 ? 1
+                  : std::strcmp(e, "ar512") == 0  ? 2
+                                                  : 3;
   grs_status st = GRS_OK;
   auto alloc = [&](void** p, size_t bytes) {
     if (st != GRS_OK) return;
@@ -320,12 +341,17 @@ namespace {
 // Which pass kernel a sort call launches: the persistent v3 pass for u32 keys without payload,
 // the one-tile-per-workgroup atomic-rank pass otherwise, the ballot-match pass if the LDS
 // order probe failed (or GRS_RANK=match).
-enum class PassKind { V3, AR, MATCH };
+enum class PassKind { V3, AR, MATCH, AR1024, AR512, AR512X72 };
 
 template <typename K, bool PAIRS>
 PassKind pass_kind(const grs_sorter* s) {
   if (s->rank_mode != 0) return PassKind::MATCH;
-  return (!PAIRS && sizeof(K) == 4) ? PassKind::V3 : PassKind::AR;
+  if (!PAIRS && sizeof(K) == 4)
+    return s->u32_pass == 1   ? PassKind::AR1024
+           : s->u32_pass == 2 ? PassKind::AR512
+           : s->u32_pass == 3 ? PassKind::AR512X72
+                              : PassKind::V3;
+  return PassKind::AR;
 }
 
 template <typename K, bool PAIRS, int RB>
@@ -335,7 +361,11 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   constexpr int RADIX = 1 << RB;
   const PassKind kind = pass_kind<K, PAIRS>(s);
   const int passes = (end_bit - begin_bit + RB - 1) / RB;
-  const uint32_t tile = kind == PassKind::V3 ? V3Cfg::TILE : Cfg::TILE;
+  const uint32_t tile = kind == PassKind::V3       ? V3Cfg::TILE
+                        : kind == PassKind::AR1024 ? BigCfg<1024, 32>::TILE
+                        : kind == PassKind::AR512  ? BigCfg<512, 64>::TILE
+                        : kind == PassKind::AR512X72 ? BigCfg<512, 72>::TILE
+                                                   : Cfg::TILE;
   const uint32_t tiles = (n + tile - 1) / tile;
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
@@ -388,6 +418,21 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
           hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS>),
                              dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
                              hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+      }
+    } else if (kind == PassKind::AR1024 || kind == PassKind::AR512 || kind == PassKind::AR512X72) {
+      if constexpr (!PAIRS && sizeof(K) == 4) {
+        if (kind == PassKind::AR512X72)
+          hipLaunchKernelGGL((grs::grs_onesweep_ar<K, false, RB, 512, 72>), dim3(tiles), dim3(512),
+                             0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
+                             tickets + p, st_cur, st_nxt, err);
+        else if (kind == PassKind::AR1024)
+          hipLaunchKernelGGL((grs::grs_onesweep_ar<K, false, RB, 1024, 32>), dim3(tiles),
+                             dim3(1024), 0, stream, src, dst, vsrc, vdst, n, dig,
+                             hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+        else
+          hipLaunchKernelGGL((grs::grs_onesweep_ar<K, false, RB, 512, 64>), dim3(tiles), dim3(512),
+                             0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
+                             tickets + p, st_cur, st_nxt, err);
       }
     } else if (kind == PassKind::AR) {
       hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
@@ -915,6 +960,13 @@ grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
     r = set_err(GRS_EHIP, "grs_sort_host: synchronize");
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
+}
+
+const char* grs_pass_kernel(const grs_sorter* s) {
+  if (!s) return "";
+  if (s->rank_mode != 0) return "grs_onesweep_pass";
+  if (s->key_type == GRS_KEY_U32 && !s->pairs && s->u32_pass == 0) return "grs_onesweep_v3";
+  return "grs_onesweep_ar";
 }
 
 }  // extern "C"

@@ -74,9 +74,7 @@ class RadixSorter:
     @property
     def pass_kernel(self) -> str:
         """Name of the pass kernel a sort() call launches (profiling / roofline reports)."""
-        if self.rank_mode == "match":
-            return "grs_onesweep_pass"
-        return "grs_onesweep_v3" if (self.key_bits == 32 and not self.pairs) else "grs_onesweep_ar"
+        return lib().grs_pass_kernel(self._h).decode()
 
     def _check_keys(self, keys: torch.Tensor, vals: Optional[torch.Tensor]) -> None:
         if not keys.is_cuda or not keys.is_contiguous():

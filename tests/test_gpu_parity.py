@@ -67,10 +67,11 @@ def distributions(n, kb, rng):
                           & rng.integers(0, top, n, dtype=dt, endpoint=True))
 
 
-# tile edges of every pass kernel: 4096 / 8192 / 12288 (one-tile passes), 16384 (v3), and the
-# look-back group / supergroup edges (8 and 64 tiles)
-SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 12289, 16383, 16385, 65536,
-         131073, 1 << 20]
+# tile edges of every pass kernel: 12288 / 16384 (one-tile pair / u64 passes, 16384 also v3),
+# 36864 (the default u32 keys-only pass, 512 x 72), and the look-back group edges (8 tiles:
+# 98304 / 131072 / 294912)
+SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 12289, 16383, 16385, 36863,
+         36865, 65536, 98305, 131073, 294913, 1 << 20]
 
 
 @pytest.mark.parametrize("radix_bits", [4, 8])
@@ -108,7 +109,7 @@ def test_rank_mode_is_atomic_on_gfx950(gpu):
     """The LDS lane-order probe passes on MI355X, so the atomic-rank passes (v3 / ar) run."""
     s = sorter(32, False, 8, 1 << 20)
     assert s.rank_mode == "atomic"
-    assert s.pass_kernel == "grs_onesweep_v3"
+    assert s.pass_kernel == "grs_onesweep_ar"      # u32 keys: 512 x 72 tiles by default
     assert sorter(32, True, 8, 1 << 20).pass_kernel == "grs_onesweep_ar"
 
 
@@ -149,6 +150,28 @@ def test_ballot_match_fallback(gpu, monkeypatch):
         assert np.array_equal(k.cpu().numpy(), keys[perm])
         if pairs:
             assert np.array_equal(v.cpu().numpy(), perm)
+        s.close()
+
+
+@pytest.mark.parametrize("choice", ["v3", "ar1024", "ar512"])
+def test_u32_pass_alternatives(gpu, monkeypatch, choice):
+    """GRS_U32_PASS selects the other u32 keys-only pass kernels (the persistent v3 pass and
+    the 1024 x 32 / 512 x 64 one-tile passes, kept for A/B measurements): same bit-exact
+    results, across tile edges and both digit widths."""
+    import gpuradixsort_amd as grs
+
+    monkeypatch.setenv("GRS_U32_PASS", choice)
+    rng = np.random.default_rng(11)
+    for n, rb in ((1, 8), (16383, 8), (32769, 8), (36865, 4), (1_000_003, 8), (300_007, 4)):
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        keys[::7] = 0xFFFFFFFF
+        s = grs.RadixSorter(n, key_bits=32, radix_bits=rb)
+        assert s.pass_kernel == ("grs_onesweep_v3" if choice == "v3" else "grs_onesweep_ar")
+        k = to_dev(keys, gpu)
+        s.sort(k)
+        torch.cuda.synchronize()
+        s.check_error()
+        assert np.array_equal(k.cpu().numpy(), np.sort(keys)), (choice, n, rb)
         s.close()
 
 
