@@ -14,8 +14,8 @@ rank range-partitions its shard, exchanges buckets with one RCCL all-to-all-v ov
 sorts what it received (gpuradixsort_amd/sharded.py).
 
 Rank 0 prints ONE JSON line with the driver contract plus:
-  roofline      dominant kernel (the pass kernel: grs_onesweep_v3 for u32 keys, else
-                grs_onesweep_ar): algorithmic bytes per launch
+  roofline      dominant kernel (the pass kernel the sorter reports, grs_pass_kernel():
+                grs_onesweep_ar by default): algorithmic bytes per launch
                 (n_local x 2 x (key + value bytes)) / its mean duration from
                 hipEvents recorded on the sort's stream during the timed steps
   cpu_baseline  the oracle's host std::sort on a bounded sample (rank 0, N = 1 only)
@@ -183,7 +183,7 @@ def main():
     hist_ms = sum(t["hist_ms"] for t in tims) / len(tims)
     sort_ms = sum(t["total_ms"] for t in tims) / len(tims)
     n_sorted_local = sorter.last_local_n if world > 1 else n_local
-    kernel_name = (sorter.ops.local if world > 1 else sorter).pass_kernel
+    kernel_name = (sorter.ops.local if world > 1 else sorter).pass_kernel_for(n_sorted_local)
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
 

@@ -46,7 +46,7 @@ SIGNATURES = [
     ("grs_destroy", None, [c_void_p]),
     ("grs_scratch_bytes", c_size_t, [c_void_p]),
     ("grs_rank_mode", c_int, [c_void_p]),
-    ("grs_pass_kernel", c_char_p, [c_void_p]),
+    ("grs_pass_kernel", c_char_p, [c_void_p, c_size_t]),
     ("grs_sort", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     ("grs_sort_bits", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
     ("grs_set_profiling", c_int, [c_void_p, c_int]),

@@ -181,11 +181,12 @@ struct grs_sorter {
   // the pass 1 % faster but the next histogram 20 % slower (106.5 vs 104.2 Gkeys/s), so off.
   bool v3_dma_nt = false;
   int hist_grid_cap = 1024;             // GRS_HIST_GRID: cap of the upfront histogram grid
-  // GRS_U32_PASS (u32 keys without payload): 3 = ar512x72 (default), 0 = v3, 1 = ar1024,
-  // 2 = ar512.  Same box, same process, 2^27 keys (tools/ab_u32_pass.sh): v3 105.4, ar1024
-  // 109.5, ar512x72 109.8 Gkeys/s (pass 0.273 / 0.266 / 0.266 ms; the histogram after a
-  // one-tile-per-workgroup pass also runs 0.02 ms faster).
-  int u32_pass = 3;
+  // GRS_U32_PASS (u32 keys without payload): -1 = auto (default), 0 = v3, 1 = ar1024,
+  // 2 = ar512, 3 = ar512x72.  Same box, same process (tools/ab_u32_pass.sh, ab_u32_size.sh):
+  // at 2^27 keys v3 105.4, ar1024 109.5, ar512x72 109.8 Gkeys/s; but a one-tile-per-workgroup
+  // grid of 36K-key tiles has a tail: at 2^24 / 2^25 / 2^26 keys v3 wins (77 / 89 / 97 vs
+  // 53 / 71 / 87 Gkeys/s).  Auto = ar512x72 from 12 tiles per resident v3 workgroup (CU) up.
+  int u32_pass = -1;
 };
 
 extern "C" {
@@ -274,10 +275,11 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_V3_DMA")) s->v3_dma_nt = std::strcmp(e, "nt") == 0;
   if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("GRS_U32_PASS"))
-    s->u32_pass = std::strcmp(e, "v3") == 0       ? 0
-                  : std::strcmp(e, "ar1024") == 0 ? 1
-                  : std::strcmp(e, "ar512") == 0  ? 2
-                                                  : 3;
+    s->u32_pass = std::strcmp(e, "v3") == 0         ? 0
+                  : std::strcmp(e, "ar1024") == 0   ? 1
+                  : std::strcmp(e, "ar512") == 0    ? 2
+                  : std::strcmp(e, "ar512x72") == 0 ? 3
+                                                    : -1;
   grs_status st = GRS_OK;
   auto alloc = [&](void** p, size_t bytes) {
     if (st != GRS_OK) return;
@@ -343,13 +345,22 @@ namespace {
 // order probe failed (or GRS_RANK=match).
 enum class PassKind { V3, AR, MATCH, AR1024, AR512, AR512X72 };
 
+// u32 keys without payload, GRS_U32_PASS unset: the 36K-tile pass once the grid has >= 12
+// tiles per CU (its tail is then small), the persistent v3 pass below that
+int u32_pass_for(const grs_sorter* s, size_t n) {
+  if (s->u32_pass >= 0) return s->u32_pass;
+  const size_t tiles = (n + BigCfg<512, 72>::TILE - 1) / BigCfg<512, 72>::TILE;
+  return tiles >= 12 * static_cast<size_t>(std::max(1, s->v3_grid)) ? 3 : 0;
+}
+
 template <typename K, bool PAIRS>
-PassKind pass_kind(const grs_sorter* s) {
+PassKind pass_kind(const grs_sorter* s, size_t n) {
   if (s->rank_mode != 0) return PassKind::MATCH;
+  const int u32_pass = u32_pass_for(s, n);
   if (!PAIRS && sizeof(K) == 4)
-    return s->u32_pass == 1   ? PassKind::AR1024
-           : s->u32_pass == 2 ? PassKind::AR512
-           : s->u32_pass == 3 ? PassKind::AR512X72
+    return u32_pass == 1   ? PassKind::AR1024
+           : u32_pass == 2 ? PassKind::AR512
+           : u32_pass == 3 ? PassKind::AR512X72
                               : PassKind::V3;
   return PassKind::AR;
 }
@@ -359,7 +370,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
                     int end_bit, hipStream_t stream) {
   using Cfg = TileCfg<K, PAIRS, RB>;
   constexpr int RADIX = 1 << RB;
-  const PassKind kind = pass_kind<K, PAIRS>(s);
+  const PassKind kind = pass_kind<K, PAIRS>(s, n);
   const int passes = (end_bit - begin_bit + RB - 1) / RB;
   const uint32_t tile = kind == PassKind::V3       ? V3Cfg::TILE
                         : kind == PassKind::AR1024 ? BigCfg<1024, 32>::TILE
@@ -962,10 +973,10 @@ grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
   return r;
 }
 
-const char* grs_pass_kernel(const grs_sorter* s) {
+const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
   if (!s) return "";
   if (s->rank_mode != 0) return "grs_onesweep_pass";
-  if (s->key_type == GRS_KEY_U32 && !s->pairs && s->u32_pass == 0) return "grs_onesweep_v3";
+  if (s->key_type == GRS_KEY_U32 && !s->pairs && u32_pass_for(s, n) == 0) return "grs_onesweep_v3";
   return "grs_onesweep_ar";
 }
 

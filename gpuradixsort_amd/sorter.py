@@ -73,8 +73,12 @@ class RadixSorter:
 
     @property
     def pass_kernel(self) -> str:
-        """Name of the pass kernel a sort() call launches (profiling / roofline reports)."""
-        return lib().grs_pass_kernel(self._h).decode()
+        """Name of the pass kernel a sort() of `capacity` items launches (roofline reports)."""
+        return self.pass_kernel_for(self.capacity)
+
+    def pass_kernel_for(self, n: int) -> str:
+        """Name of the pass kernel a sort() of n items launches (grs_pass_kernel)."""
+        return lib().grs_pass_kernel(self._h, int(n)).decode()
 
     def _check_keys(self, keys: torch.Tensor, vals: Optional[torch.Tensor]) -> None:
         if not keys.is_cuda or not keys.is_contiguous():

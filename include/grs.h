@@ -89,10 +89,11 @@ size_t grs_scratch_bytes(const grs_sorter* s);
  * environment variable GRS_RANK=match was set at grs_create).  -1 for a NULL sorter. */
 int grs_rank_mode(const grs_sorter* s);
 
-/* Name of the pass kernel this sorter's sorts launch ("grs_onesweep_ar" by default,
- * "grs_onesweep_v3" with GRS_U32_PASS=v3 for u32 keys, "grs_onesweep_pass" on the ballot-match
- * fallback): what profiling and roofline reports attribute the pass time to. */
-const char* grs_pass_kernel(const grs_sorter* s);
+/* Name of the pass kernel a sort of n items launches: "grs_onesweep_ar" (pairs, u64 keys,
+ * and u32 keys from 12 tiles of 36K keys per CU up), "grs_onesweep_v3" (smaller u32 sorts, or
+ * GRS_U32_PASS=v3), "grs_onesweep_pass" (ballot-match fallback): what profiling and roofline
+ * reports attribute the pass time to. */
+const char* grs_pass_kernel(const grs_sorter* s, size_t n);
 
 /* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a
  * payload, d_vals[0..n) is permuted with its keys (d_vals may be NULL otherwise).

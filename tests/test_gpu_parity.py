@@ -109,7 +109,8 @@ def test_rank_mode_is_atomic_on_gfx950(gpu):
     """The LDS lane-order probe passes on MI355X, so the atomic-rank passes (v3 / ar) run."""
     s = sorter(32, False, 8, 1 << 20)
     assert s.rank_mode == "atomic"
-    assert s.pass_kernel == "grs_onesweep_ar"      # u32 keys: 512 x 72 tiles by default
+    assert s.pass_kernel_for(1 << 20) == "grs_onesweep_v3"     # small u32 sorts: persistent v3
+    assert s.pass_kernel_for(1 << 27) == "grs_onesweep_ar"     # large: 36K-key tiles
     assert sorter(32, True, 8, 1 << 20).pass_kernel == "grs_onesweep_ar"
 
 
@@ -153,11 +154,11 @@ def test_ballot_match_fallback(gpu, monkeypatch):
         s.close()
 
 
-@pytest.mark.parametrize("choice", ["v3", "ar1024", "ar512"])
+@pytest.mark.parametrize("choice", ["v3", "ar1024", "ar512", "ar512x72"])
 def test_u32_pass_alternatives(gpu, monkeypatch, choice):
-    """GRS_U32_PASS selects the other u32 keys-only pass kernels (the persistent v3 pass and
-    the 1024 x 32 / 512 x 64 one-tile passes, kept for A/B measurements): same bit-exact
-    results, across tile edges and both digit widths."""
+    """GRS_U32_PASS pins one u32 keys-only pass kernel whatever the size (the persistent v3
+    pass, and the 1024 x 32 / 512 x 64 / 512 x 72 one-tile passes): same bit-exact results,
+    across tile edges and both digit widths."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_U32_PASS", choice)
