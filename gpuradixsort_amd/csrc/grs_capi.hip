@@ -46,8 +46,9 @@ struct TileCfg {
   // digit runs per tile, fewer look-back steps.  Lab (2^27, ms per pass, two sweeps):
   // u32 pairs 16 / 24 / 32 items 0.55 / 0.53-0.60 / 0.56; u64 keys 16 / 24 / 32 items
   // 0.56 / 0.53-0.56 / 0.51; u64 pairs 8 / 12 / 16 / 24 items 1.02 / 0.90-0.96 / 0.81-0.87 /
-  // 0.80; bench C3 48 -> 55 Gkeys/s and C5 28.5 -> 30 going to 24 / 24 / 16 items.
-  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 24 : 32) : (PAIRS ? 32 : 24);
+  // 0.80; bench C3 48 -> 55 Gkeys/s and C5 28.5 -> 30 going to 24 / 24 / 16 items; 36 items
+  // (147 KB) another 1-2 % over 32 for u32 pairs and u64 keys (15 interleaved rounds).
+  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 24 : 36) : (PAIRS ? 36 : 24);
   static constexpr int TILE = BLOCK * ITEMS;
 };
 

@@ -130,7 +130,7 @@ int lab_ar(int kb, int pairs, int block, int items, int dbg, int grid, const voi
     A(64, 1, 512, 16, 0) A(32, 1, 1024, 12, 0) A(64, 0, 1024, 12, 0)
     A(32, 1, 512, 32, 0) A(64, 0, 512, 32, 0) A(64, 1, 512, 24, 0) A(32, 1, 1024, 16, 0)
     A(64, 0, 1024, 16, 0) A(32, 0, 1024, 32, 0) A(32, 0, 512, 64, 0) A(32, 0, 512, 48, 0)
-    A(32, 0, 1024, 24, 0)
+    A(32, 0, 1024, 24, 0) A(32, 1, 512, 36, 0) A(64, 0, 512, 36, 0)
     A(32, 0, 512, 24, 8192) A(32, 0, 512, 16, 8192) A(32, 0, 1024, 16, 8192)
     A(32, 0, 512, 24, 8) A(32, 0, 512, 16, 8) A(32, 0, 1024, 16, 8)
     A(32, 0, 512, 24, 16) A(32, 0, 1024, 16, 16)
