@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_stream(
 }
 
 // ----------------------------------------------------------------------------------------
-// atomic-rank onesweep pass (default path)
+// atomic-rank onesweep pass (the library default: every key type, tiles as large as LDS allows)
 // ----------------------------------------------------------------------------------------
 //
 // Ranking by ONE returning LDS atomic per key: lane l of wave w adds 1 to the wave's counter
@@ -1838,7 +1838,7 @@ __global__ __launch_bounds__(BLOCK) void grs_onesweep_ar2(
 }
 
 // ----------------------------------------------------------------------------------------
-// v3 onesweep pass (the library's default): persistent workgroups, LDS-DMA double-buffered
+// v3 onesweep pass (u32 keys below 12 tiles of 36K keys per CU, or GRS_U32_PASS=v3): persistent workgroups, LDS-DMA double-buffered
 // tiles, ranking by lane-ordered LDS atomics, hierarchical look-back overlapped with the
 // LDS reorder
 // ----------------------------------------------------------------------------------------
