@@ -15,6 +15,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "../../include/grs.h"
 #include "grs_config.h"
@@ -188,6 +189,7 @@ struct grs_sorter {
   // grid of 36K-key tiles has a tail: at 2^24 / 2^25 / 2^26 keys v3 wins (77 / 89 / 97 vs
   // 53 / 71 / 87 Gkeys/s).  Auto = ar512x72 from 12 tiles per resident v3 workgroup (CU) up.
   int u32_pass = -1;
+  bool part_match = false;              // GRS_PART_RANK=match: ballot-match partition pass
 };
 
 extern "C" {
@@ -275,6 +277,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   }
   if (const char* e = std::getenv("GRS_V3_DMA")) s->v3_dma_nt = std::strcmp(e, "nt") == 0;
   if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("GRS_PART_RANK")) s->part_match = std::strcmp(e, "match") == 0;
   if (const char* e = std::getenv("GRS_U32_PASS"))
     s->u32_pass = std::strcmp(e, "v3") == 0         ? 0
                   : std::strcmp(e, "ar1024") == 0   ? 1
@@ -494,11 +497,38 @@ grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* 
   uint32_t* hist = s->ctrl;
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
   const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
-  hipLaunchKernelGGL((grs::grs_digit_hist<K, grs::SplitterDigit<K>>), dim3(grid),
-                     dim3(GRS_HIST_BLOCK), 0, stream, keys, n, dig, hist, s->status,
-                     static_cast<uint32_t>(words));
+  if (count == 7) {
+    grs::SplitterDigitN<K, 7> d7{};
+    d7.count = 7;
+    for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) d7.s[i] = dig.s[i];
+    hipLaunchKernelGGL((grs::grs_digit_hist<K, grs::SplitterDigitN<K, 7>>), dim3(grid),
+                       dim3(GRS_HIST_BLOCK), 0, stream, keys, n, d7, hist, s->status,
+                       static_cast<uint32_t>(words));
+  } else {
+    hipLaunchKernelGGL((grs::grs_digit_hist<K, grs::SplitterDigit<K>>), dim3(grid),
+                       dim3(GRS_HIST_BLOCK), 0, stream, keys, n, dig, hist, s->status,
+                       static_cast<uint32_t>(words));
+  }
   GRS_HIP(hipGetLastError());
-  if (s->rank_mode == 0)
+  // power-of-two rank counts get a compile-time splitter count (unrolled in SGPRs)
+  auto fixed = [&](auto nconst) {
+    constexpr int N = decltype(nconst)::value;
+    grs::SplitterDigitN<K, N> dn{};
+    dn.count = N;
+    for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) dn.s[i] = dig.s[i];
+    hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
+                                             grs::SplitterDigitN<K, N>>),
+                       dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
+                       dn, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
+                       s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
+  };
+  if (s->rank_mode == 0 && !s->part_match && count == 7)
+    fixed(std::integral_constant<int, 7>{});
+  else if (s->rank_mode == 0 && !s->part_match && count == 3)
+    fixed(std::integral_constant<int, 3>{});
+  else if (s->rank_mode == 0 && !s->part_match && count == 1)
+    fixed(std::integral_constant<int, 1>{});
+  else if (s->rank_mode == 0 && !s->part_match)
     hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
                                              grs::SplitterDigit<K>>),
                        dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,

@@ -60,6 +60,21 @@ struct SplitterDigit {
   __device__ __forceinline__ uint32_t max_digit() const { return count; }
 };
 
+// The same bucket function with the splitter count fixed at compile time (N = G - 1 for
+// G = 2, 4, 8, 16 ranks): fully unrolled, no predicate, the splitters stay in SGPRs.
+template <typename K, int N>
+struct SplitterDigitN {
+  uint32_t count;   // == N (kept for layout compatibility with SplitterDigit)
+  K s[GRS_MAX_SPLITTERS];
+  __device__ __forceinline__ uint32_t operator()(K k) const {
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) b += s[i] <= k;
+    return b;
+  }
+  __device__ __forceinline__ uint32_t max_digit() const { return N; }
+};
+
 // Number of set bits of `m` in lanes strictly below this lane.
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -212,21 +227,30 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
   }
 }
 
-// Histogram of one digit functor (the bucket sizes of a key-range partition).
+// Histogram of one digit functor (the bucket sizes of a key-range partition).  At most 16
+// buckets, so one counter per bucket would take 64 same-address lanes per wave-instruction
+// (serialised): lane l adds into its own copy, s_hist[bucket][l] — bank (64·bucket + l) mod
+// 32 differs across each 32-lane group, so every add is conflict-free.
 template <typename K, typename DigitF>
 __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_digit_hist(
     const K* __restrict__ keys, uint32_t n, const DigitF dig, uint32_t* __restrict__ g_hist,
     uint32_t* __restrict__ clear, uint32_t clear_words) {
-  __shared__ uint32_t s_hist[GRS_MAX_SPLITTERS + 1];
+  constexpr int NB = GRS_MAX_SPLITTERS + 1;
+  __shared__ uint32_t s_hist[NB * GRS_WAVE];
   const uint32_t t = threadIdx.x;
-  if (t <= GRS_MAX_SPLITTERS) s_hist[t] = 0;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  for (uint32_t i = t; i < static_cast<uint32_t>(NB * GRS_WAVE); i += GRS_HIST_BLOCK) s_hist[i] = 0;
   for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < clear_words; i += gridDim.x * GRS_HIST_BLOCK)
     clear[i] = 0;
   __syncthreads();
   for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < n; i += gridDim.x * GRS_HIST_BLOCK)
-    atomicAdd(&s_hist[dig(keys[i])], 1u);
+    atomicAdd(&s_hist[dig(keys[i]) * GRS_WAVE + lane], 1u);
   __syncthreads();
-  if (t <= GRS_MAX_SPLITTERS && s_hist[t]) atomicAdd(&g_hist[t], s_hist[t]);
+  if (t < static_cast<uint32_t>(NB)) {
+    uint32_t c = 0;
+    for (int l = 0; l < GRS_WAVE; ++l) c += s_hist[t * GRS_WAVE + ((l + t) & (GRS_WAVE - 1))];
+    if (c) atomicAdd(&g_hist[t], c);
+  }
 }
 
 // ----------------------------------------------------------------------------------------
