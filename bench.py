@@ -7,17 +7,17 @@ A step = one complete sort of one batch of synthetic keys already resident in HB
 (key[i] = splitmix64(seed ^ global_i)).  Every step sorts its OWN unsorted
 buffer (generated before the timed region), so nothing is restored or skipped inside it.
 
-Default workload (config c4, the one the metric "Gkeys/s (uint32) at 1/2/4/8 MI355X" is
-quoted on): 2^27 uniform uint32 keys per GPU (weak scaling; at 8 GPUs this is BASELINE
-config 4, 2^30 keys), 8-bit digits.  At N = 1 it is a plain single-GPU sort; at N > 1 each
-rank range-partitions its shard, exchanges buckets with one RCCL all-to-all-v over xGMI and
-sorts what it received (gpuradixsort_amd/sharded.py).
+Default workload: BASELINE config C4 itself, 2^30 uniform uint32 keys in total, 8-bit digits,
+STRONG scaling: at N = 1 one MI355X sorts all 2^30 keys in one call; at N > 1 rank r holds
+2^30 / N keys and the sort is grs_sort_sharded (range partition, one RCCL all-to-all over
+xGMI, local sort; gpuradixsort_amd/sharded.py).  `value` = 2^30 keys x steps / wall time.
 
 Rank 0 prints ONE JSON line with the driver contract plus:
-  roofline      dominant kernel (the pass kernel the sorter reports, grs_pass_kernel():
-                grs_onesweep_ar by default): algorithmic bytes per launch
+  roofline      dominant kernel (grs_onesweep_v4, the pass): algorithmic bytes per launch
                 (n_local x 2 x (key + value bytes)) / its mean duration from
-                hipEvents recorded on the sort's stream during the timed steps
+                hipEvents recorded on the sort's stream during the timed steps; `traffic` is
+                the PMC-measured HBM bytes per launch when --traffic-json names the output of
+                tools/bench_pmc.py for this same workload (null otherwise)
   cpu_baseline  the oracle's host std::sort on a bounded sample (rank 0, N = 1 only)
 """
 from __future__ import annotations
@@ -38,9 +38,10 @@ METRIC = "Gkeys/s (uint32) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 
 CONFIGS = {
-    # name: (config_id, keys per GPU, key_bits, pairs, radix_bits, description)
-    "c4": (4, 1 << 27, 32, False, 8, "C4: uint32 keys, 2^27 per GPU (2^30 at 8 GPUs), 8-bit LSD, "
-                                     "range partition + RCCL all-to-all-v"),
+    # name: (config_id, total keys (c4: strong scaling) or keys per GPU, key_bits, pairs,
+    #        radix_bits, description)
+    "c4": (4, 1 << 30, 32, False, 8, "C4: 2^30 uint32 keys in total (strong scaling: 2^30 / N per "
+                                     "GPU), 8-bit LSD; N > 1: range partition + one RCCL all-to-all"),
     "c2": (2, 1 << 24, 32, False, 4, "C2: 16M uint32 keys, 4-bit-digit LSD"),
     "c3": (3, 1 << 28, 32, True, 8, "C3: 256M uint32 key + uint32 payload, stable"),
     "c5": (5, 1 << 28, 64, False, 8, "C5: 256M uint64 keys, 8 x 8-bit passes"),
@@ -53,7 +54,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="override keys per GPU")
+    ap.add_argument("--n", type=int, default=0, help="override the total (c4) / per-GPU key count")
+    ap.add_argument("--traffic-json", default="", help="tools/bench_pmc.py output of this workload")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--pool-gib", type=float, default=96.0,
@@ -110,9 +112,11 @@ def main():
 
     import gpuradixsort_amd as grs
 
-    cid, n_local, kb, pairs, rb, desc = CONFIGS[a.config]
+    cid, n_cfg, kb, pairs, rb, desc = CONFIGS[a.config]
     if a.n:
-        n_local = a.n
+        n_cfg = a.n
+    strong = a.config == "c4"
+    n_local = n_cfg // world if strong else n_cfg
     seed = (0x6A09E667F3BCC908 + cid) & ((1 << 64) - 1)
     kdt = torch.uint32 if kb == 32 else torch.uint64
     step_bytes = n_local * (kb // 8 + (4 if pairs else 0))
@@ -142,14 +146,16 @@ def main():
     else:
         from gpuradixsort_amd.sharded import ShardedSorter
 
-        sorter = ShardedSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb)
+        sorter = ShardedSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb, device=dev)
         sorter.set_profiling(max(1, a.steps))
 
         def step(i):
             k = keys_pool[i % pool]
             if i >= pool:
                 grs.fill_splitmix(k, seed, first_index=i * n_total + rank * n_local)
-            sorter.sort(k, vals_pool[i % pool] if pairs else None)
+            # the exchange synchronises once per call (the counts); the timeout check of the
+            # local sort happens after the timed region (bench.py reads the error word below)
+            sorter.sort(k, vals_pool[i % pool] if pairs else None, check_error=False)
 
     def barrier():
         torch.cuda.synchronize()
@@ -171,10 +177,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # look-back timeouts of the timed steps surface here (error word; raises GrsError)
+    (sorter.sorter if world > 1 else sorter).check_error()
     # correctness of the last timed step (cheap property: sortedness on device)
     last = (a.warmup + a.steps - 1) % pool
-    inversions = sorter.count_inversions(keys_pool[last]) if world > 1 else \
-        grs.count_inversions(keys_pool[last])
+    inversions = sorter.count_inversions() if world > 1 else grs.count_inversions(keys_pool[last])
 
     # per-phase GPU times over the timed steps (hipEvents on the sort's stream)
     tims = [sorter.timing(k) for k in range(min(a.steps, pool))]
@@ -182,8 +189,8 @@ def main():
     mean_pass_ms = sum(pass_ms) / len(pass_ms)
     hist_ms = sum(t["hist_ms"] for t in tims) / len(tims)
     sort_ms = sum(t["total_ms"] for t in tims) / len(tims)
-    n_sorted_local = sorter.last_local_n if world > 1 else n_local
-    kernel_name = (sorter.ops.local if world > 1 else sorter).pass_kernel_for(n_sorted_local)
+    n_sorted_local = sorter.last_n_out if world > 1 else n_local
+    kernel_name = (sorter.sorter if world > 1 else sorter).pass_kernel_for(n_sorted_local)
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
 
@@ -191,11 +198,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(min(a.cpu_sample, n_local), kb, pairs, seed)
 
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        rec = json.load(open(pmc_path)).get(f"{a.config}:{n_sorted_local}")
-        if rec:
+    traffic = None   # PMC bytes need a separate rocprofv3 --pmc run (tools/bench_pmc.py)
+    if a.traffic_json and os.path.exists(a.traffic_json):
+        rec = json.load(open(a.traffic_json))
+        if rec.get("n") == n_sorted_local and rec.get("config") == a.config:
             traffic = rec.get("hbm_bytes_per_launch")
 
     sort_alg = n_local * 2 * tims[0]["passes"] * (kb // 8 + (4 if pairs else 0))
@@ -205,7 +211,7 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "Gkeys/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32" if kb == 32 else "u64",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32" if kb == 32 else "u64",
             "data": "synthetic: splitmix64(seed ^ global_index) uniform keys, a distinct unsorted "
                     "buffer per step resident in HBM" + ("; payload = global index" if pairs else ""),
             "config": {"workload": desc, "keys_per_gpu": n_local, "total_keys": n_total,
@@ -227,7 +233,7 @@ def main():
             "check": {"inversions_last_step": inversions},
         }
         if world > 1:
-            out["phases_ms"].update(sorter.phase_summary())
+            out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

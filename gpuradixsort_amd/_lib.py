@@ -18,16 +18,17 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libgrs.so")
 
-GRS_OK, GRS_EINVAL, GRS_ENOMEM, GRS_EHIP, GRS_ECAPACITY, GRS_ENODEV, GRS_ETIMEOUT = range(7)
+GRS_OK, GRS_EINVAL, GRS_ENOMEM, GRS_EHIP, GRS_ECAPACITY, GRS_ENODEV, GRS_ETIMEOUT, GRS_ERCCL = range(8)
 GRS_KEY_U32, GRS_KEY_U64 = 0, 1
-GRS_MAX_N = (1 << 30) - 1
+GRS_RCCL_ID_BYTES = 128
+GRS_MAX_N = (1 << 32) - (1 << 16)
 
 
 class GrsError(RuntimeError):
     def __init__(self, status: int, what: str, detail: str = ""):
         self.status = status
         names = ["GRS_OK", "GRS_EINVAL", "GRS_ENOMEM", "GRS_EHIP", "GRS_ECAPACITY", "GRS_ENODEV",
-                 "GRS_ETIMEOUT"]
+                 "GRS_ETIMEOUT", "GRS_ERCCL"]
         name = names[status] if 0 <= status < len(names) else str(status)
         super().__init__(f"{what}: {name}" + (f" ({detail})" if detail else ""))
 
@@ -53,8 +54,21 @@ SIGNATURES = [
     ("grs_last_timing", c_int, [c_void_p, POINTER(grs_timing)]),
     ("grs_timing_history", c_int, [c_void_p, c_int, POINTER(grs_timing)]),
     ("grs_check_error", c_int, [c_void_p]),
+    ("grs_stream_check_error", c_int, [c_void_p, c_void_p]),
     ("grs_partition", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                               c_int, c_void_p, c_void_p]),
+    ("grs_partition_ranges", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                     c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("grs_sort_sharded", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                 c_size_t, POINTER(c_size_t), c_void_p, c_void_p]),
+    ("grs_rccl_unique_id", c_int, [c_void_p]),
+    ("grs_rccl_comm_init", c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int]),
+    ("grs_rccl_comm_destroy", None, [c_void_p]),
+    ("grs_shard_splitters_host", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                         c_void_p, c_void_p]),
+    ("grs_shard_plan_host", c_int, [c_void_p, c_int, c_int, POINTER(c_uint64), POINTER(c_uint64),
+                                    POINTER(c_uint64)]),
+    ("grs_shard_samples_per_rank", c_int, [c_int]),
     ("grs_iota_u32", c_int, [c_void_p, c_size_t, c_uint32, c_void_p]),
     ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),

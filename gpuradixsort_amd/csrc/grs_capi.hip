@@ -20,6 +20,10 @@
 #include "../../include/grs.h"
 #include "grs_config.h"
 #include "grs_kernels.hpp"
+#include "grs_pass.hpp"
+#include "grs_shard.hpp"
+
+#include <rccl/rccl.h>
 
 namespace {
 
@@ -37,53 +41,38 @@ grs_status set_err(grs_status s, const std::string& msg) {
       return set_err(GRS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
-// Tile geometry per (key type, payload, radix) of the one-tile-per-workgroup passes (the
-// atomic-rank pass grs_onesweep_ar and the ballot-match fallback grs_onesweep_pass).
-// ITEMS keys per thread, GRS_BLOCK threads; measured on MI355X (tools/lab.py).
-template <typename K, bool PAIRS, int RB>
-struct TileCfg {
-  static constexpr int BLOCK = GRS_BLOCK;
-  // The largest tiles that fit one workgroup's LDS (128-144 KB of keys + payload): longer
-  // digit runs per tile, fewer look-back steps.  Lab (2^27, ms per pass, two sweeps):
-  // u32 pairs 16 / 24 / 32 items 0.55 / 0.53-0.60 / 0.56; u64 keys 16 / 24 / 32 items
-  // 0.56 / 0.53-0.56 / 0.51; u64 pairs 8 / 12 / 16 / 24 items 1.02 / 0.90-0.96 / 0.81-0.87 /
-  // 0.80; bench C3 48 -> 55 Gkeys/s and C5 28.5 -> 30 going to 24 / 24 / 16 items; 36 items
-  // (147 KB) another 1-2 % over 32 for u32 pairs and u64 keys (15 interleaved rounds).
-  static constexpr int ITEMS = sizeof(K) == 8 ? (PAIRS ? 24 : 36) : (PAIRS ? 36 : 24);
+// Tile shapes of the pass (grs_onesweep_v4, grs_pass.hpp).  Measured on MI355X
+// (tools/lab2.py, 2^27 keys, ms per pass against the round-1 512-thread pass on the same box:
+// u32 keys 0.249 vs 0.290, u32 pairs 0.505 vs 0.557, u64 keys 0.479 vs 0.514, u64 pairs
+// 0.798 vs 0.790): 16 waves per workgroup and the largest tile that fits LDS beside the
+// 16 x RADIX wave counters.  Big: one 1024-thread workgroup per CU.  Small (grids of few big
+// tiles per CU, e.g. BASELINE C2's 16M keys): 256-thread workgroups of 4K-16K keys, four per
+// CU, so the grid has no tail.
+template <typename K, bool PAIRS>
+struct BigTile {
+  static constexpr int BLOCK = 1024, MINW = 1;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 32) : (PAIRS ? 10 : 16);
   static constexpr int TILE = BLOCK * ITEMS;
 };
-
-// The persistent pass grs_onesweep_v3 (u32 keys without payload): 16 waves x 16 keys, one
-// workgroup per CU (double-buffered 64 KB tiles in LDS).  Smaller v3 tiles, or v3 with a
-// payload or u64 keys (8K- or 4K-key tiles), measured 2-6x slower: a workgroup holds the
-// ticket of the tile it prefetches for a whole iteration, and with more, shorter tiles in
-// flight later tiles' look-backs wait on those held tiles.
-struct V3Cfg {
-  static constexpr int BLOCK = 1024;
-  static constexpr int ITEMS = 16;
+template <typename K, bool PAIRS>
+struct SmallTile {
+  static constexpr int BLOCK = 256, MINW = 4;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 8 : 16) : (PAIRS ? 6 : 8);
   static constexpr int TILE = BLOCK * ITEMS;
 };
-
-// One-tile-per-workgroup atomic-rank pass with 32K-36K-key tiles for u32 keys without payload
-// (the default, 512 x 72; GRS_U32_PASS=ar1024 / ar512 select 1024 x 32 / 512 x 64): longer
-// digit runs per tile beat v3's prefetching of 16K-key tiles (lab 0.276 vs 0.285 ms per pass,
-// in the sort 109.8 vs 105.4 Gkeys/s).
-template <int B, int I>
-struct BigCfg {
-  static constexpr int BLOCK = B;
-  static constexpr int ITEMS = I;
-  static constexpr int TILE = B * I;
+// Partition pass (key-range buckets for the multi-GPU exchange): its digit needs the element
+// index, so the reordered digits are kept in LDS (one byte per key) beside the tile.
+template <typename K, bool PAIRS>
+struct PartTile {
+  static constexpr int BLOCK = 1024, MINW = 1;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 24) : (PAIRS ? 8 : 16);
+  static constexpr int TILE = BLOCK * ITEMS;
 };
+constexpr uint32_t kPassOpt = 128;                     // nontemporal tile loads (grs_pass.hpp)
+constexpr uint32_t kMatchOpt = 128 | 512;              // + ballot-match ranking (fallback)
 
-constexpr int max_tile_min() { return 2048; }  // smallest TILE over configs (sizes status)
-
-// Status words of one look-back buffer for `tiles` tiles: the larger of the one-tile passes'
-// layout (tile words + group accumulators + group INCLUSIVE words) and v3's (tile words +
-// group + 2 x supergroup words).
-size_t status_words_for(size_t tiles, size_t radix) {
-  const size_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
-  return std::max((tiles + 2 * groups) * radix, grs::hier_status_words(tiles, radix));
-}
+// Status words of one look-back buffer for `tiles` tiles of radix `radix`.
+size_t status_words_for(size_t tiles, size_t radix) { return grs::lb3_status_words(tiles, radix); }
 
 // Probe of the property the atomic-rank passes rely on: the lanes of ONE returning ds_add
 // wave-instruction that hit one LDS address get their old values in ascending lane order
@@ -156,14 +145,15 @@ struct grs_sorter {
   grs_key_type key_type = GRS_KEY_U32;
   int pairs = 0;
   int radix_bits = 8;
-  int rank_mode = 0;               // 0: atomic ranking (v3 / ar passes), 1: ballot-match fallback
-  int v3_grid = 0;                 // resident v3 workgroups (CUs x blocks per CU)
+  int rank_mode = 0;               // 0: lane-ordered LDS atomics, 1: ballot-match fallback
+  int cus = 0;                     // compute units of the device
   size_t capacity = 0;
   void* alt_keys = nullptr;
   uint32_t* alt_vals = nullptr;
   uint32_t* status = nullptr;      // 2 x status_words
   size_t status_words = 0;         // per buffer
   uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
+  uint32_t* h_err = nullptr;       // pinned host word: the error word read back by checked calls
   size_t scratch_bytes = 0;
   // Profiling ring: the last `ring` calls keep their per-phase hipEvents.
   static constexpr int EV_PER_CALL = GRS_MAX_PASSES + 3;
@@ -178,18 +168,14 @@ struct grs_sorter {
   grs_sorter* seg64 = nullptr;     // u64 pair sorter of (segment << 32 | key), u32 keys only
   void* host_stage = nullptr;      // grs_sort_host device staging (keys | payload), on first use
   size_t host_stage_bytes = 0;
+  // grs_sort_sharded scratch (first use): samples, gathered samples, count matrix, digit
+  void* shard_buf = nullptr;
+  size_t shard_bytes = 0;
+  uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
-  // GRS_V3_DMA=nt: nontemporal tile DMA.  One box, same process (tools/ab_v3_dma.sh): nt made
-  // the pass 1 % faster but the next histogram 20 % slower (106.5 vs 104.2 Gkeys/s), so off.
-  bool v3_dma_nt = false;
-  int hist_grid_cap = 1024;             // GRS_HIST_GRID: cap of the upfront histogram grid
-  // GRS_U32_PASS (u32 keys without payload): -1 = auto (default), 0 = v3, 1 = ar1024,
-  // 2 = ar512, 3 = ar512x72.  Same box, same process (tools/ab_u32_pass.sh, ab_u32_size.sh):
-  // at 2^27 keys v3 105.4, ar1024 109.5, ar512x72 109.8 Gkeys/s; but a one-tile-per-workgroup
-  // grid of 36K-key tiles has a tail: at 2^24 / 2^25 / 2^26 keys v3 wins (77 / 89 / 97 vs
-  // 53 / 71 / 87 Gkeys/s).  Auto = ar512x72 from 12 tiles per resident v3 workgroup (CU) up.
-  int u32_pass = -1;
-  bool part_match = false;              // GRS_PART_RANK=match: ballot-match partition pass
+  int hist_grid_cap = 1024;        // GRS_HIST_GRID: cap of the upfront histogram grid
+  int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
+  int u32_variant = 0;             // GRS_U32_PASS: u32-keys pass variant (0 = default; lab A/B)
 };
 
 extern "C" {
@@ -205,6 +191,7 @@ const char* grs_status_string(grs_status s) {
     case GRS_ECAPACITY: return "GRS_ECAPACITY";
     case GRS_ENODEV: return "GRS_ENODEV";
     case GRS_ETIMEOUT: return "GRS_ETIMEOUT";
+    case GRS_ERCCL: return "GRS_ERCCL";
   }
   return "GRS_UNKNOWN";
 }
@@ -220,9 +207,12 @@ void grs_destroy(grs_sorter* s) {
   if (s->alt_vals) (void)hipFree(s->alt_vals);
   if (s->status) (void)hipFree(s->status);
   if (s->ctrl) (void)hipFree(s->ctrl);
+  if (s->h_err) (void)hipHostFree(s->h_err);
   if (s->seg_buf) (void)hipFree(s->seg_buf);
   if (s->seg64) grs_destroy(s->seg64);
   if (s->host_stage) (void)hipFree(s->host_stage);
+  if (s->shard_buf) (void)hipFree(s->shard_buf);
+  if (s->shard_host) (void)hipHostFree(s->shard_host);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   delete[] s->ev;
@@ -230,6 +220,34 @@ void grs_destroy(grs_sorter* s) {
   (void)hipSetDevice(prev);
   delete s;
 }
+
+}  // extern "C"
+
+namespace {
+
+// Tiles of the pass a sort of n items launches, and which shape (true = big).
+bool use_big_tiles(const grs_sorter* s, size_t n, size_t big_tile) {
+  if (s->tile_mode >= 0) return s->tile_mode == 1;
+  // a grid of big tiles needs enough tiles per CU for its tail to stay small
+  return (n + big_tile - 1) / big_tile >= 6 * static_cast<size_t>(std::max(1, s->cus));
+}
+
+// Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
+template <typename K, bool PAIRS>
+size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
+  const size_t big = BigTile<K, PAIRS>::TILE, small = SmallTile<K, PAIRS>::TILE;
+  // small tiles are used below 6 big tiles per CU (or everywhere when forced)
+  const size_t small_cap = s->tile_mode == 0 ? cap : std::min(cap, 6 * big * std::max(1, s->cus));
+  size_t w = std::max(status_words_for((cap + big - 1) / big, radix),
+                      status_words_for((small_cap + small - 1) / small, radix));
+  // the partition pass (16 buckets)
+  const size_t part = PartTile<K, PAIRS>::TILE;
+  return std::max(w, status_words_for((cap + part - 1) / part, 16));
+}
+
+}  // namespace
+
+extern "C" {
 
 grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
                       int with_u32_payload, int radix_bits, int device) {
@@ -241,7 +259,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (radix_bits != 4 && radix_bits != 8)
     return set_err(GRS_EINVAL, "grs_create: radix_bits must be 4, 8 or 0");
   if (capacity > GRS_MAX_N)
-    return set_err(GRS_ECAPACITY, "grs_create: capacity exceeds 2^30-1 items per device call");
+    return set_err(GRS_ECAPACITY, "grs_create: capacity exceeds GRS_MAX_N (2^32 - 2^16) items per device call");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return set_err(GRS_ENODEV, "grs_create: no HIP device");
@@ -256,34 +274,21 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   s->pairs = with_u32_payload ? 1 : 0;
   s->radix_bits = radix_bits;
   s->capacity = capacity;
+  s->rank_mode = device_rank_mode(device);
+  (void)hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("GRS_TILE"))
+    s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
+  if (const char* e = std::getenv("GRS_U32_PASS")) s->u32_variant = std::max(0, std::atoi(e));
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(capacity, 1);
-  const size_t tiles = (cap + max_tile_min() - 1) / max_tile_min();
-  s->status_words = status_words_for(tiles, size_t(1) << radix_bits);
-  s->rank_mode = device_rank_mode(device);
-  {
-    int cus = 0, per_cu = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (radix_bits == 8)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void*>(&grs::grs_onesweep_v3<uint32_t, false, 8, V3Cfg::BLOCK, V3Cfg::ITEMS>),
-          V3Cfg::BLOCK, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void*>(&grs::grs_onesweep_v3<uint32_t, false, 4, V3Cfg::BLOCK, V3Cfg::ITEMS>),
-          V3Cfg::BLOCK, 0);
-    (void)hipGetLastError();
-    s->v3_grid = std::max(1, cus) * std::max(1, per_cu);
-  }
-  if (const char* e = std::getenv("GRS_V3_DMA")) s->v3_dma_nt = std::strcmp(e, "nt") == 0;
-  if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("GRS_PART_RANK")) s->part_match = std::strcmp(e, "match") == 0;
-  if (const char* e = std::getenv("GRS_U32_PASS"))
-    s->u32_pass = std::strcmp(e, "v3") == 0         ? 0
-                  : std::strcmp(e, "ar1024") == 0   ? 1
-                  : std::strcmp(e, "ar512") == 0    ? 2
-                  : std::strcmp(e, "ar512x72") == 0 ? 3
-                                                    : -1;
+  const size_t radix = std::max<size_t>(size_t(1) << radix_bits, 16);
+  if (key_type == GRS_KEY_U32)
+    s->status_words = s->pairs ? max_status_words<uint32_t, true>(s, cap, radix)
+                               : max_status_words<uint32_t, false>(s, cap, radix);
+  else
+    s->status_words = s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
+                               : max_status_words<uint64_t, false>(s, cap, radix);
   grs_status st = GRS_OK;
   auto alloc = [&](void** p, size_t bytes) {
     if (st != GRS_OK) return;
@@ -300,6 +305,10 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
   if (st == GRS_OK && hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess)
     st = set_err(GRS_EHIP, "grs_create: hipMemset failed");
+  if (st == GRS_OK && hipHostMalloc(reinterpret_cast<void**>(&s->h_err), 4, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    st = set_err(GRS_ENOMEM, "grs_create: hipHostMalloc failed");
+  }
   (void)hipSetDevice(prev);
   if (st != GRS_OK) {
     grs_destroy(s);
@@ -344,51 +353,43 @@ grs_status grs_set_profiling(grs_sorter* s, int ring) {
 
 namespace {
 
-// Which pass kernel a sort call launches: the persistent v3 pass for u32 keys without payload,
-// the one-tile-per-workgroup atomic-rank pass otherwise, the ballot-match pass if the LDS
-// order probe failed (or GRS_RANK=match).
-enum class PassKind { V3, AR, MATCH, AR1024, AR512, AR512X72 };
-
-// u32 keys without payload, GRS_U32_PASS unset: the 36K-tile pass once the grid has >= 12
-// tiles per CU (its tail is then small), the persistent v3 pass below that
-int u32_pass_for(const grs_sorter* s, size_t n) {
-  if (s->u32_pass >= 0) return s->u32_pass;
-  const size_t tiles = (n + BigCfg<512, 72>::TILE - 1) / BigCfg<512, 72>::TILE;
-  return tiles >= 12 * static_cast<size_t>(std::max(1, s->v3_grid)) ? 3 : 0;
+// One pass launch: grid = tiles, one tile per workgroup (grs_pass.hpp).
+template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, typename DigitF>
+grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
+                       uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
+                       uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream) {
+  const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
+  if (status_words_for(tiles, 1u << RB) > s->status_words)
+    return set_err(GRS_ECAPACITY, "status buffer too small");
+  hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW, OPT,
+                                           DigitF>),
+                     dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
+                     ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
 }
 
-template <typename K, bool PAIRS>
-PassKind pass_kind(const grs_sorter* s, size_t n) {
-  if (s->rank_mode != 0) return PassKind::MATCH;
-  const int u32_pass = u32_pass_for(s, n);
-  if (!PAIRS && sizeof(K) == 4)
-    return u32_pass == 1   ? PassKind::AR1024
-           : u32_pass == 2 ? PassKind::AR512
-           : u32_pass == 3 ? PassKind::AR512X72
-                              : PassKind::V3;
-  return PassKind::AR;
-}
+// Lab variants of the u32-keys pass, selected by GRS_U32_PASS=1..4 at grs_create (A/B only).
+template <int B, int I, int O>
+struct U32Var {
+  static constexpr int BLOCK = B, ITEMS = I, MINW = 1, TILE = B * I, OPT = O;
+};
 
 template <typename K, bool PAIRS, int RB>
 grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begin_bit,
                     int end_bit, hipStream_t stream) {
-  using Cfg = TileCfg<K, PAIRS, RB>;
+  using Big = BigTile<K, PAIRS>;
+  using Small = SmallTile<K, PAIRS>;
   constexpr int RADIX = 1 << RB;
-  const PassKind kind = pass_kind<K, PAIRS>(s, n);
+  const bool big = use_big_tiles(s, n, Big::TILE);
   const int passes = (end_bit - begin_bit + RB - 1) / RB;
-  const uint32_t tile = kind == PassKind::V3       ? V3Cfg::TILE
-                        : kind == PassKind::AR1024 ? BigCfg<1024, 32>::TILE
-                        : kind == PassKind::AR512  ? BigCfg<512, 64>::TILE
-                        : kind == PassKind::AR512X72 ? BigCfg<512, 72>::TILE
-                                                   : Cfg::TILE;
-  const uint32_t tiles = (n + tile - 1) / tile;
+  const uint32_t tiles = (n + (big ? Big::TILE : Small::TILE) - 1) / (big ? Big::TILE : Small::TILE);
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
   uint32_t* st1 = s->status + s->status_words;
   uint32_t* hist = s->ctrl;
   uint32_t* tickets = s->ctrl + GRS_CTRL_TICKETS;
-  uint32_t* err = s->ctrl + GRS_CTRL_ERROR;
   int ev = 0;
   hipEvent_t* evs = s->ring ? s->ev + (s->calls % s->ring) * grs_sorter::EV_PER_CALL : nullptr;
   auto mark = [&]() -> grs_status {
@@ -398,12 +399,11 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
 
   grs_status r;
   if ((r = mark()) != GRS_OK) return r;
-  // zero histograms + tickets (the error word is sticky: only grs_check_error clears it)
+  // zero histograms + tickets (the error word is sticky: only the checks clear it)
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
   {
     // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout)
-    // 1024 blocks: 5 % faster than 2048 alone (tools/histlab.py) and 0.008 ms faster inside
-    // the sort (tools/ab_v3_dma.sh); GRS_HIST_GRID overrides the cap
+    // 1024 blocks: 5 % faster than 2048 alone (tools/histlab.py); GRS_HIST_GRID overrides the cap
     const int grid = std::max<int>((n >> 18) + 1, std::min<int>(s->hist_grid_cap, (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
                        stream, keys, n, begin_bit, end_bit, passes, hist, st0,
@@ -416,49 +416,37 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   K* dst = static_cast<K*>(s->alt_keys);
   uint32_t* vsrc = vals;
   uint32_t* vdst = s->alt_vals;
+  using Dig = grs::RadixDigit<K>;
+  auto u32_lab = [&](bool big_tiles) {
+    if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) return big_tiles && s->u32_variant != 0;
+    else return false;
+  };
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
     const int bits = std::min(RB, end_bit - shift);
     uint32_t* st_cur = (p & 1) ? st1 : st0;
     uint32_t* st_nxt = (p & 1) ? st0 : st1;
-    const grs::RadixDigit<K> dig{shift, (1u << bits) - 1u};
-    if (kind == PassKind::V3) {
-      if constexpr (!PAIRS && sizeof(K) == 4) {
-        const uint32_t grid = std::min<uint32_t>(tiles, static_cast<uint32_t>(s->v3_grid));
-        if (!s->v3_dma_nt)   // default cache policy for the tile DMA (see grs_create)
-          hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS, 128>),
-                             dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
-                             hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
-        else
-          hipLaunchKernelGGL((grs::grs_onesweep_v3<K, false, RB, V3Cfg::BLOCK, V3Cfg::ITEMS>),
-                             dim3(grid), dim3(V3Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig,
-                             hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
+    const Dig dig{shift, (1u << bits) - 1u};
+    const uint32_t* ph = hist + p * RADIX;
+    if (s->rank_mode != 0) {
+      r = big ? launch_pass<K, PAIRS, RB, Big, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream)
+              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream);
+    } else if (u32_lab(big)) {
+      using V1 = U32Var<1024, 32, 144>;   // look-back issued after the reorder
+      using V2 = U32Var<512, 72, 144>;    // 8 waves, 36K-key tiles
+      using V3 = U32Var<1024, 36, 400>;   // 16-bit wave counters, 36K-key tiles
+      using V4 = U32Var<1024, 32, 0>;     // default-policy tile loads
+      if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) switch (s->u32_variant) {
+        case 1: r = launch_pass<K, PAIRS, RB, V1, V1::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
+        case 2: r = launch_pass<K, PAIRS, RB, V2, V2::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
+        case 3: r = launch_pass<K, PAIRS, RB, V3, V3::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
+        default: r = launch_pass<K, PAIRS, RB, V4, V4::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
       }
-    } else if (kind == PassKind::AR1024 || kind == PassKind::AR512 || kind == PassKind::AR512X72) {
-      if constexpr (!PAIRS && sizeof(K) == 4) {
-        if (kind == PassKind::AR512X72)
-          hipLaunchKernelGGL((grs::grs_onesweep_ar<K, false, RB, 512, 72>), dim3(tiles), dim3(512),
-                             0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
-                             tickets + p, st_cur, st_nxt, err);
-        else if (kind == PassKind::AR1024)
-          hipLaunchKernelGGL((grs::grs_onesweep_ar<K, false, RB, 1024, 32>), dim3(tiles),
-                             dim3(1024), 0, stream, src, dst, vsrc, vdst, n, dig,
-                             hist + p * RADIX, tickets + p, st_cur, st_nxt, err);
-        else
-          hipLaunchKernelGGL((grs::grs_onesweep_ar<K, false, RB, 512, 64>), dim3(tiles), dim3(512),
-                             0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
-                             tickets + p, st_cur, st_nxt, err);
-      }
-    } else if (kind == PassKind::AR) {
-      hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
-                         dim3(Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
-                         tickets + p, st_cur, st_nxt, err);
     } else {
-      hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS>), dim3(tiles),
-                         dim3(Cfg::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist + p * RADIX,
-                         tickets + p, st_cur, st_nxt, err);
+      r = big ? launch_pass<K, PAIRS, RB, Big, kPassOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream)
+              : launch_pass<K, PAIRS, RB, Small, kPassOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream);
     }
-    GRS_HIP(hipGetLastError());
+    if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;
     std::swap(src, dst);
     std::swap(vsrc, vdst);
@@ -479,80 +467,71 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   return GRS_OK;
 }
 
-// Stable key-range partition: one histogram launch + one pass with a splitter digit (4-bit
-// slot, up to 16 buckets).  Buckets land contiguously in keys_out/vals_out in bucket order;
-// bucket sizes are copied to d_counts[0..count].
-template <typename K, bool PAIRS>
-grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
-                         uint32_t* vals_out, uint32_t n, const K* splitters, int count,
-                         uint32_t* d_counts, hipStream_t stream) {
-  constexpr int RB = 4;
-  using Cfg = TileCfg<K, PAIRS, RB>;
-  grs::SplitterDigit<K> dig{};
-  dig.count = static_cast<uint32_t>(count);
-  for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) dig.s[i] = i < count ? splitters[i] : K(0);
-  const uint32_t tiles = (n + Cfg::TILE - 1) / Cfg::TILE;
-  const size_t words = status_words_for(tiles, 1u << RB);
+// Stable key-range partition with N (compile-time) splitters: one bucket histogram + one pass
+// whose digit is the bucket (grs::SplitterIdxDigit).  Buckets land contiguously in
+// keys_out / vals_out in bucket order; the count + 1 bucket sizes go to d_counts (device).
+// dig_dev: the functor in device memory (splitters computed on the device) or null.
+template <typename K, bool PAIRS, int N>
+grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
+                           uint32_t* vals_out, uint32_t n, const grs::SplitterIdxDigit<K, N>& dig,
+                           const grs::SplitterIdxDigit<K, N>* dig_dev, int count,
+                           uint32_t* d_counts, hipStream_t stream) {
+  using T = PartTile<K, PAIRS>;
+  using Dig = grs::SplitterIdxDigit<K, N>;
+  const uint32_t tiles = (n + T::TILE - 1) / T::TILE;
+  const size_t words = status_words_for(tiles, 16);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* hist = s->ctrl;
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
   const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
-  if (count == 7) {
-    grs::SplitterDigitN<K, 7> d7{};
-    d7.count = 7;
-    for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) d7.s[i] = dig.s[i];
-    hipLaunchKernelGGL((grs::grs_digit_hist<K, grs::SplitterDigitN<K, 7>>), dim3(grid),
-                       dim3(GRS_HIST_BLOCK), 0, stream, keys, n, d7, hist, s->status,
-                       static_cast<uint32_t>(words));
-  } else {
-    hipLaunchKernelGGL((grs::grs_digit_hist<K, grs::SplitterDigit<K>>), dim3(grid),
-                       dim3(GRS_HIST_BLOCK), 0, stream, keys, n, dig, hist, s->status,
-                       static_cast<uint32_t>(words));
-  }
+  hipLaunchKernelGGL((grs::grs_digit_hist<K, Dig>), dim3(grid), dim3(GRS_HIST_BLOCK), 0, stream,
+                     keys, n, dig, dig_dev, hist, s->status, static_cast<uint32_t>(words));
   GRS_HIP(hipGetLastError());
-  // power-of-two rank counts get a compile-time splitter count (unrolled in SGPRs)
-  auto fixed = [&](auto nconst) {
-    constexpr int N = decltype(nconst)::value;
-    grs::SplitterDigitN<K, N> dn{};
-    dn.count = N;
-    for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) dn.s[i] = dig.s[i];
-    hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
-                                             grs::SplitterDigitN<K, N>>),
-                       dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
-                       dn, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
-                       s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
-  };
-  if (s->rank_mode == 0 && !s->part_match && count == 7)
-    fixed(std::integral_constant<int, 7>{});
-  else if (s->rank_mode == 0 && !s->part_match && count == 3)
-    fixed(std::integral_constant<int, 3>{});
-  else if (s->rank_mode == 0 && !s->part_match && count == 1)
-    fixed(std::integral_constant<int, 1>{});
-  else if (s->rank_mode == 0 && !s->part_match)
-    hipLaunchKernelGGL((grs::grs_onesweep_ar<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
-                                             grs::SplitterDigit<K>>),
-                       dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
-                       dig, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
-                       s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
+  grs_status r;
+  if (s->rank_mode == 0)
+    r = launch_pass<K, PAIRS, 4, T, kPassOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
+                                             s->ctrl + GRS_CTRL_TICKETS, s->status,
+                                             s->status + s->status_words, stream);
   else
-    hipLaunchKernelGGL((grs::grs_onesweep_pass<K, PAIRS, RB, Cfg::BLOCK, Cfg::ITEMS, 0,
-                                               grs::SplitterDigit<K>>),
-                       dim3(tiles), dim3(Cfg::BLOCK), 0, stream, keys, keys_out, vals, vals_out, n,
-                       dig, hist, s->ctrl + GRS_CTRL_TICKETS, s->status,
-                       s->status + s->status_words, s->ctrl + GRS_CTRL_ERROR);
-  GRS_HIP(hipGetLastError());
+    r = launch_pass<K, PAIRS, 4, T, kMatchOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
+                                              s->ctrl + GRS_CTRL_TICKETS, s->status,
+                                              s->status + s->status_words, stream);
+  if (r != GRS_OK) return r;
   GRS_HIP(hipMemcpyAsync(d_counts, hist, (count + 1) * 4, hipMemcpyDeviceToDevice, stream));
   return GRS_OK;
+}
+
+// Host-side splitters (keys, optional shard-local thresholds) -> the smallest N >= count.
+template <typename K, bool PAIRS>
+grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
+                         uint32_t* vals_out, uint32_t n, const K* splitters, const uint32_t* th,
+                         int count, uint32_t* d_counts, hipStream_t stream) {
+  auto go = [&](auto nconst) {
+    constexpr int N = decltype(nconst)::value;
+    grs::SplitterIdxDigit<K, N> d{};
+    d.count = N;
+    for (int i = 0; i < GRS_MAX_SPLITTERS; ++i) {
+      // padding splitters (i >= count) never count: (max key, max index) is above every element
+      d.s[i] = i < count ? splitters[i] : static_cast<K>(~static_cast<K>(0));
+      d.th[i] = i < count ? (th ? th[i] : 0u) : 0xFFFFFFFFu;
+    }
+    return run_partition_n<K, PAIRS, N>(s, keys, vals, keys_out, vals_out, n, d, nullptr, count,
+                                        d_counts, stream);
+  };
+  if (count <= 1) return go(std::integral_constant<int, 1>{});
+  if (count <= 3) return go(std::integral_constant<int, 3>{});
+  if (count <= 7) return go(std::integral_constant<int, 7>{});
+  return go(std::integral_constant<int, 15>{});
 }
 
 }  // namespace
 
 extern "C" {
 
-grs_status grs_partition(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
-                         void* d_keys_out, uint32_t* d_vals_out, size_t n,
-                         const void* splitters, int n_splitters, uint32_t* d_counts,
-                         void* stream) {
+static grs_status partition_impl(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                                 void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                                 const void* splitters, const uint32_t* thresholds,
+                                 int n_splitters, uint32_t* d_counts, void* stream) {
   if (!s) return set_err(GRS_EINVAL, "grs_partition: NULL sorter");
   if (n_splitters < 0 || n_splitters > GRS_MAX_SPLITTERS || (n_splitters > 0 && !splitters))
     return set_err(GRS_EINVAL, "grs_partition: 0..15 splitters required");
@@ -574,24 +553,42 @@ grs_status grs_partition(grs_sorter* s, const void* d_keys, const uint32_t* d_va
   if (s->key_type == GRS_KEY_U32) {
     if (s->pairs)
       r = run_partition<uint32_t, true>(s, (const uint32_t*)d_keys, d_vals, (uint32_t*)d_keys_out,
-                                        d_vals_out, n32, (const uint32_t*)splitters, n_splitters,
-                                        d_counts, st);
+                                        d_vals_out, n32, (const uint32_t*)splitters, thresholds,
+                                        n_splitters, d_counts, st);
     else
       r = run_partition<uint32_t, false>(s, (const uint32_t*)d_keys, nullptr, (uint32_t*)d_keys_out,
-                                         nullptr, n32, (const uint32_t*)splitters, n_splitters,
-                                         d_counts, st);
+                                         nullptr, n32, (const uint32_t*)splitters, thresholds,
+                                         n_splitters, d_counts, st);
   } else {
     if (s->pairs)
       r = run_partition<uint64_t, true>(s, (const uint64_t*)d_keys, d_vals, (uint64_t*)d_keys_out,
-                                        d_vals_out, n32, (const uint64_t*)splitters, n_splitters,
-                                        d_counts, st);
+                                        d_vals_out, n32, (const uint64_t*)splitters, thresholds,
+                                        n_splitters, d_counts, st);
     else
       r = run_partition<uint64_t, false>(s, (const uint64_t*)d_keys, nullptr, (uint64_t*)d_keys_out,
-                                         nullptr, n32, (const uint64_t*)splitters, n_splitters,
-                                         d_counts, st);
+                                         nullptr, n32, (const uint64_t*)splitters, thresholds,
+                                         n_splitters, d_counts, st);
   }
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
+}
+
+grs_status grs_partition(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                         void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                         const void* splitters, int n_splitters, uint32_t* d_counts,
+                         void* stream) {
+  return partition_impl(s, d_keys, d_vals, d_keys_out, d_vals_out, n, splitters, nullptr,
+                        n_splitters, d_counts, stream);
+}
+
+grs_status grs_partition_ranges(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                                void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                                const void* splitters, const uint32_t* thresholds,
+                                int n_splitters, uint32_t* d_counts, void* stream) {
+  if (n_splitters > 0 && !thresholds)
+    return set_err(GRS_EINVAL, "grs_partition_ranges: thresholds are NULL");
+  return partition_impl(s, d_keys, d_vals, d_keys_out, d_vals_out, n, splitters, thresholds,
+                        n_splitters, d_counts, stream);
 }
 
 grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, int begin_bit,
@@ -666,14 +663,37 @@ grs_status grs_last_timing(grs_sorter* s, grs_timing* out) { return grs_timing_h
 
 grs_status grs_check_error(grs_sorter* s) {
   if (!s) return set_err(GRS_EINVAL, "grs_check_error: NULL sorter");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
   uint32_t e = 0;
-  GRS_HIP(hipDeviceSynchronize());
-  GRS_HIP(hipMemcpy(&e, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost));
-  if (e) {
-    GRS_HIP(hipMemset(s->ctrl + GRS_CTRL_ERROR, 0, 4));
-    return set_err(GRS_ETIMEOUT, "a look-back spin exceeded its bound");
-  }
-  return GRS_OK;
+  grs_status r = GRS_OK;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&e, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+      (e && hipMemset(s->ctrl + GRS_CTRL_ERROR, 0, 4) != hipSuccess))
+    r = set_err(GRS_EHIP, "grs_check_error: HIP failure");
+  if (prev != s->device) (void)hipSetDevice(prev);
+  if (r != GRS_OK) return r;
+  return e ? set_err(GRS_ETIMEOUT, "a look-back spin exceeded its bound") : GRS_OK;
+}
+
+grs_status grs_stream_check_error(grs_sorter* s, void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_stream_check_error: NULL sorter");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  grs_status r = GRS_OK;
+  *s->h_err = 0;
+  if (hipMemcpyAsync(s->h_err, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_stream_check_error: HIP failure");
+  const uint32_t e = *s->h_err;
+  if (r == GRS_OK && e && hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_stream_check_error: HIP failure");
+  if (prev != s->device) (void)hipSetDevice(prev);
+  if (r != GRS_OK) return r;
+  return e ? set_err(GRS_ETIMEOUT, "a look-back spin exceeded its bound") : GRS_OK;
 }
 
 static int grid_for(size_t n, int block) {
@@ -841,7 +861,6 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
   }
   if (r == GRS_OK && (!s->seg64 || s->seg64->capacity < n)) {
     if (s->seg64) grs_destroy(s->seg64);
-  if (s->host_stage) (void)hipFree(s->host_stage);
     s->seg64 = nullptr;
     r = grs_create(&s->seg64, s->capacity, GRS_KEY_U64, 1, 8, s->device);
   }
@@ -902,8 +921,6 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   grs_status r = GRS_OK;
   if (s->seg_bytes < need) {
     if (s->seg_buf) (void)hipFree(s->seg_buf);
-  if (s->seg64) grs_destroy(s->seg64);
-  if (s->host_stage) (void)hipFree(s->host_stage);
     s->seg_buf = nullptr;
     s->seg_bytes = 0;
     if (hipMalloc(&s->seg_buf, need) != hipSuccess) {
@@ -1004,11 +1021,246 @@ grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
   return r;
 }
 
+// ---------------------------------------------------------------------------------------
+// multi-GPU key-range sort: grs_sort_sharded
+// ---------------------------------------------------------------------------------------
+
+int grs_shard_samples_per_rank(int nranks) {
+  return nranks <= 0 ? 0 : std::min(1024, GRS_SHARD_SAMPLES_MAX / nranks);
+}
+
+}  // extern "C"
+
+namespace {
+
+#define GRS_RCCL(call)                                                                     \
+  do {                                                                                     \
+    ncclResult_t e_ = (call);                                                              \
+    if (e_ != ncclSuccess)                                                                 \
+      return set_err(GRS_ERCCL, std::string(#call) + ": " + ncclGetErrorString(e_));       \
+  } while (0)
+
+// Exchange plan from the G x G count matrix (row r: rank r's bucket sizes).
+void shard_plan(const uint32_t* mat, int g, int me, uint64_t* soff, uint64_t* roff, uint64_t* n_out) {
+  uint64_t so = 0, ro = 0;
+  for (int p = 0; p < g; ++p) {
+    soff[p] = so;
+    so += mat[me * g + p];
+    roff[p] = ro;
+    ro += mat[p * g + me];
+  }
+  *n_out = ro;
+}
+
+template <typename K>
+constexpr ncclDataType_t nccl_type() { return sizeof(K) == 4 ? ncclUint32 : ncclUint64; }
+
+template <typename K, bool PAIRS, int N>
+grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uint32_t n, K* out_k,
+                         uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
+                         int me, hipStream_t st) {
+  using Dig = grs::SplitterIdxDigit<K, N>;
+  const uint32_t S = static_cast<uint32_t>(grs_shard_samples_per_rank(g));
+  // scratch: sk[S] | sp[S] | ak[G*S] | ap[G*S] | cnt[16] | mat[G*G] | digit, 256-B aligned parts
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t gs = static_cast<size_t>(g) * S;
+  const size_t need = al(S * sizeof(K)) + al(S * 4) + al(gs * sizeof(K)) + al(gs * 4) + al(64) +
+                      al(static_cast<size_t>(g) * g * 4) + al(sizeof(Dig));
+  if (s->shard_bytes < need) {
+    if (s->shard_buf) (void)hipFree(s->shard_buf);
+    s->shard_buf = nullptr;
+    s->shard_bytes = 0;
+    if (hipMalloc(&s->shard_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      return set_err(GRS_ENOMEM, "grs_sort_sharded: scratch allocation failed");
+    }
+    s->shard_bytes = need;
+  }
+  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), (16 * 16 + 4) * 4,
+                                      hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(GRS_ENOMEM, "grs_sort_sharded: pinned allocation failed");
+  }
+  char* b = static_cast<char*>(s->shard_buf);
+  K* sk = reinterpret_cast<K*>(b);                  b += al(S * sizeof(K));
+  uint32_t* sp = reinterpret_cast<uint32_t*>(b);     b += al(S * 4);
+  K* ak = reinterpret_cast<K*>(b);                   b += al(gs * sizeof(K));
+  uint32_t* ap = reinterpret_cast<uint32_t*>(b);     b += al(gs * 4);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(b);    b += al(64);
+  uint32_t* mat = reinterpret_cast<uint32_t*>(b);    b += al(static_cast<size_t>(g) * g * 4);
+  Dig* dig = reinterpret_cast<Dig*>(b);
+
+  // 1-2. samples, all-gathered (rank-major)
+  hipLaunchKernelGGL((grs::grs_shard_samples<K>), dim3((S + 255) / 256), dim3(256), 0, st, keys, n,
+                     S, sk, sp);
+  GRS_HIP(hipGetLastError());
+  GRS_RCCL(ncclGroupStart());
+  GRS_RCCL(ncclAllGather(sk, ak, S, nccl_type<K>(), comm, st));
+  GRS_RCCL(ncclAllGather(sp, ap, S, ncclUint32, comm, st));
+  GRS_RCCL(ncclGroupEnd());
+  // 3. this rank's partition digit, on the device
+  hipLaunchKernelGGL((grs::grs_shard_splitters<K, N>), dim3(1), dim3(1024), 0, st, ak, ap,
+                     static_cast<uint32_t>(g), S, static_cast<uint32_t>(me), dig);
+  GRS_HIP(hipGetLastError());
+  // 4. partition into the send buffer (the sorter's ping-pong scratch, free until step 8)
+  K* send_k = static_cast<K*>(s->alt_keys);
+  uint32_t* send_v = s->alt_vals;
+  if (n > 0) {
+    const grs_status r = run_partition_n<K, PAIRS, N>(s, keys, vals, send_k, send_v, n, Dig{}, dig,
+                                                      g - 1, cnt, st);
+    if (r != GRS_OK) return r;
+  } else {
+    GRS_HIP(hipMemsetAsync(cnt, 0, static_cast<size_t>(g) * 4, st));
+  }
+  // 5-6. count matrix to every rank, then the one host synchronisation (counts + error word)
+  GRS_RCCL(ncclAllGather(cnt, mat, g, ncclUint32, comm, st));
+  GRS_HIP(hipMemcpyAsync(s->shard_host, mat, static_cast<size_t>(g) * g * 4, hipMemcpyDeviceToHost, st));
+  GRS_HIP(hipMemcpyAsync(s->shard_host + g * g, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st));
+  GRS_HIP(hipStreamSynchronize(st));
+  if (s->shard_host[g * g] != 0) {
+    GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
+    return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a partition look-back spin exceeded its bound");
+  }
+  uint64_t soff[16], roff[16], total = 0;
+  shard_plan(s->shard_host, g, me, soff, roff, &total);
+  if (total > out_cap || total > s->capacity)
+    return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
+                                      " items) exceeds out_capacity or the sorter capacity");
+  // 7. exchange: keys and payload in one group; the self part is a device copy
+  GRS_RCCL(ncclGroupStart());
+  for (int p = 0; p < g; ++p) {
+    if (p == me) continue;
+    const size_t sc = s->shard_host[me * g + p], rc = s->shard_host[p * g + me];
+    if (sc) GRS_RCCL(ncclSend(send_k + soff[p], sc, nccl_type<K>(), p, comm, st));
+    if (rc) GRS_RCCL(ncclRecv(out_k + roff[p], rc, nccl_type<K>(), p, comm, st));
+    if (PAIRS && sc) GRS_RCCL(ncclSend(send_v + soff[p], sc, ncclUint32, p, comm, st));
+    if (PAIRS && rc) GRS_RCCL(ncclRecv(out_v + roff[p], rc, ncclUint32, p, comm, st));
+  }
+  GRS_RCCL(ncclGroupEnd());
+  const size_t self = s->shard_host[me * g + me];
+  if (self) {
+    GRS_HIP(hipMemcpyAsync(out_k + roff[me], send_k + soff[me], self * sizeof(K),
+                           hipMemcpyDeviceToDevice, st));
+    if (PAIRS)
+      GRS_HIP(hipMemcpyAsync(out_v + roff[me], send_v + soff[me], self * 4,
+                             hipMemcpyDeviceToDevice, st));
+  }
+  *n_out = static_cast<size_t>(total);
+  // 8. local stable sort of the received run (source-rank order = global order for ties)
+  return grs_sort(s, out_k, out_v, static_cast<size_t>(total), st);
+}
+
+template <typename K, bool PAIRS>
+grs_status run_sharded(grs_sorter* s, const K* keys, const uint32_t* vals, uint32_t n, K* out_k,
+                       uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
+                       int me, hipStream_t st) {
+  if (g <= 2) return run_sharded_n<K, PAIRS, 1>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
+  if (g <= 4) return run_sharded_n<K, PAIRS, 3>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
+  if (g <= 8) return run_sharded_n<K, PAIRS, 7>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
+  return run_sharded_n<K, PAIRS, 15>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+grs_status grs_sort_sharded(grs_sorter* s, const void* d_keys_in, const uint32_t* d_vals_in,
+                            size_t n_local, void* d_keys_out, uint32_t* d_vals_out,
+                            size_t out_capacity, size_t* n_out, void* nccl_comm, void* stream) {
+  if (!s || !n_out || !nccl_comm) return set_err(GRS_EINVAL, "grs_sort_sharded: NULL argument");
+  *n_out = 0;
+  if (n_local > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_sharded: n_local exceeds capacity");
+  if ((n_local && !d_keys_in) || !d_keys_out)
+    return set_err(GRS_EINVAL, "grs_sort_sharded: NULL keys");
+  if (s->pairs && ((n_local && !d_vals_in) || !d_vals_out))
+    return set_err(GRS_EINVAL, "grs_sort_sharded: payload sorter needs d_vals_in / d_vals_out");
+  ncclComm_t comm = static_cast<ncclComm_t>(nccl_comm);
+  int g = 0, me = 0;
+  GRS_RCCL(ncclCommCount(comm, &g));
+  GRS_RCCL(ncclCommUserRank(comm, &me));
+  if (g < 1 || g > GRS_MAX_SPLITTERS + 1)
+    return set_err(GRS_EINVAL, "grs_sort_sharded: 1..16 ranks supported");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint32_t n32 = static_cast<uint32_t>(n_local);
+  grs_status r;
+  if (s->key_type == GRS_KEY_U32)
+    r = s->pairs ? run_sharded<uint32_t, true>(s, (const uint32_t*)d_keys_in, d_vals_in, n32, (uint32_t*)d_keys_out, d_vals_out, out_capacity, n_out, comm, g, me, st)
+                 : run_sharded<uint32_t, false>(s, (const uint32_t*)d_keys_in, nullptr, n32, (uint32_t*)d_keys_out, nullptr, out_capacity, n_out, comm, g, me, st);
+  else
+    r = s->pairs ? run_sharded<uint64_t, true>(s, (const uint64_t*)d_keys_in, d_vals_in, n32, (uint64_t*)d_keys_out, d_vals_out, out_capacity, n_out, comm, g, me, st)
+                 : run_sharded<uint64_t, false>(s, (const uint64_t*)d_keys_in, nullptr, n32, (uint64_t*)d_keys_out, nullptr, out_capacity, n_out, comm, g, me, st);
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_rccl_unique_id(void* id_out) {
+  if (!id_out) return set_err(GRS_EINVAL, "grs_rccl_unique_id: NULL");
+  static_assert(sizeof(ncclUniqueId) == GRS_RCCL_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  GRS_RCCL(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return GRS_OK;
+}
+
+grs_status grs_rccl_comm_init(void** comm_out, const void* id, int nranks, int rank, int device) {
+  if (!comm_out || !id || nranks < 1 || rank < 0 || rank >= nranks)
+    return set_err(GRS_EINVAL, "grs_rccl_comm_init: bad argument");
+  *comm_out = nullptr;
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  GRS_HIP(hipSetDevice(device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  const ncclResult_t e = ncclCommInitRank(&c, nranks, uid, rank);
+  (void)hipSetDevice(prev);
+  if (e != ncclSuccess)
+    return set_err(GRS_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
+  *comm_out = c;
+  return GRS_OK;
+}
+
+void grs_rccl_comm_destroy(void* comm) {
+  if (comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm));
+}
+
+grs_status grs_shard_splitters_host(const void* sorted_keys, const uint32_t* sorted_idx,
+                                    const uint32_t* gathered_pos, int key_bytes, int nranks,
+                                    int samples_per_rank, int rank, void* splitters_out,
+                                    uint32_t* thresholds_out) {
+  if (!sorted_keys || !sorted_idx || !gathered_pos || (nranks > 1 && (!splitters_out || !thresholds_out)) ||
+      (key_bytes != 4 && key_bytes != 8) || nranks < 1 || nranks > 16 || samples_per_rank < 1 ||
+      rank < 0 || rank >= nranks)
+    return set_err(GRS_EINVAL, "grs_shard_splitters_host: bad argument");
+  const uint32_t m = static_cast<uint32_t>(nranks * samples_per_rank);
+  for (int bb = 0; bb + 1 < nranks; ++bb) {
+    const uint32_t q = grs::shard_quantile(static_cast<uint32_t>(bb), m, static_cast<uint32_t>(nranks));
+    const uint32_t j = sorted_idx[q];
+    if (key_bytes == 4)
+      static_cast<uint32_t*>(splitters_out)[bb] = static_cast<const uint32_t*>(sorted_keys)[q];
+    else
+      static_cast<uint64_t*>(splitters_out)[bb] = static_cast<const uint64_t*>(sorted_keys)[q];
+    thresholds_out[bb] = grs::shard_threshold(j / static_cast<uint32_t>(samples_per_rank),
+                                              static_cast<uint32_t>(rank), gathered_pos[j]);
+  }
+  return GRS_OK;
+}
+
+grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int rank,
+                               uint64_t* send_off, uint64_t* recv_off, uint64_t* n_out) {
+  if (!count_matrix || !send_off || !recv_off || !n_out || nranks < 1 || nranks > 16 || rank < 0 ||
+      rank >= nranks)
+    return set_err(GRS_EINVAL, "grs_shard_plan_host: bad argument");
+  shard_plan(count_matrix, nranks, rank, send_off, recv_off, n_out);
+  return GRS_OK;
+}
+
 const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
-  if (!s) return "";
-  if (s->rank_mode != 0) return "grs_onesweep_pass";
-  if (s->key_type == GRS_KEY_U32 && !s->pairs && u32_pass_for(s, n) == 0) return "grs_onesweep_v3";
-  return "grs_onesweep_ar";
+  (void)n;
+  return s ? "grs_onesweep_v4" : "";
 }
 
 }  // extern "C"

@@ -16,18 +16,15 @@
 #define GRS_BLOCK 512               // threads per onesweep workgroup (8 waves)
 #define GRS_HIST_BLOCK 256
 
-// Decoupled look-back status word: [31:30] flag, [29:0] digit count.
-#define GRS_FLAG_SHIFT 30u
-#define GRS_FLAG_NOT_READY 0u
-#define GRS_FLAG_AGGREGATE 1u
-#define GRS_FLAG_INCLUSIVE 2u
-#define GRS_VALUE_MASK 0x3FFFFFFFu
-// Largest element count one device sort call accepts: a tile's inclusive digit
-// prefix must fit the 30-bit value field of a status word.
-#define GRS_MAX_N ((uint64_t)GRS_VALUE_MASK)
+// Largest element count one device sort call accepts.  Look-back words hold counts + 1
+// (grs_pass.hpp), so every prefix fits 32 bits; the bound keeps tile arithmetic
+// (tile * TILE + TILE) inside 32 bits for every tile shape (TILE < 2^16).
+#define GRS_MAX_N 0xFFFF0000ull
 
 // Bounded spins (look-back): give up after this many polls and raise the error word.
+#ifndef GRS_SPIN_LIMIT
 #define GRS_SPIN_LIMIT (1u << 22)
+#endif
 // Key-range partition (multi-GPU exchange): at most this many splitters -> 16 buckets.
 #define GRS_MAX_SPLITTERS 15
 

@@ -1,0 +1,506 @@
+// grs_pass.hpp — the LSD pass kernel of libgrs (one launch per digit), gfx950.
+//
+// Replaces one bit-iteration of the reference's pass loop (ParallelSort.cpp:236-298): K2
+// (GetBitForPrefixScan.comp:25-68) + K3a/K3b (ParallelPrefixScan.comp:41-196) + K4
+// (SortIntermediateData.comp:32-67), i.e. "extract the digit, scan it within the group and
+// over the groups, scatter stably", for a whole RB-bit digit in ONE launch:
+//
+//   ticket   tile id from an atomic counter: tiles start in id order, so a tile only ever
+//            waits on tiles that already started (no forward-progress assumption)
+//   load     the tile, wave-striped into registers (item j of lane l of wave w is tile key
+//            w*64*ITEMS + j*64 + l): ranking items in (j, lane) order visits input order
+//   rank     ONE returning LDS add per key on its wave's digit counter: the LDS serialises the
+//            lanes of one wave-instruction that hit one address in ascending lane order, so
+//            the returned count is the key's stable rank among its wave's keys of that digit
+//            (probed at sorter creation; the ballot-match fallback is RANK_MATCH below)
+//   B1       digit threads: wave starts (column scan), tile count, publish the count, add it
+//            into the group accumulator; wave scans over digits (tile and pass starts)
+//   B2       tile-local digit starts folded into the wave counters; look-back polls ISSUED
+//   B3       all waves reorder the tile in LDS by (digit, input order); the digit threads
+//            then FINISH the look-back (its round trip overlapped the reorder) and write the
+//            global base of each digit
+//   B4       stores: consecutive threads write consecutive slots of each digit run
+//
+// MINW workgroups per CU (launch bounds + LDS sized for it): while one workgroup waits on a
+// ticket, a look-back or its loads, another ranks or reorders — the phases of one tile are a
+// serial chain, so overlap comes from co-resident tiles.
+#pragma once
+
+#include "grs_kernels.hpp"
+
+namespace grs {
+
+// Inclusive wave64 scan of a u32 by DPP (row_shr 1/2/4/8, row_bcast 15/31): 6 VALU, no LDS.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+// Look-back status of one pass (uint32 words, all zero at pass start):
+//   tile words   [tiles][R]   count + 1 of the tile's digit (0 = not published yet)
+//   group accs   [groups][R]  (arrivals << 24) | sum of the group's tile counts
+//   group incl   [groups][R]  inclusive prefix of the group + 1 (0 = not published yet),
+//                             written by the tile whose add completes the accumulator
+// Values are stored +1 so that no flag bits are needed: prefixes reach n (< 2^32).
+__host__ __device__ constexpr size_t lb3_status_words(size_t tiles, size_t radix) {
+  return (tiles + 2 * ((tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP)) * radix;
+}
+
+// Exclusive prefix of digit d over tiles [0, tile): own group's earlier tiles (< G words)
+// plus the group-level prefix (newest published group INCLUSIVE + complete accumulators
+// after it).  issue() sends the first round of loads, finish() consumes them.
+template <int RADIX>
+struct Lb3 {
+  static constexpr int G = GRS_LB_GROUP;
+  static constexpr int GW = GRS_LB_GWIN;
+  uint32_t tw[G - 1];
+  uint32_t gi[GW], ga[GW];
+  int32_t ph;
+
+  __device__ __forceinline__ void load_groups(const uint32_t* gacc, const uint32_t* ginc,
+                                              uint32_t d) {
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      const int32_t h = ph - k;
+      gi[k] = h >= 0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      ga[k] = h >= 0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
+    }
+  }
+  __device__ __forceinline__ void issue(const uint32_t* status, const uint32_t* gacc,
+                                        const uint32_t* ginc, uint32_t tile, uint32_t d) {
+    const uint32_t first = (tile / G) * G;
+#pragma unroll
+    for (int k = 0; k < G - 1; ++k)
+      tw[k] = first + k < tile ? ld_status(status + static_cast<size_t>(first + k) * RADIX + d) : 1u;
+    ph = static_cast<int32_t>(tile / G) - 1;
+    load_groups(gacc, ginc, d);
+  }
+  // gold: the value this tile's add to its group accumulator returned; publish: its count
+  __device__ __forceinline__ uint32_t finish(const uint32_t* status, const uint32_t* gacc,
+                                             uint32_t* ginc, uint32_t tile, uint32_t tiles,
+                                             uint32_t d, uint32_t gold, uint32_t publish,
+                                             uint32_t* error_word) {
+    const uint32_t g = tile / G;
+    const uint32_t first = g * G;
+    uint32_t spins = 0, own = 0;
+#pragma unroll
+    for (int k = 0; k < G - 1; ++k) {
+      uint32_t v = tw[k];
+      while (v == 0u) {
+        if (++spins > GRS_SPIN_LIMIT) {
+          atomicOr(error_word, 1u);
+          v = 1u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = ld_status(status + static_cast<size_t>(first + k) * RADIX + d);
+      }
+      own += v - 1u;
+    }
+    uint32_t gp = 0;
+    while (ph >= 0) {
+      int consumed = 0;
+      bool done = false, blocked = false;
+#pragma unroll
+      for (int k = 0; k < GW; ++k) {
+        if (!done && !blocked && ph - k >= 0) {
+          if (gi[k] != 0u) {
+            gp += gi[k] - 1u;
+            done = true;
+          } else if ((ga[k] >> 24) == static_cast<uint32_t>(G)) {
+            gp += ga[k] & 0xFFFFFFu;
+            ++consumed;
+          } else {
+            blocked = true;
+          }
+        }
+      }
+      if (done) break;
+      ph -= consumed;
+      if (ph < 0) break;
+      if (consumed == 0) {
+        if (++spins > GRS_SPIN_LIMIT) {
+          atomicOr(error_word, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      load_groups(gacc, ginc, d);
+    }
+    const uint32_t in_group = min(static_cast<uint32_t>(G), tiles - g * G);
+    if ((gold >> 24) == in_group - 1u)  // this tile's add completed the group
+      st_status(ginc + static_cast<size_t>(g) * RADIX + d, gp + (gold & 0xFFFFFFu) + publish + 1u);
+    return gp + own;
+  }
+};
+
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
+          bool IDX = false>
+struct V4Smem {
+  static constexpr int RADIX = 1 << RB;
+  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int TILE = BLOCK * ITEMS;
+  // per-wave digit counters -> tile position of (wave, digit); CNT16: 16-bit, two per word
+  uint32_t cnt[WAVES * RADIX / (CNT16 ? 2 : 1)];
+  uint32_t base[RADIX];         // global destination of tile position 0 of digit d
+  uint32_t wsum[2 * WAVES];     // wave totals of the two digit scans
+  uint32_t ticket;
+  alignas(16) K keys[TILE];
+  uint32_t vals[PAIRS ? TILE : 1];
+  uint8_t dig8[IDX ? TILE : 1];  // indexed digits: digit of each reordered position
+};
+
+// OPT bits (lab ablations; the library uses OPT = 0):
+//   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
+//   16 look-back issued after the reorder (no overlap)
+//   32 contiguous stores (dst = tile position; wrong output)      64 no look-back (estimate)
+//   128 nontemporal key loads
+//   256 16-bit wave counters (two digits per LDS word: half the counter LDS)
+//   512 ballot-match ranking instead of lane-ordered LDS atomics (the fallback when the
+//       device probe of the lane order fails, grs_capi.hip)
+
+// One tile, start to finish.  Precondition: sm.cnt is zero and sm.ticket holds `tile`, and
+// every thread passed a barrier since both were written and since the previous tile's last
+// LDS access.  Leaves sm.cnt dirty.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
+__device__ __forceinline__ void onesweep_tile(
+    V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>& sm, uint32_t tile, const K* __restrict__ keys_in,
+    K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word, uint64_t t_begin) {
+  using SM = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>;
+  constexpr bool C16 = (OPT & 256) != 0;
+  constexpr int RADIX = SM::RADIX;
+  constexpr int WAVES = SM::WAVES;
+  constexpr int TILE = SM::TILE;
+  static_assert(!C16 || TILE < 65536, "16-bit tile positions");
+  uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
+  constexpr bool IDX = DigitF::kIndexed;
+  auto cnt_ld = [&](uint32_t i) -> uint32_t { if constexpr (C16) return c16[i]; else return sm.cnt[i]; };
+  auto cnt_st = [&](uint32_t i, uint32_t v) { if constexpr (C16) c16[i] = static_cast<uint16_t>(v); else sm.cnt[i] = v; };
+  constexpr int DW = (RADIX + GRS_WAVE - 1) / GRS_WAVE;  // waves holding digit threads
+  constexpr int G = GRS_LB_GROUP;
+  static_assert(RADIX <= BLOCK, "one digit thread per digit");
+  static_assert(static_cast<long>(G) * TILE < (1l << 24), "group accumulator field");
+  // opaque per call: keeps the compiler from hoisting ITEMS per-thread addresses out of a
+  // persistent loop (they would stay live across the whole tile and spill)
+  uint32_t t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  const uint32_t groups = (tiles + G - 1) / G;
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t pad = TILE - valid;
+  const uint32_t dmask = dig.max_digit();
+  uint32_t* gacc = status + static_cast<size_t>(tiles) * RADIX;
+  uint32_t* ginc = gacc + static_cast<size_t>(groups) * RADIX;
+
+#define V4_STAMP(k)                                                                        \
+  do {                                                                                     \
+    if constexpr ((OPT & 8) != 0) {                                                        \
+      if (t == 0)                                                                          \
+        error_word[64 + static_cast<size_t>(tile) * 8 + (k)] =                             \
+            static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);                 \
+    }                                                                                      \
+  } while (0)
+
+  // ---- load, wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l ----
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  {
+    const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS) + lane;
+    auto ld = [&](const auto* p, uint32_t i) {
+      if constexpr ((OPT & 128) != 0) return __builtin_nontemporal_load(p + i);
+      else return p[i];
+    };
+    if (valid == static_cast<uint32_t>(TILE)) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) key[j] = ld(keys_in, wbase + j * GRS_WAVE);
+      if constexpr (PAIRS) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) val[j] = ld(vals_in, wbase + j * GRS_WAVE);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t i = wbase + j * GRS_WAVE;
+        // padding sorts after every valid key of its digit: all-ones digit, highest index
+        key[j] = i < n ? keys_in[i] : static_cast<K>(~static_cast<K>(0));
+        if constexpr (PAIRS) val[j] = i < n ? vals_in[i] : 0u;
+      }
+    }
+  }
+
+  // digit of item j (indexed digits: of (key, shard-local index); padding: the largest)
+  auto dig_of = [&](int j) -> uint32_t {
+    if constexpr (IDX) {
+      const uint32_t i = tile_base + w * (GRS_WAVE * ITEMS) + j * GRS_WAVE + lane;
+      return (valid == static_cast<uint32_t>(TILE) || i < n) ? dig(key[j], i) : dmask;
+    } else {
+      return dig(key[j]);
+    }
+  };
+
+  // ---- rank ----  (two 16-bit ranks per register: a wave ranks at most 64 * ITEMS keys)
+  static_assert(GRS_WAVE * ITEMS < 65536, "16-bit ranks");
+  uint32_t rank[(ITEMS + 1) / 2];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    uint32_t r;
+    if constexpr ((OPT & 512) != 0) {
+      // peers of this lane's digit in this item: the lowest one adds their count; LDS runs a
+      // wave's instructions in order, so the plain read sees items < j exactly
+      static_assert(!C16, "match ranking uses 32-bit counters");
+      const uint32_t d = dig_of(j);
+      const uint64_t m = match_digit<RB>(d);
+      const uint32_t below = mbcnt64(m);
+      uint32_t* c = &sm.cnt[w * RADIX + d];
+      const uint32_t old = *c;
+      if (below == 0) atomicAdd(c, static_cast<uint32_t>(__popcll(m)));
+      r = old + below;
+    } else if constexpr (C16) {
+      const uint32_t d = dig_of(j);
+      const uint32_t sh = (d & 1u) << 4;
+      r = (atomicAdd(&sm.cnt[(w * RADIX + d) >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    } else {
+      r = atomicAdd(&sm.cnt[w * RADIX + dig_of(j)], 1u);
+    }
+    if (j & 1)
+      rank[j / 2] |= r << 16;
+    else
+      rank[j / 2] = r;
+  }
+  V4_STAMP(0);
+  // this tile's (and its group's) words of the next pass's status buffer
+  if (t < static_cast<uint32_t>(RADIX)) {
+    status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
+    if (tile % G == 0) {
+      status_next[static_cast<size_t>(tiles) * RADIX + (tile / G) * RADIX + t] = 0;
+      status_next[static_cast<size_t>(tiles + groups) * RADIX + (tile / G) * RADIX + t] = 0;
+    }
+  }
+  lds_barrier();  // B1
+  V4_STAMP(1);
+
+  uint32_t tile_cnt = 0, publish = 0, gold = 0, lstart = 0, gstart = 0;
+  if (t < static_cast<uint32_t>(RADIX)) {
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) {
+      const uint32_t c = cnt_ld(ww * RADIX + t);
+      cnt_st(ww * RADIX + t, tile_cnt);
+      tile_cnt += c;
+    }
+    publish = (t == dmask) ? tile_cnt - pad : tile_cnt;  // padding is ranked, never counted
+    st_status(status + static_cast<size_t>(tile) * RADIX + t, publish + 1u);
+    gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
+                                  (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (w < static_cast<uint32_t>(DW)) {
+    const uint32_t li = wave_scan_dpp(tile_cnt);
+    const uint32_t gi = wave_scan_dpp(gh);
+    if (lane == GRS_WAVE - 1) {
+      sm.wsum[w] = li;
+      sm.wsum[WAVES + w] = gi;
+    }
+    lstart = li - tile_cnt;
+    gstart = gi - gh;
+  }
+  lds_barrier();  // B2
+  V4_STAMP(2);
+
+  Lb3<RADIX> lb;
+  if (t < static_cast<uint32_t>(RADIX)) {
+    for (uint32_t ww = 0; ww < w; ++ww) {
+      lstart += sm.wsum[ww];
+      gstart += sm.wsum[WAVES + ww];
+    }
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
+    if constexpr ((OPT & (16 | 64)) == 0) lb.issue(status, gacc, ginc, tile, t);
+  }
+  lds_barrier();  // B3
+  V4_STAMP(3);
+
+  // ---- reorder the tile in LDS by (digit, input order) ----
+  // the digits are recomputed from the keys (1 VALU each) instead of being kept live since
+  // the ranking: the empty asm hides the earlier values from common-subexpression elimination
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) asm volatile("" : "+v"(key[j]));
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t r = (j & 1) ? rank[j / 2] >> 16 : rank[j / 2] & 0xFFFFu;
+    const uint32_t d = dig_of(j);
+    const uint32_t pos = cnt_ld(w * RADIX + d) + r;
+    sm.keys[pos] = key[j];
+    if constexpr (IDX) sm.dig8[pos] = static_cast<uint8_t>(d);
+    if constexpr (PAIRS) sm.vals[pos] = val[j];
+  }
+  if (t < static_cast<uint32_t>(RADIX)) {
+    uint32_t prefix;
+    if constexpr ((OPT & 64) != 0) {
+      prefix = static_cast<uint32_t>((static_cast<uint64_t>(gh) * tile) / tiles);
+    } else {
+      if constexpr ((OPT & 16) != 0) lb.issue(status, gacc, ginc, tile, t);
+      prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
+    }
+    sm.base[t] = gstart + prefix - lstart;
+  }
+  lds_barrier();  // B4
+  V4_STAMP(4);
+
+  // ---- store: consecutive threads write consecutive slots of each digit run ----
+  auto dig_at = [&](uint32_t i, K kk) -> uint32_t {  // digit of reordered position i
+    if constexpr (IDX) return sm.dig8[i];
+    else return dig(kk);
+  };
+  if (valid == static_cast<uint32_t>(TILE)) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const uint32_t i = k * BLOCK + t;
+      const K kk = sm.keys[i];
+      uint32_t dst = sm.base[dig_at(i, kk)] + i;
+      if constexpr ((OPT & 64) != 0) dst = min(dst, n - 1);
+      if constexpr ((OPT & 32) != 0) dst = tile_base + i;
+      keys_out[dst] = kk;
+      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const uint32_t i = k * BLOCK + t;
+      if (i < valid) {
+        const K kk = sm.keys[i];
+        const uint32_t dst = sm.base[dig_at(i, kk)] + i;
+        keys_out[dst] = kk;
+        if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+      }
+    }
+  }
+  if constexpr ((OPT & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    V4_STAMP(5);
+    if (t == 0) error_word[64 + static_cast<size_t>(tile) * 8 + 7] = static_cast<uint32_t>(t_begin >> 8);
+  }
+#undef V4_STAMP
+}
+
+// One tile per workgroup (grid = tiles), tile ids from a ticket counter.  dig_dev: when not
+// null, the digit functor is read from device memory instead of the `dig` argument.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
+  using SM = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>;
+  __shared__ SM sm;
+  const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+  for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+  const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
+  __syncthreads();
+  // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
+  const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
+  onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, sm.ticket, keys_in, keys_out, vals_in,
+                                                 vals_out, n, dg, gh, status, status_next,
+                                                 error_word, t_begin);
+}
+
+// ---------------------------------------------------------------------------------------
+// XCD-chunked tile schedule
+// ---------------------------------------------------------------------------------------
+// A digit run of tile T and the run of tile T+1 meet inside one 128-B line (and so do runs
+// with a few keys).  Written by two workgroups on two XCDs, such a line leaves two L2s as two
+// partial writes; measured (tools/lab2.py --emu): the uniform-key scatter of 36K-key tiles
+// with 576-B runs runs at 4.56 TB/s against 5.47 for 512-B (line-aligned) runs, and at 4.91
+// when consecutive tiles share an XCD (their partial lines merge in its L2).  So tiles are
+// handed out in chunks of CH consecutive tiles per XCD: each XCD has a word {chunk id + 1,
+// tiles taken}; a workgroup adds 1 to its XCD's word; the one that finds the chunk full (or
+// no chunk yet) claims the next chunk from a global chunk counter and installs it.  Chunks
+// are claimed in increasing order and an XCD hands out its chunk's tiles in increasing
+// order, so the lowest unfinished tile is always being processed or is the next one its
+// XCD hands out: with persistent workgroups (each loops until it draws a tile >= tiles) the
+// grid cannot deadlock, whatever the residency, as long as an XCD that claimed a chunk keeps
+// one workgroup (the claimer itself).
+struct XcdSched {
+  unsigned long long xw[8];  // per XCD: (chunk id + 1) << 32 | tiles taken from it
+  uint32_t gchunk;           // chunks claimed so far
+  uint32_t pad[15];
+};
+static_assert(sizeof(XcdSched) == 128, "XcdSched is 32 words");
+
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x & 7u;
+}
+
+template <int CH>
+__device__ __forceinline__ uint32_t xcd_ticket(XcdSched* sc, uint32_t x, uint32_t* error_word) {
+  unsigned long long v = atomicAdd(&sc->xw[x], 1ull);
+  uint32_t spins = 0;
+  while (true) {
+    const uint32_t c1 = static_cast<uint32_t>(v >> 32);
+    const uint32_t j = static_cast<uint32_t>(v);
+    if (c1 != 0u && j < static_cast<uint32_t>(CH)) return (c1 - 1u) * CH + j;
+    if (c1 == 0u ? j == 0u : j == static_cast<uint32_t>(CH)) {  // exactly one installer per chunk
+      const uint32_t g = atomicAdd(&sc->gchunk, 1u);
+      __hip_atomic_exchange(&sc->xw[x], (static_cast<unsigned long long>(g + 1u) << 32) | 1ull,
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return g * CH;
+    }
+    // another workgroup installs the next chunk: wait for it, then draw again
+    unsigned long long v2;
+    do {
+      if (++spins > GRS_SPIN_LIMIT) {
+        atomicOr(error_word, 2u);
+        return 0xFFFFFFFFu;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v2 = __hip_atomic_load(&sc->xw[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while (static_cast<uint32_t>(v2 >> 32) == c1);
+    v = atomicAdd(&sc->xw[x], 1ull);
+  }
+}
+
+// Persistent workgroups over the XCD-chunked schedule (grid = resident workgroups).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int CH, int OPT = 0,
+          typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v5(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
+    const uint32_t* __restrict__ pass_hist, XcdSched* __restrict__ sched,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word) {
+  using SM = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>;
+  __shared__ SM sm;
+  const uint32_t t = threadIdx.x;
+  const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
+  const uint32_t x = xcc_id();
+  const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
+  while (true) {
+    const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
+    if (t == 0) sm.ticket = xcd_ticket<CH>(sched, x, error_word);
+    for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    lds_barrier();
+    const uint32_t tile = sm.ticket;
+    if (tile >= tiles) break;
+    onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, keys_in, keys_out, vals_in, vals_out,
+                                                   n, dig, gh, status, status_next, error_word,
+                                                   t_begin);
+    lds_barrier();  // every LDS read of this tile is done before the counters are reset
+  }
+}
+
+}  // namespace grs

@@ -59,6 +59,13 @@ class ParallelSort:
                                    radix_bits=8, device=dataToSort.Buffer().device.index)
 
     def Sort(self) -> None:
+        """Sort the bound buffer in place and synchronise the stream (the reference's Sort()
+        ends with a blocking map, ParallelSort.cpp:330-333); raises GrsError (GRS_ETIMEOUT) if
+        a look-back spin gave up.  SortAsync() only enqueues."""
+        self.SortAsync()
+        self._sorter.check_error(self._stream)
+
+    def SortAsync(self) -> None:
         buf = self._originalDataSsbo.Buffer()
         self._sorter.sort(buf, stream=self._stream)
 

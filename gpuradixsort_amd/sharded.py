@@ -1,182 +1,131 @@
-"""Multi-GPU sort: one process per GPU, key-range sharding with ONE all-to-all-v exchange.
+"""Multi-GPU sort: one process per GPU, key-range sharding with ONE all-to-all exchange.
 
 New with respect to the reference (which is single-context).  Input: each
-rank r holds a contiguous shard of the global input (global indices [r*n, (r+1)*n) in rank
-order).  Output: rank r holds a contiguous, sorted range of the global stable order; the
-concatenation over ranks in rank order equals the stable sort of the whole input.
+rank r holds a contiguous shard of the global input (the global range that follows ranks < r).
+Output: rank r holds a contiguous, sorted range of the global stable order; the concatenation
+over ranks in rank order equals the stable sort of the whole input.
 
-Per call:
-  1. splitters  every rank contributes `oversample` regularly spaced keys of its shard;
-                one all_gather; every rank sorts the G*oversample samples on the host
-                (tiny) and picks the same G-1 quantiles as splitters
-  2. partition  grs_partition: stable key-range partition into G contiguous send buckets
-                (bucket = number of splitters <= key, monotone in the key)
-  3. counts     all_to_all of the G bucket sizes -> receive sizes (one D2H sync)
-  4. exchange   all_to_all_single of the keys (and payload) -- on the "nccl" backend this is
-                RCCL over xGMI, every peer pair on its own link
-  5. local sort the received buckets are concatenated in SOURCE-RANK order, i.e. global
-                input order for equal keys; the stable LSD sort then gives the global stable
-                order (ties broken by global index, exactly the reference's order)
+All of it runs in libgrs's C-ABI entry point grs_sort_sharded (include/grs.h) on an RCCL
+communicator that libgrs owns (RcclComm below; a C++ caller passes its own ncclComm_t):
+  1. samples     S regularly spaced (key, position) samples of the shard, RCCL all-gather
+  2. splitters   on the device: the G*S samples sorted by (key, global index) in one
+                 workgroup, G-1 quantiles -> this rank's partition digit; ties are broken by
+                 global index, so equal keys split evenly across ranks
+  3. partition   the grs pass kernel with the splitter digit: G contiguous send buckets
+  4. counts      RCCL all-gather of the G x G bucket counts -> the ONE host synchronisation
+  5. exchange    grouped ncclSend / ncclRecv of keys and payload (xGMI: one link per peer)
+  6. local sort  grs_sort of the received run, which arrived in source-rank order = global
+                 input order for equal keys, so the result is the global stable order
 
-Correctness does not depend on the splitters (any non-decreasing splitters give the right
-global order); they only set the balance.  Equal keys never straddle two ranks.
-
-The device steps go through an `ops` object: HipOps (libgrs, the only production path) by
-default.  tests/ substitute a numpy implementation to run the orchestration under `gloo`
-on CPU; the collective pattern is identical.
+torch.distributed only carries the 128-byte RCCL id from rank 0 to the others.  The CPU tests
+run the same orchestration under gloo (tests/sharded_sim.py) with libgrs's host twins of the
+splitter and plan arithmetic (grs_shard_splitters_host, grs_shard_plan_host).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
-
-class HipOps:
-    """Device steps on libgrs (HIP, gfx950)."""
-
-    def __init__(self, capacity: int, key_bits: int, pairs: bool, radix_bits: int, device):
-        from .sorter import RadixSorter
-
-        self.device = device
-        self.key_bits = key_bits
-        self.pairs = pairs
-        self.radix_bits = radix_bits
-        self.part = RadixSorter(capacity, key_bits=key_bits, pairs=pairs, radix_bits=radix_bits,
-                                device=device.index)
-        self.local = None
-        self.local_cap = 0
-
-    def partition(self, keys, vals, keys_out, vals_out, splitters, counts):
-        self.part.partition(keys, keys_out, splitters, counts, vals, vals_out)
-
-    def local_sort(self, keys, vals, n):
-        if self.local is None or self.local_cap < n:
-            if self.local is not None:
-                self.local.close()
-            self.local_cap = max(n, 1)
-            from .sorter import RadixSorter
-
-            self.local = RadixSorter(self.local_cap, key_bits=self.key_bits, pairs=self.pairs,
-                                     radix_bits=self.radix_bits, device=self.device.index)
-            if getattr(self, "_ring", 0):
-                self.local.set_profiling(self._ring)
-        self.local.sort(keys, vals, n=n)
-
-    def set_profiling(self, ring):
-        self._ring = ring
-        if self.local is not None:
-            self.local.set_profiling(ring)
-
-    def timing(self, k=0):
-        return self.local.timing(k)
-
-    def count_inversions(self, keys):
-        from .sorter import count_inversions
-
-        return count_inversions(keys)
+from ._lib import GRS_RCCL_ID_BYTES, check, lib
+from .sorter import RadixSorter, _ptr, _stream_ptr
 
 
-def _comm_view(t: torch.Tensor) -> torch.Tensor:
-    """Collectives move bytes: view unsigned keys as the signed type of the same width."""
-    if t.dtype == torch.uint32:
-        return t.view(torch.int32)
-    if t.dtype == torch.uint64:
-        return t.view(torch.int64)
-    return t
+class RcclComm:
+    """An RCCL communicator over the ranks of a torch.distributed group, one rank per GPU,
+    created by libgrs (grs_rccl_comm_init); `handle` is the ncclComm_t."""
+
+    def __init__(self, group=None, device: Optional[int] = None):
+        L = lib()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        idbuf = ctypes.create_string_buffer(GRS_RCCL_ID_BYTES)
+        if self.rank == 0:
+            check(L.grs_rccl_unique_id(idbuf), "grs_rccl_unique_id")
+        obj = [bytes(idbuf.raw) if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
+                                   group=group)
+        idbuf = ctypes.create_string_buffer(obj[0], GRS_RCCL_ID_BYTES)
+        h = ctypes.c_void_p()
+        check(L.grs_rccl_comm_init(ctypes.byref(h), idbuf, self.world, self.rank, self.device),
+              "grs_rccl_comm_init")
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().grs_rccl_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class ShardedSorter:
-    """Stable sort of a key (+ uint32 payload) array sharded over the ranks of `group`."""
+    """Stable sort of a key (+ uint32 payload) array sharded over the ranks of `group`
+    (grs_sort_sharded).  capacity_local bounds this rank's input; the received run may be
+    larger on skewed inputs: recv_slack sizes the output buffer (and the sorter) for it."""
 
     def __init__(self, capacity_local: int, key_bits: int = 32, pairs: bool = False,
                  radix_bits: int = 8, group=None, device: Optional[torch.device] = None,
-                 oversample: int = 1024, recv_slack: float = 1.25, ops=None):
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+                 recv_slack: float = 1.25, comm: Optional[RcclComm] = None):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = device
         self.key_bits = key_bits
         self.pairs = pairs
-        self.oversample = int(oversample)
-        if self.world - 1 > 15:
-            raise ValueError("grs_partition supports at most 16 ranks per exchange")
-        self.kdt = torch.uint32 if key_bits == 32 else torch.uint64
-        self.ndt = np.uint32 if key_bits == 32 else np.uint64
-        self.ops = ops if ops is not None else HipOps(capacity_local, key_bits, pairs, radix_bits,
-                                                      device)
+        self.comm = comm if comm is not None else RcclComm(group, device.index)
+        self.world = self.comm.world
+        self.rank = self.comm.rank
+        if self.world > 16:
+            raise ValueError("grs_sort_sharded supports at most 16 ranks per exchange")
         self.cap = int(capacity_local)
-        self.send_k = torch.empty(max(self.cap, 1), dtype=self.kdt, device=device)
-        self.send_v = torch.empty(max(self.cap, 1), dtype=torch.uint32, device=device) if pairs else None
-        self.recv_cap = max(int(self.cap * recv_slack), 1)
-        self.recv_k = torch.empty(self.recv_cap, dtype=self.kdt, device=device)
-        self.recv_v = torch.empty(self.recv_cap, dtype=torch.uint32, device=device) if pairs else None
-        self.counts = torch.zeros(self.world, dtype=torch.uint32, device=device)
-        self.last_local_n = 0
-        self.last_send_counts = None
-        self.last_recv_counts = None
+        self.out_cap = max(int(self.cap * recv_slack), self.cap, 1)
+        self.sorter = RadixSorter(self.out_cap, key_bits=key_bits, pairs=pairs,
+                                  radix_bits=radix_bits, device=device.index)
+        kdt = torch.uint32 if key_bits == 32 else torch.uint64
+        self.out_k = torch.empty(self.out_cap, dtype=kdt, device=device)
+        self.out_v = torch.empty(self.out_cap, dtype=torch.uint32, device=device) if pairs else None
+        self.last_n_out = 0
 
-    # ---- step 1 ---------------------------------------------------------------------------
-    def splitters(self, keys: torch.Tensor, n: int) -> np.ndarray:
-        G, S = self.world, self.oversample
-        if n > 0:
-            idx = (torch.arange(S, device=keys.device, dtype=torch.int64) * n) // S
-            local = _comm_view(keys[:n]).index_select(0, idx)
-        else:   # an empty shard contributes max keys (they only bias the top splitter)
-            local = torch.full((S,), -1, dtype=_comm_view(keys[:0]).dtype, device=keys.device)
-        gathered = torch.empty(G * S, dtype=local.dtype, device=keys.device)
-        dist.all_gather_into_tensor(gathered, local.contiguous(), group=self.group)
-        samples = np.sort(gathered.cpu().numpy().view(self.ndt))
-        q = (np.arange(1, G, dtype=np.int64) * samples.size) // G
-        return samples[q]
-
-    # ---- steps 2-5 ------------------------------------------------------------------------
     def sort(self, keys: torch.Tensor, vals: Optional[torch.Tensor] = None,
-             n: Optional[int] = None, splitters=None):
-        """Returns (keys_out, vals_out) views of this rank's sorted output range."""
-        n = keys.numel() if n is None else int(n)
+             n: Optional[int] = None, stream: Optional[torch.cuda.Stream] = None, check_error=True):
+        """Returns (keys_out, vals_out): views of this rank's sorted output range (valid until
+        the next call).  check_error=True synchronises the stream once more to surface a
+        look-back timeout of the local sort (the exchange itself already synchronised)."""
+        self.sorter._check_keys(keys, vals)
+        n = RadixSorter._check_n(n, keys, vals)
         if n > self.cap:
             raise ValueError("shard exceeds capacity_local")
-        if (vals is not None) != self.pairs:
-            raise ValueError("payload presence must match the sorter")
-        sp = self.splitters(keys, n) if splitters is None else np.asarray(splitters, self.ndt)
-        self.ops.partition(keys, vals, self.send_k, self.send_v, sp, self.counts)
-
-        send_counts = self.counts.to(torch.int64)
-        recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-        sc = send_counts.cpu().tolist()   # the one host sync of the call
-        rc = recv_counts.cpu().tolist()
-        n_out = int(sum(rc))
-        if n_out > self.recv_cap:          # skewed input: grow the receive buffers
-            self.recv_cap = int(n_out * 1.1) + 1
-            self.recv_k = torch.empty(self.recv_cap, dtype=self.kdt, device=self.device)
-            if self.pairs:
-                self.recv_v = torch.empty(self.recv_cap, dtype=torch.uint32, device=self.device)
-        dist.all_to_all_single(_comm_view(self.recv_k[:n_out]), _comm_view(self.send_k[:n]),
-                               output_split_sizes=rc, input_split_sizes=sc, group=self.group)
-        if self.pairs:
-            dist.all_to_all_single(_comm_view(self.recv_v[:n_out]), _comm_view(self.send_v[:n]),
-                                   output_split_sizes=rc, input_split_sizes=sc, group=self.group)
-        self.ops.local_sort(self.recv_k, self.recv_v, n_out)
-        self.last_local_n = n_out
-        self.last_send_counts, self.last_recv_counts = sc, rc
-        return self.recv_k[:n_out], (self.recv_v[:n_out] if self.pairs else None)
+        n_out = ctypes.c_size_t(0)
+        vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
+        vo = _ptr(self.out_v) if self.pairs else ctypes.c_void_p(0)
+        check(lib().grs_sort_sharded(self.sorter._h, _ptr(keys), vp, n, _ptr(self.out_k), vo,
+                                     self.out_cap, ctypes.byref(n_out), self.comm.handle,
+                                     _stream_ptr(stream)), "grs_sort_sharded")
+        if check_error:
+            self.sorter.check_error(stream)
+        self.last_n_out = int(n_out.value)
+        m = self.last_n_out
+        return self.out_k[:m], (self.out_v[:m] if self.pairs else None)
 
     # ---- bench plumbing ---------------------------------------------------------------------
     def set_profiling(self, ring: int) -> None:
-        self.ops.set_profiling(ring)
+        self.sorter.set_profiling(ring)
 
     def timing(self, k: int = 0) -> dict:
-        return self.ops.timing(k)
+        return self.sorter.timing(k)
 
-    def count_inversions(self, _keys=None) -> int:
-        return self.ops.count_inversions(self.recv_k[: self.last_local_n])
+    def count_inversions(self) -> int:
+        from .sorter import count_inversions
 
-    def phase_summary(self) -> dict:
-        return {"recv_keys_this_rank": self.last_local_n,
-                "send_counts": self.last_send_counts, "recv_counts": self.last_recv_counts}
+        return count_inversions(self.out_k[: self.last_n_out])
+
+    def close(self) -> None:
+        self.sorter.close()
+        self.comm.close()

@@ -92,12 +92,25 @@ class RadixSorter:
         elif vals is not None:
             raise ValueError("this sorter was created without a payload")
 
+    @staticmethod
+    def _check_n(n: Optional[int], *tensors: Optional[torch.Tensor]) -> int:
+        """n defaults to the first tensor's length; every given tensor must hold n items
+        (libgrs cannot see tensor extents: a larger n would read and write past them)."""
+        n = tensors[0].numel() if n is None else int(n)
+        if n < 0:
+            raise ValueError("n must be >= 0")
+        for t in tensors:
+            if t is not None and t.numel() < n:
+                raise ValueError(f"n = {n} exceeds a tensor of {t.numel()} items")
+        return n
+
     def sort(self, keys: torch.Tensor, vals: Optional[torch.Tensor] = None, n: Optional[int] = None,
              begin_bit: int = 0, end_bit: Optional[int] = None,
              stream: Optional[torch.cuda.Stream] = None) -> None:
-        """Sort keys[:n] (and vals[:n]) in place, stably, on `stream` (default: current)."""
+        """Sort keys[:n] (and vals[:n]) in place, stably, on `stream` (default: current).
+        Asynchronous: call check_error(stream) to surface a look-back timeout."""
         self._check_keys(keys, vals)
-        n = keys.numel() if n is None else int(n)
+        n = self._check_n(n, keys, vals)
         end_bit = self.key_bits if end_bit is None else int(end_bit)
         vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
         check(lib().grs_sort_bits(self._h, _ptr(keys), vp, n, int(begin_bit), end_bit,
@@ -111,9 +124,18 @@ class RadixSorter:
         import numpy as np
 
         self._check_keys(keys, vals)
-        n = keys.numel() if n is None else int(n)
+        if not keys_out.is_cuda or not keys_out.is_contiguous() or keys_out.element_size() != keys.element_size():
+            raise ValueError("keys_out must be a contiguous device tensor of the key width")
+        if not counts.is_cuda or counts.element_size() != 4 or not counts.is_contiguous():
+            raise ValueError("counts must be a contiguous 32-bit device tensor")
+        n = self._check_n(n, keys, vals, keys_out, vals_out)
         sp = np.ascontiguousarray(np.asarray(splitters, dtype=np.uint32 if self.key_bits == 32
                                              else np.uint64))
+        if counts.numel() < sp.size + 1:
+            raise ValueError("counts needs len(splitters) + 1 entries")
+        if self.pairs and (vals_out is None or not vals_out.is_cuda or not vals_out.is_contiguous()
+                           or vals_out.element_size() != 4):
+            raise ValueError("pairs partition needs a contiguous 32-bit device vals_out")
         vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
         vo = _ptr(vals_out) if vals_out is not None else ctypes.c_void_p(0)
         check(lib().grs_partition(self._h, _ptr(keys), vp, _ptr(keys_out), vo, n,
@@ -154,7 +176,9 @@ class RadixSorter:
         if vals is not None and (not vals.is_cuda or not vals.is_contiguous()
                                  or vals.element_size() != 4):
             raise ValueError("vals must be a contiguous 32-bit device tensor")
-        n = keys.numel() if n is None else int(n)
+        n = self._check_n(n, keys, vals)
+        if offsets.numel() < 2:
+            raise ValueError("offsets needs num_segments + 1 >= 2 entries")
         vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
         check(lib().grs_sort_segmented(self._h, _ptr(keys), vp, n, _ptr(offsets),
                                        offsets.numel() - 1, _stream_ptr(stream)),
@@ -171,8 +195,14 @@ class RadixSorter:
         return {"passes": t.passes, "total_ms": t.total_ms, "hist_ms": t.hist_ms,
                 "pass_ms": list(t.pass_ms)[: t.passes], "copy_ms": t.copy_ms}
 
-    def check_error(self) -> None:
-        check(lib().grs_check_error(self._h), "grs_check_error")
+    def check_error(self, stream: Optional[torch.cuda.Stream] = None, device_wide: bool = False) -> None:
+        """Raise GrsError(GRS_ETIMEOUT) if a look-back spin of an earlier call gave up.
+        Synchronises `stream` (default: current; grs_stream_check_error), or the whole device
+        with device_wide=True (grs_check_error)."""
+        if device_wide:
+            check(lib().grs_check_error(self._h), "grs_check_error")
+        else:
+            check(lib().grs_stream_check_error(self._h, _stream_ptr(stream)), "grs_stream_check_error")
 
 
 # ---- boundary helpers -----------------------------------------------------------------

@@ -40,17 +40,22 @@
 extern "C" {
 #endif
 
-#define GRS_VERSION 100 /* 1.0.0 */
+#define GRS_VERSION 200 /* 2.0.0: v4 pass, 32-bit prefixes, sharded C-ABI */
 
 typedef enum grs_status {
   GRS_OK = 0,
   GRS_EINVAL = 1,      /* bad argument (null pointer, bad radix/bit range, ...) */
   GRS_ENOMEM = 2,      /* hipMalloc failed */
   GRS_EHIP = 3,        /* a HIP runtime call failed; see grs_last_error() */
-  GRS_ECAPACITY = 4,   /* n exceeds the sorter's capacity or the 2^30-1 per-call limit */
+  GRS_ECAPACITY = 4,   /* n exceeds the sorter's capacity or GRS_MAX_N per call */
   GRS_ENODEV = 5,      /* no HIP device / bad device ordinal */
-  GRS_ETIMEOUT = 6     /* a look-back spin exceeded its bound (reported by grs_check_error) */
+  GRS_ETIMEOUT = 6,    /* a look-back spin exceeded its bound (reported by the checks) */
+  GRS_ERCCL = 7        /* an RCCL call failed (multi-GPU entry points) */
 } grs_status;
+
+/* Largest item count of one device call: 2^32 - 2^16 (look-back words hold 32-bit prefixes;
+ * the reference stops at 1,048,576 items, PrefixScanBuffer.comp:36). */
+#define GRS_MAX_N 0xFFFF0000ull
 
 typedef enum grs_key_type { GRS_KEY_U32 = 0, GRS_KEY_U64 = 1 } grs_key_type;
 
@@ -89,10 +94,8 @@ size_t grs_scratch_bytes(const grs_sorter* s);
  * environment variable GRS_RANK=match was set at grs_create).  -1 for a NULL sorter. */
 int grs_rank_mode(const grs_sorter* s);
 
-/* Name of the pass kernel a sort of n items launches: "grs_onesweep_ar" (pairs, u64 keys,
- * and u32 keys from 12 tiles of 36K keys per CU up), "grs_onesweep_v3" (smaller u32 sorts, or
- * GRS_U32_PASS=v3), "grs_onesweep_pass" (ballot-match fallback): what profiling and roofline
- * reports attribute the pass time to. */
+/* Name of the pass kernel a sort of n items launches ("grs_onesweep_v4"): what profiling
+ * and roofline reports attribute the pass time to. */
 const char* grs_pass_kernel(const grs_sorter* s, size_t n);
 
 /* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a
@@ -112,8 +115,13 @@ grs_status grs_set_profiling(grs_sorter* s, int ring);
 grs_status grs_last_timing(grs_sorter* s, grs_timing* out);
 /* Same for the k-th most recent profiled call (k = 0: the last one; k < ring). */
 grs_status grs_timing_history(grs_sorter* s, int k, grs_timing* out);
-/* Synchronises and returns GRS_ETIMEOUT if any look-back spin of past calls gave up. */
+/* Synchronises the sorter's device and returns GRS_ETIMEOUT if any look-back spin of past
+ * calls gave up (the error word is then cleared). */
 grs_status grs_check_error(grs_sorter* s);
+/* The same for the calls issued on `stream` so far: enqueues a read-back of the error word and
+ * synchronises `stream` only (the documented sync point of the checked facades:
+ * ParallelSort::Sort() in grs_parallel_sort.hpp, gpuradixsort_amd.ParallelSort.Sort). */
+grs_status grs_stream_check_error(grs_sorter* s, void* stream);
 
 /* Stable key-range partition for the multi-GPU exchange (gpuradixsort_amd/sharded.py):
  * bucket(key) = number of splitters <= key (splitters: host array of n_splitters <= 15
@@ -125,6 +133,57 @@ grs_status grs_partition(grs_sorter* s, const void* d_keys, const uint32_t* d_va
                          void* d_keys_out, uint32_t* d_vals_out, size_t n,
                          const void* splitters, int n_splitters, uint32_t* d_counts,
                          void* stream);
+
+/* Same, with splitters that break ties by position: splitter b is the element (key
+ * splitters[b], shard-local index thresholds[b]) and element i of this shard goes to bucket
+ * #{b : splitters[b] < key_i || (splitters[b] == key_i && thresholds[b] <= i)}.  A run of
+ * equal keys can then be split between buckets (balance on duplicate-heavy inputs) while every
+ * bucket stays a range of the stable order. */
+grs_status grs_partition_ranges(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                                void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                                const void* splitters, const uint32_t* thresholds,
+                                int n_splitters, uint32_t* d_counts, void* stream);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI ----
+ * The reference has no multi-device path; this is BASELINE config C4's exchange.  Rank r's
+ * input is the global range that follows ranks < r; on return rank r holds a contiguous,
+ * sorted range of the global stable order, and the ranks' outputs concatenated in rank order
+ * are the stable sort of the whole input.  Steps (one stream): regular samples of the shard ->
+ * RCCL all-gather -> on-device splitter choice (ties broken by global index) -> grs partition
+ * pass into G buckets -> all-gather of the G x G bucket counts -> ONE host synchronisation
+ * (the counts) -> grouped ncclSend / ncclRecv of keys and payload -> local grs_sort of the
+ * received run (received in source-rank order = global order for equal keys).
+ * nccl_comm: an initialised ncclComm_t (any RCCL communicator of G <= 16 ranks, one rank per
+ * device); the sorter needs capacity >= max(n_local, *n_out) and out_capacity >= *n_out
+ * (GRS_ECAPACITY otherwise, detected before any data moves).  Returns after enqueuing the local
+ * sort (check it with grs_stream_check_error); look-back timeouts of the partition are reported
+ * by the call itself. */
+grs_status grs_sort_sharded(grs_sorter* s, const void* d_keys_in, const uint32_t* d_vals_in,
+                            size_t n_local, void* d_keys_out, uint32_t* d_vals_out,
+                            size_t out_capacity, size_t* n_out, void* nccl_comm, void* stream);
+
+/* RCCL communicator helpers for callers without their own RCCL binding (ctypes, tests):
+ * rank 0 creates the id (GRS_RCCL_ID_BYTES bytes), every rank passes it to comm_init. */
+#define GRS_RCCL_ID_BYTES 128
+grs_status grs_rccl_unique_id(void* id_out);
+grs_status grs_rccl_comm_init(void** comm_out, const void* id, int nranks, int rank, int device);
+void grs_rccl_comm_destroy(void* comm);
+
+/* Host twins of the sharded sort's host-visible arithmetic (no device needed; the CPU tests
+ * run the orchestration under gloo with them):
+ *  - splitters of `rank` from the G*S gathered samples sorted by (key, gathered index):
+ *    sorted_keys / sorted_idx (M = G*S entries), gathered_pos (shard position of sample j);
+ *    writes G-1 splitter keys and this rank's thresholds (the device step's exact output).
+ *  - the exchange plan from the G x G count matrix (row r = what rank r sends to each bucket):
+ *    send / receive offsets per peer and the received total. */
+grs_status grs_shard_splitters_host(const void* sorted_keys, const uint32_t* sorted_idx,
+                                    const uint32_t* gathered_pos, int key_bytes, int nranks,
+                                    int samples_per_rank, int rank, void* splitters_out,
+                                    uint32_t* thresholds_out);
+grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int rank,
+                               uint64_t* send_off, uint64_t* recv_off, uint64_t* n_out);
+/* Samples per rank of the sharded sort for nranks ranks (min(1024, 8192 / nranks)). */
+int grs_shard_samples_per_rank(int nranks);
 
 /* ---- boundary helpers (reference K1/K5/verification, synthetic data) ---- */
 

@@ -112,12 +112,20 @@ class ParallelSort {
   ParallelSort(const ParallelSort&) = delete;
   ParallelSort& operator=(const ParallelSort&) = delete;
 
-  // Sorts the bound buffer in place (ParallelSort.cpp:168-422).  Asynchronous on the stream.
+  // Sorts the bound buffer in place (ParallelSort.cpp:168-422) and synchronises the stream:
+  // like the reference's Sort(), which ends by mapping the buffer (ParallelSort.cpp:330-333),
+  // it returns with the data sorted, and it throws grs::Error (GRS_ETIMEOUT) if a look-back
+  // spin of the sort gave up.  SortAsync() only enqueues (check later with CheckError()).
   void Sort() {
+    SortAsync();
+    CheckError();
+  }
+  void SortAsync() {
     grs::check(grs_sort(_sorter, _originalDataSsbo->DevicePtr(), nullptr,
                         _originalDataSsbo->NumItems(), _stream),
                "ParallelSort::Sort");
   }
+  void CheckError() { grs::check(grs_stream_check_error(_sorter, _stream), "ParallelSort::CheckError"); }
 
   // Per-phase GPU times of the last Sort() when profiling is on (durations.txt successor).
   void SetProfiling(bool on) { grs::check(grs_set_profiling(_sorter, on ? 1 : 0), "SetProfiling"); }

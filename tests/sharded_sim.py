@@ -1,0 +1,101 @@
+"""Host simulation of grs_sort_sharded for the CPU (gloo) tests — TEST INFRASTRUCTURE.
+
+It follows the device steps of gpuradixsort_amd/csrc/grs_capi.hip (run_sharded_n) one by one,
+with gloo collectives in place of RCCL and numpy restatements of the three device kernels:
+
+  grs_shard_samples      (grs_shard.hpp)   -> _samples
+  grs_shard_splitters    (grs_shard.hpp)   -> np.lexsort by (key, gathered index), then
+                                              libgrs's host twin grs_shard_splitters_host
+  partition pass         (grs_pass.hpp with grs::SplitterIdxDigit) -> _buckets + stable argsort
+  count exchange + plan  -> gloo all_gather + libgrs's host twin grs_shard_plan_host
+  exchange               -> gloo all_to_all_single, source-rank order
+  local sort             -> stable argsort
+
+The splitter and plan arithmetic are the product's own (libgrs host twins, the same inline
+functions the device code uses); nothing here is imported by gpuradixsort_amd.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _lib():
+    from gpuradixsort_amd._lib import check, lib
+
+    return lib(), check
+
+
+def _samples(keys: np.ndarray, s: int):
+    n = keys.size
+    if n == 0:
+        return np.full(s, np.iinfo(keys.dtype).max, keys.dtype), np.full(s, 0xFFFFFFFF, np.uint32)
+    pos = (np.arange(s, dtype=np.uint64) * np.uint64(n)) // np.uint64(s)
+    return keys[pos.astype(np.int64)], pos.astype(np.uint32)
+
+
+def _buckets(keys: np.ndarray, sk: np.ndarray, th: np.ndarray) -> np.ndarray:
+    """grs::SplitterIdxDigit: #{b : sk[b] < k || (sk[b] == k && th[b] <= i)}."""
+    i = np.arange(keys.size, dtype=np.uint64)
+    b = np.zeros(keys.size, np.int64)
+    for kb, tb in zip(sk, th):
+        b += (kb < keys) | ((kb == keys) & (np.uint64(tb) <= i))
+    return b
+
+
+def _all_gather_np(a: np.ndarray, world: int, group=None) -> np.ndarray:
+    t = torch.from_numpy(np.ascontiguousarray(a).view(np.int64 if a.itemsize == 8 else np.int32))
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    return np.concatenate([o.numpy() for o in out]).view(a.dtype)
+
+
+def sim_sharded_sort(keys: np.ndarray, vals, group=None):
+    """Returns (keys_out, vals_out, count_matrix) of this rank."""
+    L, check = _lib()
+    G, me = dist.get_world_size(group), dist.get_rank(group)
+    S = int(L.grs_shard_samples_per_rank(G))
+    kb = keys.dtype.itemsize
+    sk, sp = _samples(keys, S)
+    ak = _all_gather_np(sk, G, group)                 # rank-major: j = rank * S + i
+    ap = _all_gather_np(sp, G, group)
+    order = np.lexsort((np.arange(G * S), ak))        # by (key, j)
+    sorted_k = np.ascontiguousarray(ak[order])
+    sorted_j = np.ascontiguousarray(order.astype(np.uint32))
+    spl = np.zeros(max(G - 1, 1), keys.dtype)
+    th = np.zeros(max(G - 1, 1), np.uint32)
+    check(L.grs_shard_splitters_host(sorted_k.ctypes.data, sorted_j.ctypes.data, ap.ctypes.data,
+                                     kb, G, S, me, spl.ctypes.data, th.ctypes.data),
+          "grs_shard_splitters_host")
+    spl, th = spl[:G - 1], th[:G - 1]
+    b = _buckets(keys, spl, th)
+    perm = np.argsort(b, kind="stable")
+    send_k = keys[perm]
+    send_v = vals[perm] if vals is not None else None
+    cnt = np.bincount(b, minlength=G).astype(np.uint32)
+    mat = np.ascontiguousarray(_all_gather_np(cnt, G, group))
+    soff = (ctypes.c_uint64 * G)()
+    roff = (ctypes.c_uint64 * G)()
+    n_out = ctypes.c_uint64()
+    check(L.grs_shard_plan_host(mat.ctypes.data, G, me, soff, roff, ctypes.byref(n_out)),
+          "grs_shard_plan_host")
+    sc = [int(x) for x in mat.reshape(G, G)[me]]
+    rc = [int(x) for x in mat.reshape(G, G)[:, me]]
+    assert [int(roff[p]) for p in range(G)] == list(np.concatenate([[0], np.cumsum(rc)[:-1]]))
+    assert [int(soff[p]) for p in range(G)] == list(np.concatenate([[0], np.cumsum(sc)[:-1]]))
+    wide = np.int64 if kb == 8 else np.int32
+    rk = torch.empty(int(n_out.value), dtype=torch.int64 if kb == 8 else torch.int32)
+    dist.all_to_all_single(rk, torch.from_numpy(send_k.view(wide).copy()), output_split_sizes=rc,
+                           input_split_sizes=sc, group=group)
+    out_k = rk.numpy().view(keys.dtype)
+    out_v = None
+    if vals is not None:
+        rv = torch.empty(int(n_out.value), dtype=torch.int32)
+        dist.all_to_all_single(rv, torch.from_numpy(send_v.view(np.int32).copy()),
+                               output_split_sizes=rc, input_split_sizes=sc, group=group)
+        out_v = rv.numpy().view(np.uint32)
+    p2 = np.argsort(out_k, kind="stable")
+    return out_k[p2], (out_v[p2] if out_v is not None else None), mat.reshape(G, G)

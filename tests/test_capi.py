@@ -36,7 +36,7 @@ def test_version_and_status_strings():
     from gpuradixsort_amd import _lib
 
     L = _lib.lib()
-    assert L.grs_version() == 100
+    assert L.grs_version() == 200
     assert L.grs_status_string(0) == b"GRS_OK"
     assert L.grs_status_string(4) == b"GRS_ECAPACITY"
 
@@ -49,7 +49,7 @@ def test_create_validates_arguments_without_a_device():
     assert L.grs_create(None, 10, 0, 0, 8, 0) == _lib.GRS_EINVAL
     assert L.grs_create(ctypes.byref(h), 10, 0, 0, 5, 0) == _lib.GRS_EINVAL      # radix 5
     assert L.grs_create(ctypes.byref(h), 10, 7, 0, 8, 0) == _lib.GRS_EINVAL      # key type
-    assert L.grs_create(ctypes.byref(h), 1 << 30, 0, 0, 8, 0) == _lib.GRS_ECAPACITY
+    assert L.grs_create(ctypes.byref(h), _lib.GRS_MAX_N + 1, 0, 0, 8, 0) == _lib.GRS_ECAPACITY
     assert L.grs_sort(None, None, None, 0, None) == _lib.GRS_EINVAL
     import torch
 

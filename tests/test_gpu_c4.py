@@ -1,0 +1,113 @@
+"""GPU tests of BASELINE config C4 (2^30 uint32 keys, 8 shards) on one MI355X.
+
+  * the whole 2^30-key input in ONE device call (the look-back words hold 32-bit prefixes, so
+    one call takes up to GRS_MAX_N = 2^32 - 2^16 items), against the committed digest;
+  * the 8-rank pipeline of grs_sort_sharded replayed on one GPU: eight 2^27-key shards, the
+    same sampling and tie-breaking splitters (libgrs's host twin of the device step), one
+    grs_partition_ranges per shard, buckets concatenated in source-rank order, eight local
+    sorts -- the concatenation must match the same digest, and the destinations must be
+    balanced.
+Digest: tests/golden/digests.json c4_1b_u32 (SHA-256 of the sorted splitmix64 keys, computed
+by the oracle in tests/golden/make_golden.py)."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _rec():
+    return json.load(open(os.path.join(GOLDEN, "digests.json")))["c4_1b_u32"]
+
+
+def _host_sha_update(h, t: torch.Tensor, chunk=1 << 27):
+    for i in range(0, t.numel(), chunk):
+        h.update(t[i:i + chunk].cpu().numpy().tobytes())
+
+
+def test_c4_one_call_2pow30(gpu):
+    import gpuradixsort_amd as grs
+
+    rec = _rec()
+    n = rec["n"]
+    assert n == 1 << 30
+    k = torch.empty(n, dtype=torch.uint32, device=gpu)
+    grs.fill_splitmix(k, rec["seed"])
+    s = grs.RadixSorter(n, key_bits=32)
+    s.sort(k)
+    s.check_error()
+    assert grs.count_inversions(k) == 0
+    h = hashlib.sha256()
+    _host_sha_update(h, k)
+    assert h.hexdigest() == rec["sha256_keys"]
+    assert k[:4].cpu().tolist() == rec["head"] and k[-4:].cpu().tolist() == rec["tail"]
+    s.close()
+    del k
+    torch.cuda.empty_cache()
+
+
+def test_c4_eight_shard_pipeline_on_one_gpu(gpu):
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd._lib import check, lib
+
+    L = lib()
+    rec = _rec()
+    G, n = 8, rec["n"] // 8
+    S = L.grs_shard_samples_per_rank(G)
+    part = grs.RadixSorter(n, key_bits=32)
+    shard = torch.empty(n, dtype=torch.uint32, device=gpu)
+    # 1. samples of every shard (grs_shard_samples: position floor(i * n / S)), rank-major
+    pos = (torch.arange(S, dtype=torch.int64) * n) // S
+    ak, ap = [], []
+    for r in range(G):
+        grs.fill_splitmix(shard, rec["seed"], first_index=r * n)
+        ak.append(shard.index_select(0, pos.to(gpu)).cpu().numpy())
+        ap.append(pos.numpy().astype(np.uint32))
+    ak, ap = np.concatenate(ak), np.ascontiguousarray(np.concatenate(ap))
+    order = np.lexsort((np.arange(G * S), ak))
+    sk = np.ascontiguousarray(ak[order])
+    sj = np.ascontiguousarray(order.astype(np.uint32))
+    # 2. per shard: its splitters + thresholds (host twin of grs_shard_splitters), partition
+    parts, counts = [], []
+    for r in range(G):
+        spl = np.zeros(G - 1, np.uint32)
+        th = np.zeros(G - 1, np.uint32)
+        check(L.grs_shard_splitters_host(sk.ctypes.data, sj.ctypes.data, ap.ctypes.data, 4, G, S, r,
+                                         spl.ctypes.data, th.ctypes.data), "splitters")
+        grs.fill_splitmix(shard, rec["seed"], first_index=r * n)
+        out = torch.empty_like(shard)
+        cnt = torch.zeros(G, dtype=torch.uint32, device=gpu)
+        check(L.grs_partition_ranges(part._h, ctypes.c_void_p(shard.data_ptr()), None,
+                                     ctypes.c_void_p(out.data_ptr()), None, n,
+                                     spl.ctypes.data, th.ctypes.data, G - 1,
+                                     ctypes.c_void_p(cnt.data_ptr()), None), "partition")
+        part.check_error()
+        parts.append(out)
+        counts.append(cnt.cpu().numpy().astype(np.int64))
+    mat = np.stack(counts)                      # mat[r][b]: shard r's bucket b
+    assert mat.sum() == G * n
+    dest = mat.sum(0)
+    assert dest.max() / dest.mean() <= 1.1, dest
+    # 3. per destination: buckets in source-rank order, local stable sort, digest in order
+    local = grs.RadixSorter(int(dest.max()), key_bits=32)
+    h = hashlib.sha256()
+    off = np.concatenate([np.zeros((G, 1), np.int64), np.cumsum(mat, 1)], 1)
+    for b in range(G):
+        buf = torch.cat([parts[r][off[r, b]:off[r, b + 1]] for r in range(G)])
+        local.sort(buf)
+        local.check_error()
+        assert grs.count_inversions(buf) == 0
+        _host_sha_update(h, buf)
+        del buf
+    assert h.hexdigest() == rec["sha256_keys"]
+    part.close()
+    local.close()
+    del parts, shard
+    torch.cuda.empty_cache()

@@ -218,3 +218,61 @@ def test_sort_host_u64_and_empty(gpu):
     assert np.array_equal(k, np.sort(keys))
     s.sort_host(np.zeros(0, dtype=np.uint64))
     s.close()
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+def test_sort_host_segmented_sort_host_on_one_sorter(gpu, kb):
+    """Scratch ownership of one pair sorter across entry points (the round-1 advisor's
+    use-after-free): grs_sort_host -> grs_sort_segmented -> grs_sort_host -> destroy, each
+    result bit-exact."""
+    import gpuradixsort_amd as grs
+
+    dt = np.uint32 if kb == 32 else np.uint64
+    rng = np.random.default_rng(kb)
+    n = 300_007
+    s = grs.RadixSorter(n, key_bits=kb, pairs=True)
+    for rnd in range(2):
+        keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        keys[::9] = 3
+        vals = np.arange(n, dtype=np.uint32)
+        perm = oracle.stable_argsort(keys)
+        hk, hv = keys.copy(), vals.copy()
+        s.sort_host(hk, hv)
+        assert np.array_equal(hk, keys[perm]) and np.array_equal(hv, perm), rnd
+        # segmented sort on the same sorter (allocates its own scratch)
+        offs = np.array([0, 1000, 1000, 77_777, n], np.uint32)
+        k = torch.from_numpy(keys).to(gpu)
+        v = torch.from_numpy(vals).to(gpu)
+        o = torch.from_numpy(offs).to(gpu)
+        s.sort_segmented(k, o, v)
+        s.check_error()
+        exp_k, exp_v = keys.copy(), vals.copy()
+        for a, b in zip(offs[:-1], offs[1:]):
+            p = oracle.stable_argsort(keys[a:b])
+            exp_k[a:b], exp_v[a:b] = keys[a:b][p], vals[a:b][p]
+        assert np.array_equal(k.cpu().numpy(), exp_k) and np.array_equal(v.cpu().numpy(), exp_v)
+        hk, hv = keys.copy(), vals.copy()
+        s.sort_host(hk, hv)
+        assert np.array_equal(hk, keys[perm]) and np.array_equal(hv, perm), rnd
+    s.close()
+
+
+def test_stream_check_error_and_checked_facade(gpu):
+    """grs_stream_check_error on a clean stream returns OK (the look-back never timed out);
+    the checked facades (ParallelSort.Sort) go through it."""
+    import gpuradixsort_amd as grs
+
+    st = torch.cuda.Stream()
+    s = grs.RadixSorter(1 << 20, key_bits=32)
+    k = torch.empty(1 << 20, dtype=torch.uint32, device=gpu)
+    grs.fill_splitmix(k, 17)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        s.sort(k, stream=st)
+        s.check_error(st)
+    assert grs.count_inversions(k) == 0
+    s.check_error(device_wide=True)
+    ssbo = grs.OriginalDataSsbo(1000)
+    ssbo.Upload(np.arange(1000)[::-1].copy())
+    grs.ParallelSort(ssbo).Sort()
+    assert ssbo.Download().numpy().tolist() == list(range(1000))

@@ -67,11 +67,12 @@ def distributions(n, kb, rng):
                           & rng.integers(0, top, n, dtype=dt, endpoint=True))
 
 
-# tile edges of every pass kernel: 12288 / 16384 (one-tile pair / u64 passes, 16384 also v3),
-# 36864 (the default u32 keys-only pass, 512 x 72), and the look-back group edges (8 tiles:
-# 98304 / 131072 / 294912)
-SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 12289, 16383, 16385, 36863,
-         36865, 65536, 98305, 131073, 294913, 1 << 20]
+# Tile edges of the pass (grs_capi.hip BigTile / SmallTile): small tiles 4096 (u32 keys),
+# 2048 (u32 pairs, u64 keys), 1536 (u64 pairs); big tiles 32768 / 16384 / 10240; look-back
+# groups of 8 tiles.  Sizes up to 2^20 run the small tiles by default; test_tile_shapes pins
+# the big ones.
+SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 1535, 1537, 2047, 2049, 4095, 4096, 4097,
+         12289, 16383, 16385, 32769, 36865, 65536, 98305, 131073, 262145, 1 << 20]
 
 
 @pytest.mark.parametrize("radix_bits", [4, 8])
@@ -106,73 +107,91 @@ def test_u64_matches_stable_sort(gpu, n, pairs, radix_bits):
 
 
 def test_rank_mode_is_atomic_on_gfx950(gpu):
-    """The LDS lane-order probe passes on MI355X, so the atomic-rank passes (v3 / ar) run."""
+    """The LDS lane-order probe passes on MI355X, so the atomic-rank pass runs."""
     s = sorter(32, False, 8, 1 << 20)
     assert s.rank_mode == "atomic"
-    assert s.pass_kernel_for(1 << 20) == "grs_onesweep_v3"     # small u32 sorts: persistent v3
-    assert s.pass_kernel_for(1 << 27) == "grs_onesweep_ar"     # large: 36K-key tiles
-    assert sorter(32, True, 8, 1 << 20).pass_kernel == "grs_onesweep_ar"
+    assert s.pass_kernel_for(1 << 20) == "grs_onesweep_v4"
+    assert sorter(32, True, 8, 1 << 20).pass_kernel == "grs_onesweep_v4"
 
 
+@pytest.mark.parametrize("tile", ["big", "small"])
 @pytest.mark.parametrize("kb,pairs", [(32, False), (32, True), (64, False), (64, True)])
-def test_group_and_supergroup_edges(gpu, kb, pairs):
-    """Sizes around the hierarchical look-back's group (8 tiles) and supergroup (64 tiles)
-    edges of every tile size; ragged last groups."""
+def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
+    """GRS_TILE pins the big (1024-thread) or small (256-thread) tile shape whatever the size:
+    bit-exact across each shape's tile edges and look-back group edges (8 tiles), ragged
+    last groups, both digit widths."""
+    import gpuradixsort_amd as grs
+
+    monkeypatch.setenv("GRS_TILE", tile)
+    big = {(32, False): 32768, (32, True): 16384, (64, False): 16384, (64, True): 10240}
+    small = {(32, False): 4096, (32, True): 2048, (64, False): 2048, (64, True): 1536}
+    t = (big if tile == "big" else small)[(kb, pairs)]
     rng = np.random.default_rng(kb * 10 + pairs)
     dt = np.uint32 if kb == 32 else np.uint64
-    for n in (64 * 16384 - 1, 64 * 16384 + 16384 + 5, 8 * 12288 * 9 + 3, 8 * 8192 * 65 + 1):
+    sizes = (1, t - 1, t + 1, 8 * t - 1, 8 * t + 1, 8 * t * 9 + 3, 17 * t + 5)
+    s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=8)
+    s4 = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=4)
+    for n in sizes:
         keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
-        keys[::31] = keys[5]   # ties across tiles
+        keys[::31] = keys[0]   # ties across tiles
+        keys[::97] = np.iinfo(dt).max
         perm = oracle.stable_argsort(keys)
-        gk, gv = gpu_sort(keys, pairs, 8, gpu)
-        assert np.array_equal(gk, keys[perm]), n
-        if pairs:
-            assert np.array_equal(gv, perm), n
+        for srt in (s, s4):
+            k = to_dev(keys, gpu)
+            v = to_dev(np.arange(n, dtype=np.uint32), gpu) if pairs else None
+            srt.sort(k, v)
+            srt.check_error()
+            assert np.array_equal(k.cpu().numpy(), keys[perm]), (n, srt.radix_bits)
+            if pairs:
+                assert np.array_equal(v.cpu().numpy(), perm), (n, srt.radix_bits)
+    s.close()
+    s4.close()
 
 
 def test_ballot_match_fallback(gpu, monkeypatch):
-    """GRS_RANK=match forces the ballot-match pass (the path taken if the LDS order probe
-    ever fails): same bit-exact results."""
+    """GRS_RANK=match forces ballot-match ranking (the path taken if the LDS order probe
+    ever fails): same bit-exact results, both tile shapes."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_RANK", "match")
     rng = np.random.default_rng(5)
-    for kb, pairs, rb in ((32, False, 8), (32, True, 4), (64, True, 8)):
-        dt = np.uint32 if kb == 32 else np.uint64
-        keys = rng.integers(0, np.iinfo(dt).max, 300_007, dtype=dt, endpoint=True)
-        perm = oracle.stable_argsort(keys)
-        s = grs.RadixSorter(keys.size, key_bits=kb, pairs=pairs, radix_bits=rb)
-        assert s.rank_mode == "match" and s.pass_kernel == "grs_onesweep_pass"
-        k = to_dev(keys, gpu)
-        v = to_dev(np.arange(keys.size, dtype=np.uint32), gpu) if pairs else None
-        s.sort(k, v)
-        torch.cuda.synchronize()
-        s.check_error()
-        assert np.array_equal(k.cpu().numpy(), keys[perm])
-        if pairs:
-            assert np.array_equal(v.cpu().numpy(), perm)
-        s.close()
+    for tile in ("big", "small"):
+        monkeypatch.setenv("GRS_TILE", tile)
+        for kb, pairs, rb in ((32, False, 8), (32, True, 4), (64, True, 8), (64, False, 4)):
+            dt = np.uint32 if kb == 32 else np.uint64
+            keys = rng.integers(0, np.iinfo(dt).max, 300_007, dtype=dt, endpoint=True)
+            keys[::5] = 77
+            perm = oracle.stable_argsort(keys)
+            s = grs.RadixSorter(keys.size, key_bits=kb, pairs=pairs, radix_bits=rb)
+            assert s.rank_mode == "match"
+            k = to_dev(keys, gpu)
+            v = to_dev(np.arange(keys.size, dtype=np.uint32), gpu) if pairs else None
+            s.sort(k, v)
+            s.check_error()
+            assert np.array_equal(k.cpu().numpy(), keys[perm]), (tile, kb, pairs, rb)
+            if pairs:
+                assert np.array_equal(v.cpu().numpy(), perm)
+            s.close()
 
 
-@pytest.mark.parametrize("choice", ["v3", "ar1024", "ar512", "ar512x72"])
+@pytest.mark.parametrize("choice", ["1", "2", "3", "4"])
 def test_u32_pass_alternatives(gpu, monkeypatch, choice):
-    """GRS_U32_PASS pins one u32 keys-only pass kernel whatever the size (the persistent v3
-    pass, and the 1024 x 32 / 512 x 64 / 512 x 72 one-tile passes): same bit-exact results,
-    across tile edges and both digit widths."""
+    """GRS_U32_PASS pins one of the lab variants of the big u32-keys pass (look-back after the
+    reorder / 512 x 72 tiles / 16-bit wave counters with 36K-key tiles / default-policy
+    loads): same bit-exact results across tile edges."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_U32_PASS", choice)
+    monkeypatch.setenv("GRS_TILE", "big")
     rng = np.random.default_rng(11)
-    for n, rb in ((1, 8), (16383, 8), (32769, 8), (36865, 4), (1_000_003, 8), (300_007, 4)):
+    for n in (1, 16383, 32769, 36865, 8 * 36864 + 1, 1_000_003):
         keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
         keys[::7] = 0xFFFFFFFF
-        s = grs.RadixSorter(n, key_bits=32, radix_bits=rb)
-        assert s.pass_kernel == ("grs_onesweep_v3" if choice == "v3" else "grs_onesweep_ar")
+        s = grs.RadixSorter(n, key_bits=32, radix_bits=8)
         k = to_dev(keys, gpu)
         s.sort(k)
-        torch.cuda.synchronize()
         s.check_error()
-        assert np.array_equal(k.cpu().numpy(), np.sort(keys)), (choice, n, rb)
+        assert np.array_equal(k.cpu().numpy(), np.sort(keys)), (choice, n)
         s.close()
 
 

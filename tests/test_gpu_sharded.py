@@ -1,8 +1,9 @@
-"""GPU test of the multi-GPU path's production code (HipOps + RCCL collectives) at world
-size 1, the largest world a single-GPU box offers: one real `nccl` (RCCL) process group, the
-splitter all_gather, the counts all_to_all and the all_to_all_single exchange all run, and
-the result must equal the oracle's stable sort.  World sizes 2-4 of the same orchestration
-run on CPU under gloo (tests/test_sharded_gloo.py)."""
+"""GPU tests of the multi-GPU boundary grs_sort_sharded (include/grs.h) at world size 1, the
+largest world a single-GPU box offers: a real RCCL communicator created by libgrs, the
+sample all-gather, the on-device splitter step, the partition pass, the count all-gather and
+host plan, the grouped send/recv (self copy at world 1) and the local sort all run through
+the C-ABI; the result must equal the oracle's stable sort.  World sizes 2-4 of the same
+orchestration run on CPU under gloo (tests/test_sharded_gloo.py)."""
 import os
 import socket
 
@@ -17,34 +18,65 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def nccl_group(gpu):
+def world1(gpu):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
-    yield
+    dist.init_process_group("gloo", rank=0, world_size=1)   # only carries the RCCL id
+    from gpuradixsort_amd.sharded import RcclComm
+
+    comm = RcclComm(device=gpu.index)
+    yield comm
+    comm.close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("key_bits,pairs", [(32, False), (32, True), (64, True)])
-def test_sharded_sort_world1_rccl(gpu, nccl_group, key_bits, pairs):
+@pytest.mark.parametrize("key_bits,pairs,dist_name", [(32, False, "uniform"), (32, True, "ties"),
+                                                      (64, True, "uniform"), (64, False, "ties"),
+                                                      (32, True, "all_equal")])
+def test_sharded_sort_world1_rccl(gpu, world1, key_bits, pairs, dist_name):
     from gpuradixsort_amd.sharded import ShardedSorter
 
     rng = np.random.default_rng(key_bits + pairs)
     dt = np.uint32 if key_bits == 32 else np.uint64
     n = 1_000_003
     keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
-    keys[::11] = 5
+    if dist_name == "ties":
+        keys[::11] = 5
+    elif dist_name == "all_equal":
+        keys[:] = 9
     perm = oracle.stable_argsort(keys)
-    s = ShardedSorter(n, key_bits=key_bits, pairs=pairs, device=gpu)
+    s = ShardedSorter(n, key_bits=key_bits, pairs=pairs, device=gpu, comm=world1)
     k = torch.from_numpy(keys).to(gpu)
     v = torch.arange(n, dtype=torch.int64, device=gpu).to(torch.uint32) if pairs else None
-    ko, vo = s.sort(k, v)
-    torch.cuda.synchronize()
-    assert s.last_local_n == n
-    assert np.array_equal(ko.cpu().numpy(), keys[perm])
-    if pairs:
-        assert np.array_equal(vo.cpu().numpy(), perm)
+    for _ in range(2):   # repeated calls reuse the sorter's scratch
+        ko, vo = s.sort(k.clone(), v.clone() if pairs else None)
+        assert s.last_n_out == n
+        assert np.array_equal(ko.cpu().numpy(), keys[perm])
+        if pairs:
+            assert np.array_equal(vo.cpu().numpy(), perm)
     assert s.count_inversions() == 0
+    s.sorter.close()
+
+
+def test_sharded_capacity_errors(gpu, world1):
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    s = ShardedSorter(1000, key_bits=32, device=gpu, comm=world1)
+    k = torch.zeros(2000, dtype=torch.uint32, device=gpu)
+    with pytest.raises(ValueError):
+        s.sort(k)                       # shard larger than capacity_local
+    ko, _ = s.sort(k, n=0)              # empty shard
+    assert ko.numel() == 0
+    import ctypes
+
+    from gpuradixsort_amd import _lib
+
+    n_out = ctypes.c_size_t()
+    rc = _lib.lib().grs_sort_sharded(s.sorter._h, None, None, 0, None, None, 0,
+                                     ctypes.byref(n_out), None, None)
+    assert rc == _lib.GRS_EINVAL        # NULL communicator / output
+    s.sorter.close()

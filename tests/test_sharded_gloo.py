@@ -1,10 +1,11 @@
-"""Multi-process CPU tests (gloo, world_size 2-4) of the multi-GPU orchestration in
-gpuradixsort_amd/sharded.py: splitter selection, count exchange, all-to-all-v, and the
-source-rank-order concatenation that keeps the global sort stable.
+"""Multi-process CPU tests (gloo, world_size 2-4) of the multi-GPU sort's orchestration
+(grs_sort_sharded): sampling, on-device splitter choice with ties broken by global index,
+count exchange and plan, all-to-all, source-rank-order concatenation, local stable sort.
 
-The device steps (partition, local sort) are swapped for numpy stand-ins HERE ONLY; the
-collective calls and bookkeeping are the production code.  The concatenated outputs of all
-ranks must equal the oracle's stable sort of the whole input (keys and global indices)."""
+tests/sharded_sim.py replays the device steps on the host with gloo collectives and libgrs's
+host twins of the splitter and plan arithmetic.  The concatenated outputs of all ranks must
+equal the oracle's stable sort of the whole input (keys and global indices), and the ranks'
+loads must stay balanced even when the input is all one key."""
 import os
 import socket
 
@@ -15,68 +16,42 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-class NumpyOps:
-    """CPU stand-in for HipOps (tests only)."""
-
-    def __init__(self, key_bits, pairs):
-        self.key_bits, self.pairs = key_bits, pairs
-
-    def partition(self, keys, vals, keys_out, vals_out, splitters, counts):
-        n = keys.numel()
-        k = keys.numpy()
-        b = np.searchsorted(np.asarray(splitters, k.dtype), k, side="right")
-        perm = np.argsort(b, kind="stable")
-        keys_out[:n] = torch.from_numpy(k[perm])
-        if vals is not None:
-            vals_out[:n] = torch.from_numpy(vals.numpy()[perm])
-        counts.copy_(torch.from_numpy(np.bincount(b, minlength=counts.numel()).astype(np.uint32)))
-
-    def local_sort(self, keys, vals, n):
-        k = keys[:n].numpy()
-        perm = np.argsort(k, kind="stable")
-        keys[:n] = torch.from_numpy(k[perm].copy())
-        if vals is not None:
-            vals[:n] = torch.from_numpy(vals[:n].numpy()[perm].copy())
-
-    def set_profiling(self, ring):
-        pass
-
-
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
+def _input(dist_name, total, key_bits):
+    dt = np.uint32 if key_bits == 32 else np.uint64
+    rng = np.random.default_rng(1234)   # same global input on every rank
+    if dist_name == "uniform":
+        return rng.integers(0, np.iinfo(dt).max, total, dtype=dt, endpoint=True)
+    if dist_name == "few_unique":
+        return rng.integers(0, 5, total).astype(dt) * dt(1 << (key_bits - 4))
+    if dist_name == "all_equal":
+        return np.full(total, 42, dt)
+    # skewed: 90 % of the keys in one narrow range
+    return np.where(rng.random(total) < 0.9, rng.integers(0, 1000, total),
+                    rng.integers(0, np.iinfo(dt).max, total, dtype=dt)).astype(dt)
+
+
 def _worker(rank, world, port, n_local, key_bits, pairs, dist_name, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from gpuradixsort_amd.sharded import ShardedSorter
+    import sharded_sim
 
-    dt = np.uint32 if key_bits == 32 else np.uint64
-    rng = np.random.default_rng(1234)   # same global input on every rank
-    total = n_local * world
-    if dist_name == "uniform":
-        allk = rng.integers(0, np.iinfo(dt).max, total, dtype=dt, endpoint=True)
-    elif dist_name == "few_unique":
-        allk = rng.integers(0, 5, total).astype(dt) * dt(1 << (key_bits - 4))
-    elif dist_name == "all_equal":
-        allk = np.full(total, 42, dt)
-    else:   # skewed: 90 % of the keys in one narrow range
-        allk = np.where(rng.random(total) < 0.9, rng.integers(0, 1000, total),
-                        rng.integers(0, np.iinfo(dt).max, total, dtype=dt)).astype(dt)
+    allk = _input(dist_name, n_local * world, key_bits)
     shard = allk[rank * n_local:(rank + 1) * n_local].copy()
-    keys = torch.from_numpy(shard)
-    vals = torch.arange(rank * n_local, (rank + 1) * n_local, dtype=torch.int64).to(torch.uint32) \
-        if pairs else None
-    s = ShardedSorter(n_local, key_bits=key_bits, pairs=pairs, device=torch.device("cpu"),
-                      oversample=64, ops=NumpyOps(key_bits, pairs))
-    ko, vo = s.sort(keys, vals)
-    np.save(os.path.join(out_dir, f"k{rank}.npy"), ko.numpy())
+    vals = np.arange(rank * n_local, (rank + 1) * n_local, dtype=np.uint32) if pairs else None
+    ko, vo, mat = sharded_sim.sim_sharded_sort(shard, vals)
+    np.save(os.path.join(out_dir, f"k{rank}.npy"), ko)
     if pairs:
-        np.save(os.path.join(out_dir, f"v{rank}.npy"), vo.numpy())
-    np.save(os.path.join(out_dir, "all.npy"), allk) if rank == 0 else None
+        np.save(os.path.join(out_dir, f"v{rank}.npy"), vo)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "all.npy"), allk)
+        np.save(os.path.join(out_dir, "mat.npy"), mat)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -87,6 +62,8 @@ def _worker(rank, world, port, n_local, key_bits, pairs, dist_name, out_dir):
     (3, 3001, 32, True, "skewed"),
     (4, 2500, 32, False, "uniform"),
     (4, 1000, 32, True, "all_equal"),
+    (4, 20000, 32, True, "few_unique"),
+    (3, 7000, 64, False, "all_equal"),
     (2, 0, 32, True, "uniform"),
 ])
 def test_sharded_sort_equals_global_stable_sort(tmp_path, world, n_local, key_bits, pairs,
@@ -97,9 +74,31 @@ def test_sharded_sort_equals_global_stable_sort(tmp_path, world, n_local, key_bi
     mp.spawn(_worker, args=(world, port, n_local, key_bits, pairs, dist_name, str(tmp_path)),
              nprocs=world, join=True)
     allk = np.load(tmp_path / "all.npy")
-    keys = np.concatenate([np.load(tmp_path / f"k{r}.npy") for r in range(world)])
+    outs = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
+    keys = np.concatenate(outs)
     perm = oracle.stable_argsort(allk)
     assert np.array_equal(keys, allk[perm])
     if pairs:
         vals = np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)])
         assert np.array_equal(vals, perm)
+    # balance: ties are split by global index, so duplicate-heavy inputs stay balanced
+    if n_local and dist_name in ("all_equal", "few_unique"):
+        sizes = np.array([o.size for o in outs], np.float64)
+        assert sizes.max() / sizes.mean() <= 1.1, sizes
+    mat = np.load(tmp_path / "mat.npy")
+    assert mat.sum() == n_local * world
+
+
+def test_host_twins_validate_arguments():
+    import ctypes
+
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    assert L.grs_shard_samples_per_rank(8) == 1024 and L.grs_shard_samples_per_rank(16) == 512
+    out = (ctypes.c_uint64 * 4)()
+    assert L.grs_shard_plan_host(None, 2, 0, out, out, ctypes.byref(ctypes.c_uint64())) == _lib.GRS_EINVAL
+    mat = np.array([[3, 1], [2, 5]], np.uint32)
+    so, ro, n = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)(), ctypes.c_uint64()
+    assert L.grs_shard_plan_host(mat.ctypes.data, 2, 1, so, ro, ctypes.byref(n)) == 0
+    assert list(so) == [0, 2] and list(ro) == [0, 1] and n.value == 6

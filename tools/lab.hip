@@ -5,7 +5,7 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "../gpuradixsort_amd/csrc/grs_kernels.hpp"
+#include "r1_kernels.hpp"
 
 namespace {
 

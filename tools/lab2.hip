@@ -1,0 +1,200 @@
+// lab2.hip — round-2 kernel laboratory (not part of libgrs): the v4 pass (grs_pass.hpp) at
+// several tile shapes / occupancies, the round-1 ar pass, and streaming-copy ceilings.
+// Built by tools/Makefile into tools/liblab2.so; driven by tools/lab2.py on the GPU box.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "../gpuradixsort_amd/csrc/grs_pass.hpp"
+#include "r1_kernels.hpp"
+
+namespace {
+
+// Streaming copy: U independent 16-B loads in flight per thread, then U stores.
+template <int U>
+__global__ __launch_bounds__(256) void copy_u(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                              uint32_t n4) {
+  const uint32_t stride = gridDim.x * 256;
+  uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    uint4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = in[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) out[i + u * stride] = x[u];
+  }
+  for (; i < n4; i += stride) out[i] = in[i];
+}
+
+// Read-only stream (HBM read ceiling).
+template <int U>
+__global__ __launch_bounds__(256) void read_u(const uint4* __restrict__ in, uint32_t* __restrict__ sink,
+                                              uint32_t n4) {
+  const uint32_t stride = gridDim.x * 256;
+  uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  uint32_t acc = 0;
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    uint4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = in[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= x[u].x ^ x[u].y ^ x[u].z ^ x[u].w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// Memory pattern of one pass without its compute: tile T = blockIdx.x is loaded wave-striped
+// into registers and stored by tile position i = k*BLOCK + t to
+//   MODE 0: T*TILE + i (contiguous), MODE 1: 256 equal digit runs of RUN = TILE/256 keys:
+//   dst = (i / RUN) * (n / 256) + T * RUN + i % RUN (the uniform-key scatter of a pass);
+//   MODE 2: as 1, with consecutive tiles on one XCD (block b -> tile (b%8)*tiles/8 + b/8)
+template <int BLOCK, int ITEMS, int MODE>
+__global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict__ in,
+                                                     uint32_t* __restrict__ out, uint32_t n) {
+  constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 256;
+  extern __shared__ uint32_t pad_lds[];
+  const uint32_t tiles8 = (n / TILE) / 8 * 8;
+  const uint32_t T = MODE == 2 ? (blockIdx.x % 8) * (tiles8 / 8) + blockIdx.x / 8 : blockIdx.x;
+  if (MODE == 2 && blockIdx.x >= tiles8) return;
+  if ((T + 1) * TILE > n) return;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t key[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) key[j] = in[T * TILE + w * 64 * ITEMS + j * 64 + lane];
+  if (n == 0) pad_lds[threadIdx.x] = key[0];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * BLOCK + threadIdx.x;
+    const uint32_t dst = MODE == 0 ? T * TILE + i : (i / RUN) * (n / 256) + T * RUN + i % RUN;
+    out[dst] = key[k];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// pass memory-pattern emulation: block, items, mode, dynamic LDS bytes (occupancy control)
+int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out, uint32_t n,
+             void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t tiles = n / (block * items);
+#define E(B, I, M)                                                                              if (block == B && items == I && mode == M) {                                                    hipLaunchKernelGGL((scatter_emu<B, I, M>), dim3(tiles), dim3(B), lds, s,                                         (const uint32_t*)in, (uint32_t*)out, n);                                   return hipGetLastError() == hipSuccess ? 0 : -2;                                            }
+  E(512, 72, 0) E(512, 72, 1) E(512, 64, 0) E(512, 64, 1) E(1024, 32, 0) E(1024, 32, 1)
+  E(256, 72, 1) E(512, 66, 1) E(512, 72, 2) E(512, 66, 2) E(512, 64, 2) E(256, 72, 2)
+#undef E
+  return -1;
+}
+
+// v4 pass: kb, pairs, block, items, minw, opt
+int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const void* in, void* out,
+            const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
+            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 100 + opt;
+  switch (code) {
+#define V(KB, P, B, I, M, O)                                                                   \
+  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 100 + O: {                    \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                               \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
+    hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
+                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                            \
+                       grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
+                       (const grs::RadixDigit<KT>*)nullptr);                                  \
+  } break;
+    V(32, 0, 256, 72, 2, 0) V(32, 0, 256, 64, 2, 0)
+    V(32, 0, 256, 32, 4, 0) V(32, 0, 512, 36, 2, 0) V(32, 0, 512, 72, 1, 0)
+    V(32, 0, 1024, 32, 1, 0) V(32, 0, 256, 72, 2, 16) V(32, 0, 256, 72, 2, 8)
+    V(32, 0, 512, 72, 1, 8) V(32, 0, 256, 40, 3, 0)
+    V(32, 0, 512, 72, 1, 32) V(32, 0, 512, 72, 1, 64) V(32, 0, 512, 72, 1, 96)
+    V(32, 0, 512, 72, 1, 128) V(32, 0, 1024, 32, 1, 32) V(32, 0, 1024, 32, 1, 64)
+    V(32, 0, 1024, 32, 1, 96) V(32, 0, 1024, 32, 1, 8) V(32, 0, 1024, 32, 1, 16)
+    V(32, 0, 512, 72, 1, 16) V(32, 0, 512, 72, 1, 144) V(32, 0, 1024, 32, 1, 144)
+    V(32, 0, 256, 72, 2, 144) V(32, 0, 512, 72, 1, 24)
+    V(32, 1, 256, 36, 2, 0) V(32, 1, 256, 32, 2, 0) V(64, 0, 256, 36, 2, 0)
+    V(64, 1, 256, 24, 2, 0)
+    V(32, 0, 1024, 36, 1, 400) V(32, 0, 1024, 32, 1, 400) V(32, 0, 1024, 34, 1, 144)
+    V(32, 0, 1024, 32, 1, 128) V(32, 1, 1024, 16, 1, 144) V(64, 0, 1024, 16, 1, 144)
+    V(64, 1, 1024, 10, 1, 144) V(32, 1, 1024, 18, 1, 400) V(64, 0, 1024, 18, 1, 400)
+    V(32, 0, 1024, 36, 1, 272)
+#undef V
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// v5 (persistent, XCD-chunked): kb, pairs, block, items, minw, chunk, opt, grid
+int lab2_v5(int kb, int pairs, int block, int items, int minw, int ch, int opt, int grid,
+            const void* in, void* out, const uint32_t* vin, uint32_t* vout, uint32_t n,
+            const uint32_t* hist, void* sched, uint32_t* st, uint32_t* st2, uint32_t* err,
+            int shift, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code =
+      ((((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 100 + ch) * 1000 + opt;
+  switch (code) {
+#define V(KB, P, B, I, M, C, O)                                                                  \
+  case ((((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 100 + C) * 1000 + O: {        \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                 \
+    hipLaunchKernelGGL((grs::grs_onesweep_v5<KT, P != 0, 8, B, I, M, C, O>), dim3(grid), dim3(B), \
+                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                              \
+                       grs::RadixDigit<KT>{shift, 255u}, hist, (grs::XcdSched*)sched, st, st2,   \
+                       err);                                                                     \
+  } break;
+    V(32, 0, 512, 72, 1, 4, 0) V(32, 0, 512, 72, 1, 8, 0) V(32, 0, 512, 72, 1, 16, 0)
+    V(32, 0, 512, 72, 1, 8, 16) V(32, 0, 512, 72, 1, 8, 128) V(32, 0, 512, 72, 1, 8, 144)
+    V(32, 0, 512, 72, 1, 16, 144) V(32, 0, 512, 72, 1, 32, 144) V(32, 0, 1024, 32, 1, 8, 144)
+    V(32, 0, 256, 72, 2, 8, 144) V(32, 0, 256, 72, 2, 16, 144) V(32, 0, 512, 72, 1, 8, 152)
+    V(32, 1, 512, 36, 1, 8, 144) V(64, 0, 512, 36, 1, 8, 144)
+    V(32, 0, 512, 72, 1, 4, 144) V(32, 0, 512, 72, 1, 2, 144)
+#undef V
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// round-1 library pass (grs_onesweep_ar) for reference: kb, pairs, block, items, dbg
+int lab2_ar(int kb, int pairs, int block, int items, int dbg, const void* in, void* out,
+            const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
+            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = ((((long)kb * 2 + pairs) * 10000 + block) * 100 + items) * 100 + dbg;
+  switch (code) {
+#define A(KB, P, B, I, D)                                                                     \
+  case ((((long)KB * 2 + P) * 10000 + B) * 100 + I) * 100 + D: {                                \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                              \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                         \
+    hipLaunchKernelGGL((grs::grs_onesweep_ar<KT, P != 0, 8, B, I, D>), dim3(tiles), dim3(B),   \
+                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                           \
+                       grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);         \
+  } break;
+    A(32, 0, 512, 72, 0) A(32, 0, 512, 72, 8) A(32, 1, 512, 36, 0) A(64, 0, 512, 36, 0)
+    A(64, 1, 512, 24, 0)
+#undef A
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// copy / read ceilings: kind 0 = copy, 1 = read; unroll 1/4/8; grid
+int lab2_stream(int kind, int unroll, int grid, const void* in, void* out, uint64_t bytes,
+                void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t n4 = static_cast<uint32_t>(bytes / 16);
+  const uint4* i4 = static_cast<const uint4*>(in);
+  uint4* o4 = static_cast<uint4*>(out);
+  if (kind == 0) {
+    if (unroll == 1) hipLaunchKernelGGL(copy_u<1>, dim3(grid), dim3(256), 0, s, i4, o4, n4);
+    else if (unroll == 4) hipLaunchKernelGGL(copy_u<4>, dim3(grid), dim3(256), 0, s, i4, o4, n4);
+    else hipLaunchKernelGGL(copy_u<8>, dim3(grid), dim3(256), 0, s, i4, o4, n4);
+  } else {
+    if (unroll == 1) hipLaunchKernelGGL(read_u<1>, dim3(grid), dim3(256), 0, s, i4, (uint32_t*)out, n4);
+    else if (unroll == 4) hipLaunchKernelGGL(read_u<4>, dim3(grid), dim3(256), 0, s, i4, (uint32_t*)out, n4);
+    else hipLaunchKernelGGL(read_u<8>, dim3(grid), dim3(256), 0, s, i4, (uint32_t*)out, n4);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+"""Round-2 kernel laboratory driver (tools/lab2.hip): interleaved timing of pass variants.
+
+python tools/lab2.py [--n N] [--rounds R] [--check] [--copy]
+       [--variants v4:kb:pairs:block:items:minw:opt,ar:kb:pairs:block:items:dbg,...]
+Prints median / min ms and algorithmic GB/s (2 x (key + payload) bytes per key) per variant;
+variants with the stamp bit (v4 opt & 8, ar dbg & 8) also print mean cycles per phase.
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import gpuradixsort_amd as grs  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 27)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--variants", default="v4:32:0:256:72:2:0")
+    ap.add_argument("--copy", action="store_true")
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
+    a = ap.parse_args()
+    L = ctypes.CDLL(os.path.join(HERE, "liblab2.so"))
+    vp = ctypes.c_void_p
+    P = lambda t: vp(t.data_ptr())  # noqa: E731
+    n = a.n
+    dev = torch.device("cuda", 0)
+    sp = vp(torch.cuda.current_stream().cuda_stream)
+    variants = []
+    for v in a.variants.split(","):
+        f = v.split(":")
+        variants.append((f[0],) + tuple(int(x) for x in f[1:]))
+    bufs = {}
+    for kb in sorted({v[1] for v in variants}):
+        dt = torch.uint32 if kb == 32 else torch.uint64
+        keys = torch.empty(n, dtype=dt, device=dev)
+        grs.fill_splitmix(keys, 0x6A09E667F3BCC908 + 4)
+        k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
+        hist = torch.bincount(k64 & 255, minlength=256).to(torch.int32).view(torch.uint32)
+        bufs[kb] = (keys, torch.empty_like(keys), hist.contiguous())
+    vin = torch.arange(n, dtype=torch.int64, device=dev).to(torch.int32).view(torch.uint32)
+    vout = torch.empty_like(vin)
+    ticket = torch.zeros(64, dtype=torch.uint32, device=dev)   # also the v5 XcdSched (32 words)
+    max_tiles = n // 4096 + 64
+    err = torch.zeros(64 + 8 * max_tiles + 64, dtype=torch.uint32, device=dev)
+    st = torch.zeros(3 * max_tiles * 256, dtype=torch.uint32, device=dev)
+    st2 = torch.zeros_like(st)
+    torch.cuda.synchronize()
+
+    def run(v):
+        kind, kb, pairs, block, items = v[:5]
+        keys, out, hist = bufs[kb]
+        args = (P(keys), P(out), P(vin), P(vout), ctypes.c_uint32(n), P(hist), P(ticket), P(st),
+                P(st2), P(err), 0, sp)
+        if kind == "v4":
+            rc = L.lab2_v4(kb, pairs, block, items, v[5], v[6], *args)
+        elif kind == "v5":   # v5:kb:pairs:block:items:minw:chunk:opt:grid
+            rc = L.lab2_v5(kb, pairs, block, items, v[5], v[6], v[7], v[8], *args)
+        else:
+            rc = L.lab2_ar(kb, pairs, block, items, v[5], *args)
+        assert rc == 0, (v, rc)
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    times = {v: [] for v in variants}
+    for r in range(a.rounds):
+        for v in variants:
+            st.zero_()
+            ticket.zero_()
+            err.zero_()
+            torch.cuda.synchronize()
+            if r == 0:
+                print("run", v, flush=True)
+            e0.record()
+            run(v)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1))
+            if r == 0:
+                print(f"   {times[v][-1]:.4f} ms  err={int(err[0].item())}", flush=True)
+    print(f"n={n}  error word={int(err[0].item())}", flush=True)
+    if a.copy:
+        src = torch.empty(n * 2, dtype=torch.uint32, device=dev)
+        src.fill_(7)
+        dst = torch.empty_like(src)
+        nbytes = n * 4
+        for kind in (0, 1):
+            for unroll in (1, 4, 8):
+                for grid in (1024, 2048, 4096, 8192):
+                    ts = []
+                    for _ in range(5):
+                        e0.record()
+                        assert L.lab2_stream(kind, unroll, grid, P(src), P(dst), ctypes.c_uint64(nbytes), sp) == 0
+                        e1.record()
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1))
+                    med = statistics.median(ts)
+                    moved = nbytes * (2 if kind == 0 else 1)
+                    print(f"{'copy' if kind == 0 else 'read'} unroll={unroll} grid={grid}: "
+                          f"{med:.4f} ms  {moved / med / 1e6:.1f} GB/s", flush=True)
+    if a.emu:
+        keys, out, _ = bufs[32]
+        for e in a.emu.split(","):
+            b, it, mode, lds = (int(x) for x in e.split(":"))
+            ts = []
+            for _ in range(a.rounds):
+                e0.record()
+                assert L.lab2_emu(b, it, mode, lds, P(keys), P(out), ctypes.c_uint32(n), sp) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            print(f"emu {e:20s} median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s", flush=True)
+    if a.check:
+        for v in variants:
+            kb, pairs = v[1], v[2]
+            keys, out, hist = bufs[kb]
+            st.zero_()
+            ticket.zero_()
+            err.zero_()
+            run(v)
+            torch.cuda.synchronize()
+            k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
+            _, idx = torch.sort(k64 & 255, stable=True)
+            o64 = out.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
+            ok = torch.equal(o64, k64[idx])
+            okv = (not pairs) or torch.equal(vout.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, idx)
+            print(f"check {v}: keys {'OK' if ok else 'MISMATCH'} vals {'OK' if okv else 'MISMATCH'} "
+                  f"err={int(err[0].item())}", flush=True)
+    for v in variants:
+        kb, pairs = v[1], v[2]
+        alg = n * 2 * (kb // 8 + (4 if pairs else 0))
+        med, mn = statistics.median(times[v]), min(times[v])
+        print(f"{':'.join(str(x) for x in v):28s} median {med:8.4f} ms  min {mn:8.4f}  "
+              f"{alg / med / 1e6:8.1f} GB/s", flush=True)
+    for v in variants:
+        stamped = (v[0] == "v4" and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v5" and v[7] & 8)
+        if not stamped:
+            continue
+        err.zero_()
+        st.zero_()
+        ticket.zero_()
+        run(v)
+        torch.cuda.synchronize()
+        tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
+        a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+        if v[0] in ("v4", "v5"):
+            m = a_[:, :6].mean(0)
+            d = np.diff(np.concatenate([[0.0], m]))
+            names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
+                     "reorder+lookback+B4", "store+drain"]
+            print(f"stamps {v}: " + ", ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d))
+                  + f"  total={m[5]:.0f}  (p90 reorder+lb {np.percentile(a_[:, 4] - a_[:, 3], 90):.0f})",
+                  flush=True)
+        else:
+            m = a_[:, :7].mean(0)
+            print(f"stamps {v}: ticket+load={m[6]:.0f} rank+B1={m[1]-m[0]:.0f} scan+B2={m[2]-m[1]:.0f} "
+                  f"lookback+B3={m[3]-m[2]:.0f} reorder+B4={m[4]-m[3]:.0f} store+drain={m[5]-m[4]:.0f} "
+                  f"total={m[5]:.0f}", flush=True)
+        starts = a_[:, 7] * 256.0
+        span = (starts.max() - starts.min())
+        print(f"   tiles={tiles} start spread {span:.0f} cycles", flush=True)
+
+
+if __name__ == "__main__":
+    main()
