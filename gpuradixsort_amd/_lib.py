@@ -38,6 +38,13 @@ class grs_timing(ctypes.Structure):
                 ("pass_ms", c_float * 16), ("copy_ms", c_float)]
 
 
+class grs_key_extract(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("offset", c_uint32), ("transform", c_int),
+                ("lo", c_float * 3), ("hi", c_float * 3)]
+
+
+GRS_EXTRACT_FIELD, GRS_EXTRACT_MORTON3 = 0, 1
+
 # (name, restype, argtypes) of every symbol include/grs.h declares
 SIGNATURES = [
     ("grs_version", c_int, []),
@@ -76,6 +83,8 @@ SIGNATURES = [
     ("grs_sort_host", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                               c_void_p]),
     ("grs_key_transform", c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p]),
+    ("grs_sort_records", c_int, [c_void_p, c_void_p, c_size_t, c_size_t, POINTER(grs_key_extract),
+                                 c_void_p]),
     ("grs_scan_scratch_bytes", c_size_t, [c_size_t]),
     ("grs_exclusive_scan_u32", c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_size_t,
                                        c_void_p]),

@@ -41,15 +41,23 @@ grs_status set_err(grs_status s, const std::string& msg) {
       return set_err(GRS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
-// Tile shapes of the pass (grs_onesweep_v4, grs_pass.hpp).  Measured on MI355X
-// (tools/lab2.py, 2^27 keys, ms per pass against the round-1 512-thread pass on the same box:
-// u32 keys 0.249 vs 0.290, u32 pairs 0.505 vs 0.557, u64 keys 0.479 vs 0.514, u64 pairs
-// 0.798 vs 0.790): 16 waves per workgroup and the largest tile that fits LDS beside the
-// 16 x RADIX wave counters.  Big: one 1024-thread workgroup per CU.  Small (grids of few big
-// tiles per CU, e.g. BASELINE C2's 16M keys): 256-thread workgroups of 4K-16K keys, four per
-// CU, so the grid has no tail.
+// Tile shapes of the pass (grs_onesweep_v4, grs_pass.hpp).  Measured on MI355X inside the
+// sort (tools/ab_r2.sh, ab_r2b.sh; C4 = 2^30 u32 keys, same box, Gkeys/s): 16 waves per
+// workgroup, 16-bit wave counters (half the counter LDS, so the tile grows to what LDS then
+// holds: 36K u32 keys) and the look-back issued after the reorder: 126.5 vs 120.7 (32K tiles,
+// 32-bit counters, early look-back), 125.2 (512 x 72), 107.7 (nontemporal tile loads); C3
+// 59.9 vs 59.2, C5 33.4 vs 32.8.  Big: one 1024-thread workgroup per CU.  Small (grids of
+// less than one big tile per CU): 256-thread workgroups of 1.5K-4K keys, four per CU.
 template <typename K, bool PAIRS>
 struct BigTile {
+  static constexpr int BLOCK = 1024, MINW = 1;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 11 : 17);
+  static constexpr int TILE = BLOCK * ITEMS;
+};
+// 4-bit digits (BASELINE C2): 32-bit wave counters (16-bit ones put 64 lanes on 8 words) and
+// the look-back before the reorder (tools/lab2.py at 2^24 keys: 1024 x 32 0.042 ms per pass).
+template <typename K, bool PAIRS>
+struct BigTile4 {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 32) : (PAIRS ? 10 : 16);
   static constexpr int TILE = BLOCK * ITEMS;
@@ -60,6 +68,13 @@ struct SmallTile {
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 8 : 16) : (PAIRS ? 6 : 8);
   static constexpr int TILE = BLOCK * ITEMS;
 };
+// Ballot-match fallback (32-bit wave counters): the round's first 16-wave shapes.
+template <typename K, bool PAIRS>
+struct MatchTile {
+  static constexpr int BLOCK = 1024, MINW = 1;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 32) : (PAIRS ? 10 : 16);
+  static constexpr int TILE = BLOCK * ITEMS;
+};
 // Partition pass (key-range buckets for the multi-GPU exchange): its digit needs the element
 // index, so the reordered digits are kept in LDS (one byte per key) beside the tile.
 template <typename K, bool PAIRS>
@@ -68,8 +83,15 @@ struct PartTile {
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 24) : (PAIRS ? 8 : 16);
   static constexpr int TILE = BLOCK * ITEMS;
 };
-constexpr uint32_t kPassOpt = 128;                     // nontemporal tile loads (grs_pass.hpp)
-constexpr uint32_t kMatchOpt = 128 | 512;              // + ballot-match ranking (fallback)
+// Pass options (grs_pass.hpp OPT bits): big tiles 16-bit wave counters + look-back after the
+// reorder; small tiles the look-back after the reorder.  Default-policy tile loads:
+// nontemporal loads made the pass alone faster in tools/lab2.py but the sort slower (C4 2^30
+// keys, same box: 107.5 vs 122.4 Gkeys/s), the pass reading what the previous pass just wrote.
+constexpr uint32_t kBigOpt = 256 | 16;
+constexpr uint32_t kBig4Opt = 0;
+constexpr uint32_t kSmallOpt = 16;
+constexpr uint32_t kNtOpt = 256 | 16 | 128;            // GRS_PASS_NT=1 (A/B)
+constexpr uint32_t kMatchOpt = 512 | 16;               // ballot-match ranking (fallback)
 
 // Status words of one look-back buffer for `tiles` tiles of radix `radix`.
 size_t status_words_for(size_t tiles, size_t radix) { return grs::lb3_status_words(tiles, radix); }
@@ -171,11 +193,14 @@ struct grs_sorter {
   // grs_sort_sharded scratch (first use): samples, gathered samples, count matrix, digit
   void* shard_buf = nullptr;
   size_t shard_bytes = 0;
+  void* rec_buf = nullptr;         // grs_sort_records scratch: keys | index | record copy
+  size_t rec_bytes = 0;
   uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
   int hist_grid_cap = 1024;        // GRS_HIST_GRID: cap of the upfront histogram grid
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
   int u32_variant = 0;             // GRS_U32_PASS: u32-keys pass variant (0 = default; lab A/B)
+  bool pass_nt = false;            // GRS_PASS_NT=1: nontemporal tile loads in the big pass (A/B)
 };
 
 extern "C" {
@@ -212,6 +237,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->seg64) grs_destroy(s->seg64);
   if (s->host_stage) (void)hipFree(s->host_stage);
   if (s->shard_buf) (void)hipFree(s->shard_buf);
+  if (s->rec_buf) (void)hipFree(s->rec_buf);
   if (s->shard_host) (void)hipHostFree(s->shard_host);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
@@ -228,17 +254,22 @@ namespace {
 // Tiles of the pass a sort of n items launches, and which shape (true = big).
 bool use_big_tiles(const grs_sorter* s, size_t n, size_t big_tile) {
   if (s->tile_mode >= 0) return s->tile_mode == 1;
-  // a grid of big tiles needs enough tiles per CU for its tail to stay small
-  return (n + big_tile - 1) / big_tile >= 6 * static_cast<size_t>(std::max(1, s->cus));
+  // big tiles from one tile per CU up (tools/lab2.py, C2's 2^24 keys at 4-bit digits: 32K-key
+  // tiles 0.042 ms per pass, two per CU, against 0.070 for 4K-key tiles, 4 workgroups per CU)
+  return (n + big_tile - 1) / big_tile >= static_cast<size_t>(std::max(1, s->cus));
 }
 
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
 template <typename K, bool PAIRS>
 size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
-  const size_t big = BigTile<K, PAIRS>::TILE, small = SmallTile<K, PAIRS>::TILE;
-  // small tiles are used below 6 big tiles per CU (or everywhere when forced)
-  const size_t small_cap = s->tile_mode == 0 ? cap : std::min(cap, 6 * big * std::max(1, s->cus));
-  size_t w = std::max(status_words_for((cap + big - 1) / big, radix),
+  const size_t big = std::min(BigTile<K, PAIRS>::TILE, BigTile4<K, PAIRS>::TILE);
+  const size_t small = SmallTile<K, PAIRS>::TILE;
+  size_t w0 = 0;
+  // small tiles are used below one big tile per CU (or everywhere when forced)
+  const size_t small_cap = s->tile_mode == 0 ? cap : std::min(cap, big * std::max(1, s->cus));
+  const size_t match = MatchTile<K, PAIRS>::TILE;
+  w0 = status_words_for((cap + match - 1) / match, radix);
+  size_t w = std::max(std::max(w0, status_words_for((cap + big - 1) / big, radix)),
                       status_words_for((small_cap + small - 1) / small, radix));
   // the partition pass (16 buckets)
   const size_t part = PartTile<K, PAIRS>::TILE;
@@ -280,6 +311,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
   if (const char* e = std::getenv("GRS_U32_PASS")) s->u32_variant = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("GRS_PASS_NT")) s->pass_nt = std::atoi(e) != 0;
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(capacity, 1);
   const size_t radix = std::max<size_t>(size_t(1) << radix_bits, 16);
@@ -357,10 +389,13 @@ namespace {
 template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, typename DigitF>
 grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
                        uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
-                       uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream) {
+                       uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream,
+                       uint32_t expect_tile = 0) {
   const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
   if (status_words_for(tiles, 1u << RB) > s->status_words)
     return set_err(GRS_ECAPACITY, "status buffer too small");
+  if (expect_tile != 0 && expect_tile != static_cast<uint32_t>(Tile::TILE))
+    return set_err(GRS_EINVAL, "internal: pass tile differs from the zeroed status layout");
   hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW, OPT,
                                            DigitF>),
                      dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
@@ -378,12 +413,22 @@ struct U32Var {
 template <typename K, bool PAIRS, int RB>
 grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begin_bit,
                     int end_bit, hipStream_t stream) {
-  using Big = BigTile<K, PAIRS>;
+  using Big = std::conditional_t<RB == 8, BigTile<K, PAIRS>, BigTile4<K, PAIRS>>;
   using Small = SmallTile<K, PAIRS>;
+  constexpr uint32_t kBig = RB == 8 ? kBigOpt : kBig4Opt;
   constexpr int RADIX = 1 << RB;
   const bool big = use_big_tiles(s, n, Big::TILE);
   const int passes = (end_bit - begin_bit + RB - 1) / RB;
-  const uint32_t tiles = (n + (big ? Big::TILE : Small::TILE) - 1) / (big ? Big::TILE : Small::TILE);
+  // the tile size the passes below launch with: it sets the status layout (tile words, then
+  // group words) that the histogram kernel zeroes for pass 0 and every pass for the next one
+  uint32_t tile = big ? Big::TILE : Small::TILE;
+  if (s->rank_mode != 0 && big) tile = MatchTile<K, PAIRS>::TILE;
+  if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) {
+    if (s->rank_mode == 0 && big && s->u32_variant != 0)
+      tile = s->u32_variant == 1 ? 1024 * 32 : s->u32_variant == 2 ? 512 * 72
+             : s->u32_variant == 3 ? 1024 * 36 : 1024 * 32;
+  }
+  const uint32_t tiles = (n + tile - 1) / tile;
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
@@ -429,22 +474,26 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     const Dig dig{shift, (1u << bits) - 1u};
     const uint32_t* ph = hist + p * RADIX;
     if (s->rank_mode != 0) {
-      r = big ? launch_pass<K, PAIRS, RB, Big, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream)
-              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream);
+      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
+              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (u32_lab(big)) {
-      using V1 = U32Var<1024, 32, 144>;   // look-back issued after the reorder
-      using V2 = U32Var<512, 72, 144>;    // 8 waves, 36K-key tiles
-      using V3 = U32Var<1024, 36, 400>;   // 16-bit wave counters, 36K-key tiles
-      using V4 = U32Var<1024, 32, 0>;     // default-policy tile loads
+      using V1 = U32Var<1024, 32, 16>;    // 32-bit wave counters, 32K-key tiles
+      using V2 = U32Var<512, 72, 16>;     // 8 waves, 36K-key tiles
+      using V3 = U32Var<1024, 36, 256>;   // look-back issued before the reorder
+      using V4 = U32Var<1024, 32, 0>;     // round-2 first default: 32-bit counters, early look-back
+#define GRS_U32V(V) r = launch_pass<K, PAIRS, RB, V, V::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
       if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) switch (s->u32_variant) {
-        case 1: r = launch_pass<K, PAIRS, RB, V1, V1::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
-        case 2: r = launch_pass<K, PAIRS, RB, V2, V2::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
-        case 3: r = launch_pass<K, PAIRS, RB, V3, V3::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
-        default: r = launch_pass<K, PAIRS, RB, V4, V4::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream); break;
+        case 1: GRS_U32V(V1); break;
+        case 2: GRS_U32V(V2); break;
+        case 3: GRS_U32V(V3); break;
+        default: GRS_U32V(V4); break;
       }
+#undef GRS_U32V
+    } else if (s->pass_nt && big) {
+      r = launch_pass<K, PAIRS, RB, Big, kNtOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else {
-      r = big ? launch_pass<K, PAIRS, RB, Big, kPassOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream)
-              : launch_pass<K, PAIRS, RB, Small, kPassOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream);
+      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
+              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     }
     if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;
@@ -489,7 +538,7 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
   GRS_HIP(hipGetLastError());
   grs_status r;
   if (s->rank_mode == 0)
-    r = launch_pass<K, PAIRS, 4, T, kPassOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
+    r = launch_pass<K, PAIRS, 4, T, kSmallOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
                                              s->ctrl + GRS_CTRL_TICKETS, s->status,
                                              s->status + s->status_words, stream);
   else
@@ -1068,6 +1117,7 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
                       al(static_cast<size_t>(g) * g * 4) + al(sizeof(Dig));
   if (s->shard_bytes < need) {
     if (s->shard_buf) (void)hipFree(s->shard_buf);
+  if (s->rec_buf) (void)hipFree(s->rec_buf);
     s->shard_buf = nullptr;
     s->shard_bytes = 0;
     if (hipMalloc(&s->shard_buf, need) != hipSuccess) {
@@ -1256,6 +1306,63 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
     return set_err(GRS_EINVAL, "grs_shard_plan_host: bad argument");
   shard_plan(count_matrix, nranks, rank, send_off, recv_off, n_out);
   return GRS_OK;
+}
+
+grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t record_bytes,
+                            const grs_key_extract* key, void* stream) {
+  if (!s || !key) return set_err(GRS_EINVAL, "grs_sort_records: NULL argument");
+  if (!s->pairs) return set_err(GRS_EINVAL, "grs_sort_records: needs a sorter created with a payload");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_records: n exceeds capacity");
+  const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  if (record_bytes == 0 || record_bytes > 0xFFFFFFFFull ||
+      (key->kind != GRS_EXTRACT_FIELD && key->kind != GRS_EXTRACT_MORTON3) ||
+      (key->kind == GRS_EXTRACT_FIELD && (key->offset + kb > record_bytes || key->transform < 0 ||
+                                          key->transform > 2)) ||
+      (key->kind == GRS_EXTRACT_MORTON3 && static_cast<size_t>(key->offset) + 12 > record_bytes))
+    return set_err(GRS_EINVAL, "grs_sort_records: key field outside the record or bad kind");
+  if (n == 0) return GRS_OK;
+  if (!d_records) return set_err(GRS_EINVAL, "grs_sort_records: NULL records");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t need = al(n * kb) + al(n * 4) + al(n * record_bytes);
+  grs_status r = GRS_OK;
+  if (s->rec_bytes < need) {
+    if (s->rec_buf) (void)hipFree(s->rec_buf);
+    s->rec_buf = nullptr;
+    s->rec_bytes = 0;
+    if (hipMalloc(&s->rec_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      r = set_err(GRS_ENOMEM, "grs_sort_records: scratch allocation failed");
+    } else {
+      s->rec_bytes = need;
+    }
+  }
+  char* b = static_cast<char*>(s->rec_buf);
+  void* keys = b;
+  uint32_t* idx = reinterpret_cast<uint32_t*>(b + al(n * kb));
+  void* copy = b + al(n * kb) + al(n * 4);
+  const grs::KeyExtract kx{key->kind, key->offset, key->transform,
+                           {key->lo[0], key->lo[1], key->lo[2]}, {key->hi[0], key->hi[1], key->hi[2]}};
+  if (r == GRS_OK) {   // K1: one fused pre-pass, key + index
+    if (kb == 4)
+      hipLaunchKernelGGL(grs::grs_extract_keys<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                         static_cast<const uint8_t*>(d_records), static_cast<uint64_t>(n),
+                         static_cast<uint32_t>(record_bytes), kx, static_cast<uint32_t*>(keys), idx);
+    else
+      hipLaunchKernelGGL(grs::grs_extract_keys<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                         static_cast<const uint8_t*>(d_records), static_cast<uint64_t>(n),
+                         static_cast<uint32_t>(record_bytes), kx, static_cast<uint64_t*>(keys), idx);
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_records: launch");
+  }
+  if (r == GRS_OK) r = grs_sort(s, keys, idx, n, stream);                        // stable pairs
+  if (r == GRS_OK) r = grs_gather_records(d_records, copy, idx, n, record_bytes, stream);  // K5
+  if (r == GRS_OK && hipMemcpyAsync(d_records, copy, n * record_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_records: copy back");                          // copy-back
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
 }
 
 const char* grs_pass_kernel(const grs_sorter* s, size_t n) {

@@ -2,16 +2,24 @@
 // OriginalDataSsbo(N) <- shuffled 0..N-1; ParallelSort(ssbo); Sort() twice; verify.
 //
 // usage: grs_demo [N] [seed]    (prints one line; exit 0 iff the output is exactly 0..N-1)
+//        grs_demo particles [N] [seed]
+//        the reference's stated purpose (ParallelSort.h:13-31): N Particle structs sorted by the
+//        Morton code of their position through ParallelSort(RecordSsbo<Particle>, MortonKey);
+//        verified against a host std::stable_sort by the same code
 // The reference's std::random_shuffle (main.cpp:125) is replaced by a seeded Fisher-Yates
 // over splitmix64 so the run is reproducible; verification strengthens the reference's
 // adjacent-order check (ParallelSort.cpp:336-352) to "output == 0..N-1".
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <cstring>
 #include <memory>
+#include <numeric>
 #include <vector>
 
 #include "../../include/grs_parallel_sort.hpp"
@@ -23,7 +31,69 @@ static uint64_t splitmix64(uint64_t& s) {
   return x ^ (x >> 31);
 }
 
+struct Particle {          // 28 bytes: position, velocity, id (= original index)
+  float pos[3];
+  float vel[3];
+  unsigned int id;
+};
+
+static uint32_t spread10(uint32_t v) {
+  v &= 0x3FFu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  return (v | (v << 2)) & 0x09249249u;
+}
+static uint32_t cell10(float v, float lo, float hi) {
+  const float t = (v - lo) / (hi - lo);
+  if (!(t > 0.0f)) return 0u;
+  if (t >= 1.0f) return 1023u;
+  const uint32_t q = static_cast<uint32_t>(t * 1024.0f);
+  return q < 1024u ? q : 1023u;
+}
+
+static int particles(unsigned n, uint64_t seed) {
+  const float lo[3] = {-1.0f, -1.0f, -1.0f}, hi[3] = {1.0f, 1.0f, 1.0f};
+  std::vector<Particle> host(n);
+  for (unsigned i = 0; i < n; ++i) {
+    for (int a = 0; a < 3; ++a) {
+      host[i].pos[a] = static_cast<float>(splitmix64(seed) >> 40) / 16777216.0f * 2.2f - 1.1f;
+      host[i].vel[a] = static_cast<float>(a);
+    }
+    host[i].id = i;
+  }
+  auto buf = std::make_shared<RecordSsbo<Particle>>(n);
+  buf->Upload(host);
+  ParallelSort ps(buf, grs::MortonKey(offsetof(Particle, pos), lo, hi));
+  ps.Sort();
+  const std::vector<Particle> out = buf->Download();
+  std::vector<uint32_t> code(n);
+  for (unsigned i = 0; i < n; ++i) {
+    const Particle& p = host[i];
+    code[i] = (spread10(cell10(p.pos[0], lo[0], hi[0])) << 2) |
+              (spread10(cell10(p.pos[1], lo[1], hi[1])) << 1) | spread10(cell10(p.pos[2], lo[2], hi[2]));
+  }
+  std::vector<unsigned> perm(n);
+  std::iota(perm.begin(), perm.end(), 0u);
+  std::stable_sort(perm.begin(), perm.end(), [&](unsigned a, unsigned b) { return code[a] < code[b]; });
+  unsigned bad = 0;
+  for (unsigned i = 0; i < n; ++i)
+    bad += std::memcmp(&out[i], &host[perm[i]], sizeof(Particle)) != 0;
+  std::printf("grs_demo particles n=%u sorted=%s mismatches=%u\n", n, bad ? "NO" : "yes", bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "particles") == 0) {
+    const unsigned n = argc > 2 ? static_cast<unsigned>(std::strtoul(argv[2], nullptr, 10)) : 100000u;
+    const uint64_t seed = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 1;
+    try {
+      return particles(n, seed);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "grs_demo: %s\n", e.what());
+      return 2;
+    }
+  }
   const unsigned n = argc > 1 ? static_cast<unsigned>(std::strtoul(argv[1], nullptr, 10)) : 1000000u;
   uint64_t seed = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1;
   try {

@@ -173,11 +173,14 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 // distribution — with 4-bit digits 64 lanes share 16 counters).  Two digits share one
 // 32-bit word as 16-bit halves; a copy counts at most ceil(n / grid / COPIES) keys, which the
 // launch keeps below 2^16 (grid > n / 2^18, COPIES >= 8).  32 KB of LDS per block.
-template <typename K, int RB>
+// Counting always happens on 8-bit "super digits"; 4-bit passes (BASELINE C2) read their
+// counts off them: pass 2q's digit is the low nibble of super digit q, pass 2q+1's the high
+// nibble, so hist4[2q][d] = sum_h cnt8[q][16h + d] and hist4[2q+1][d] = sum_l cnt8[q][16d + l].
+// That is half the LDS atomics of counting 4-bit digits directly (4 instead of 8 per u32 key).
+template <typename K>
 struct HistLayout {
-  static constexpr int RADIX = 1 << RB;
-  static constexpr int MAXP = (8 * sizeof(K) + RB - 1) / RB;
-  static constexpr int PER_COPY = MAXP * (RADIX / 2);   // words of one copy
+  static constexpr int MAXQ = static_cast<int>(sizeof(K));  // super digits per key
+  static constexpr int PER_COPY = MAXQ * 128;                // words of one copy
   static constexpr int COPIES = (8192 / PER_COPY) >= 32 ? 32 : (8192 / PER_COPY);
   static constexpr int WORDS = PER_COPY * COPIES;
   static_assert(COPIES >= 8, "16-bit counters need >= 8 copies");
@@ -187,11 +190,12 @@ template <typename K, int RB>
 __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
     uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words) {
-  using HL = HistLayout<K, RB>;
-  constexpr int RADIX = HL::RADIX;
-  constexpr int MAXP = HL::MAXP;
+  static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
+  using HL = HistLayout<K>;
+  constexpr int MAXQ = HL::MAXQ;
   constexpr int COPIES = HL::COPIES;
   __shared__ uint32_t s_hist[HL::WORDS];
+  __shared__ uint32_t s_red[RB == 4 ? MAXQ * 256 : 1];
 
   const uint32_t t = threadIdx.x;
   for (uint32_t i = t; i < HL::WORDS; i += GRS_HIST_BLOCK) s_hist[i] = 0;
@@ -201,21 +205,22 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
   __syncthreads();
 
   const uint32_t copy = t & (COPIES - 1);
-  int shifts[MAXP];
-  uint32_t masks[MAXP];
+  const int supers = (end_bit - begin_bit + 7) / 8;   // super digits covering the bit range
+  int shifts[MAXQ];
+  uint32_t masks[MAXQ];
 #pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    const int s = begin_bit + p * RB;
-    shifts[p] = s;
-    const int bits = (end_bit - s) < RB ? (end_bit - s) : RB;
-    masks[p] = (p < passes && bits > 0) ? ((1u << bits) - 1u) : 0u;
+  for (int q = 0; q < MAXQ; ++q) {
+    const int s = begin_bit + q * 8;
+    shifts[q] = s;
+    const int bits = (end_bit - s) < 8 ? (end_bit - s) : 8;
+    masks[q] = (q < supers && bits > 0) ? ((1u << bits) - 1u) : 0u;
   }
   auto count = [&](K k) {
 #pragma unroll
-    for (int p = 0; p < MAXP; ++p) {
-      if (p < passes) {
-        const uint32_t d = digit_of(k, shifts[p], masks[p]);
-        atomicAdd(&s_hist[(p * (RADIX / 2) + (d >> 1)) * COPIES + copy], 1u << ((d & 1u) << 4));
+    for (int q = 0; q < MAXQ; ++q) {
+      if (q < supers) {
+        const uint32_t d = digit_of(k, shifts[q], masks[q]);
+        atomicAdd(&s_hist[(q * 128 + (d >> 1)) * COPIES + copy], 1u << ((d & 1u) << 4));
       }
     }
   };
@@ -249,14 +254,31 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
        i += gridDim.x * GRS_HIST_BLOCK)
     count(keys[i]);
   __syncthreads();
-  // reduce the copies: one (pass, digit) counter per thread iteration
-  for (uint32_t i = t; i < static_cast<uint32_t>(passes * RADIX); i += GRS_HIST_BLOCK) {
-    const uint32_t p = i / RADIX, d = i % RADIX;
-    const uint32_t* row = &s_hist[(p * (RADIX / 2) + (d >> 1)) * COPIES];
+  // reduce the copies: count of super digit value d at position q
+  auto total8 = [&](uint32_t q, uint32_t d) {
+    const uint32_t* row = &s_hist[(q * 128 + (d >> 1)) * COPIES];
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < COPIES; ++k) c += (row[(k + t) & (COPIES - 1)] >> ((d & 1u) << 4)) & 0xFFFFu;
-    if (c) atomicAdd(&g_hist[i], c);
+    return c;
+  };
+  if constexpr (RB == 8) {
+    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 256); i += GRS_HIST_BLOCK) {
+      const uint32_t c = total8(i / 256, i % 256);
+      if (c) atomicAdd(&g_hist[i], c);
+    }
+  } else {
+    for (uint32_t i = t; i < static_cast<uint32_t>(supers * 256); i += GRS_HIST_BLOCK)
+      s_red[i] = total8(i / 256, i % 256);
+    __syncthreads();
+    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 16); i += GRS_HIST_BLOCK) {
+      const uint32_t p = i / 16, d = i % 16, q = p / 2;
+      const uint32_t* r8 = &s_red[q * 256];
+      uint32_t c = 0;
+#pragma unroll
+      for (int h = 0; h < 16; ++h) c += (p & 1u) ? r8[d * 16 + h] : r8[h * 16 + d];
+      if (c) atomicAdd(&g_hist[i], c);
+    }
   }
 }
 
@@ -363,6 +385,77 @@ __global__ void grs_key_transform(K* __restrict__ keys, uint64_t n, int kind, in
       y = (x & SIGN) ? static_cast<K>(x & ~SIGN) : static_cast<K>(~x);
     }
     keys[i] = y;
+  }
+}
+
+// Key-extraction pre-pass of grs_sort_records (the reference's K1,
+// OriginalDataToIntermediateData.comp:24-52, generalised): key[i] from record i, idx[i] = i.
+// Spreads the low 10 (u32) / 21 (u64) bits of v to every third bit.
+template <typename K>
+__host__ __device__ __forceinline__ K morton_spread(K v) {
+  if constexpr (sizeof(K) == 4) {
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+  } else {
+    v &= 0x1FFFFFull;
+    v = (v | (v << 32)) & 0x001F00000000FFFFull;
+    v = (v | (v << 16)) & 0x001F0000FF0000FFull;
+    v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+    v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+    v = (v | (v << 2)) & 0x1249249249249249ull;
+  }
+  return v;
+}
+
+// Axis value -> cell in [0, 2^B): floor((v - lo) / (hi - lo) * 2^B), clamped; NaN -> 0.
+template <int B>
+__host__ __device__ __forceinline__ uint32_t morton_cell(float v, float lo, float hi) {
+  const float t = (v - lo) / (hi - lo);
+  if (!(t > 0.0f)) return 0u;                       // also NaN and hi <= lo
+  if (t >= 1.0f) return (1u << B) - 1u;
+  const uint32_t q = static_cast<uint32_t>(t * static_cast<float>(1u << B));
+  return q < (1u << B) ? q : (1u << B) - 1u;
+}
+
+struct KeyExtract {   // device copy of grs_key_extract
+  int kind;
+  uint32_t offset;
+  int transform;
+  float lo[3], hi[3];
+};
+
+template <typename T>
+__device__ __forceinline__ T load_unaligned(const uint8_t* p) {
+  T v;
+  __builtin_memcpy(&v, p, sizeof(T));
+  return v;
+}
+
+template <typename K>
+__global__ void grs_extract_keys(const uint8_t* __restrict__ rec, uint64_t n, uint32_t rb,
+                                 const KeyExtract kx, K* __restrict__ keys,
+                                 uint32_t* __restrict__ idx) {
+  constexpr int B = sizeof(K) == 4 ? 10 : 21;
+  constexpr K SIGN = static_cast<K>(1) << (8 * sizeof(K) - 1);
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint8_t* p = rec + i * rb + kx.offset;
+    K k;
+    if (kx.kind == 0) {
+      k = load_unaligned<K>(p);
+      if (kx.transform == 1) k ^= SIGN;
+      else if (kx.transform == 2) k = (k & SIGN) ? static_cast<K>(~k) : static_cast<K>(k | SIGN);
+    } else {
+      const K x = morton_cell<B>(load_unaligned<float>(p), kx.lo[0], kx.hi[0]);
+      const K y = morton_cell<B>(load_unaligned<float>(p + 4), kx.lo[1], kx.hi[1]);
+      const K z = morton_cell<B>(load_unaligned<float>(p + 8), kx.lo[2], kx.hi[2]);
+      k = (morton_spread<K>(x) << 2) | (morton_spread<K>(y) << 1) | morton_spread<K>(z);
+    }
+    keys[i] = k;
+    idx[i] = static_cast<uint32_t>(i);
   }
 }
 

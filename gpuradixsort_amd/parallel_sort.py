@@ -13,6 +13,7 @@ records by index (K5, SortOriginalData.comp:27-51) and copy them back (ParallelS
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -71,32 +72,64 @@ class ParallelSort:
 
 
 class RecordSort:
-    """Sort arbitrary fixed-size records by a uint32 key (the reference's intended use:
-    ParallelSort.h:13-31, e.g. particles by Morton code).
+    """Sort fixed-size records (a Particle struct, ...) by a key — the reference's intended
+    use (ParallelSort.h:13-31: "sort the particles ... by Morton codes").
 
-    records: device tensor of shape (N, record_bytes) uint8 (or any contiguous tensor whose
-    first dimension is N); keys: device uint32 tensor of N keys (the K1 key-extraction hook,
-    OriginalDataToIntermediateData.comp:12-19,42, is the caller computing `keys`)."""
+    records: contiguous device tensor whose first dimension is N (e.g. uint8 (N, record_bytes)).
+    The key comes from ONE of:
+      field=offset [, transform]   the key-width field at that byte offset of every record
+                                   (transform: KEYS_UNSIGNED / KEYS_SIGNED / KEYS_FLOAT)
+      morton=(offset, lo, hi)      Morton code of the float x, y, z at offset (10 bits per axis
+                                   with key_bits=32, 21 with 64), normalised by lo / hi
+    — both run the K1 key-extraction hook inside libgrs (grs_sort_records: fused extraction
+    pre-pass, stable (key, index) sort, K5 gather, copy back) — or
+      keys=tensor                  precomputed device keys (sorted along with the records, in
+                                   place: the caller's tensor ends up in key order)
+    """
 
-    def __init__(self, capacity: int, radix_bits: int = 8, device: Optional[int] = None):
+    def __init__(self, capacity: int, key_bits: int = 32, radix_bits: int = 8,
+                 device: Optional[int] = None):
         self.capacity = int(capacity)
-        self._sorter = RadixSorter(max(self.capacity, 1), key_bits=32, pairs=True,
+        self.key_bits = int(key_bits)
+        self._sorter = RadixSorter(max(self.capacity, 1), key_bits=key_bits, pairs=True,
                                    radix_bits=radix_bits, device=device)
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self._idx = torch.empty(max(self.capacity, 1), dtype=torch.uint32, device=dev)
 
-    def sort(self, records: torch.Tensor, keys: torch.Tensor,
+    def sort(self, records: torch.Tensor, keys: Optional[torch.Tensor] = None, *,
+             field: Optional[int] = None, transform: int = 0, morton=None,
              stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
-        n = keys.numel()
-        if records.shape[0] != n:
-            raise ValueError("records and keys disagree on N")
+        if not records.is_cuda or not records.is_contiguous():
+            raise ValueError("records must be a contiguous device tensor")
+        n = records.shape[0] if records.dim() else 0
+        if sum(x is not None for x in (keys, field, morton)) != 1:
+            raise ValueError("give exactly one of keys=, field=, morton=")
+        if n > self.capacity:
+            raise ValueError("more records than the capacity")
         if n == 0:
             return records
         rb = records.numel() * records.element_size() // n
-        idx = self._idx[:n]
-        iota_u32(idx, 0, stream)                       # K1: _globalIndexOfOriginalData = tid
-        self._sorter.sort(keys, idx, n=n, stream=stream)  # stable (key, idx) sort
-        copy = torch.empty_like(records)
-        gather_records(records, copy, idx, n, rb, stream)  # K5 gather
-        records.copy_(copy)                             # copy back
+        if keys is not None:
+            if keys.numel() < n:
+                raise ValueError("records and keys disagree on N")
+            idx = self._idx[:n]
+            iota_u32(idx, 0, stream)                       # K1: _globalIndexOfOriginalData = tid
+            self._sorter.sort(keys, idx, n=n, stream=stream)  # stable (key, idx) sort, in place
+            copy = torch.empty_like(records)
+            gather_records(records, copy, idx, n, rb, stream)  # K5 gather
+            records.copy_(copy)                             # copy back
+            return records
+        from ._lib import GRS_EXTRACT_FIELD, GRS_EXTRACT_MORTON3, check, grs_key_extract, lib
+        from .sorter import _ptr, _stream_ptr
+
+        kx = grs_key_extract()
+        if field is not None:
+            kx.kind, kx.offset, kx.transform = GRS_EXTRACT_FIELD, int(field), int(transform)
+        else:
+            off, lo, hi = morton
+            kx.kind, kx.offset = GRS_EXTRACT_MORTON3, int(off)
+            for a in range(3):
+                kx.lo[a], kx.hi[a] = float(lo[a]), float(hi[a])
+        check(lib().grs_sort_records(self._sorter._h, _ptr(records), n, rb, ctypes.byref(kx),
+                                     _stream_ptr(stream)), "grs_sort_records")
         return records

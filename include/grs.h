@@ -226,6 +226,34 @@ grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
 grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, int inverse,
                              void* stream);
 
+/* Record sort with a key-extraction hook: the reference's K1 (OriginalDataToIntermediateData
+ * .comp:12-19,42: "adapt to whatever needs to be sorted") + pair sort + K5 gather + copy-back
+ * (SortOriginalData.comp:27-51, ParallelSort.cpp:300-320), for records of any size — the use
+ * the reference is built for: "sort the particles ... by Morton codes" (ParallelSort.h:13-31).
+ * One fused pre-pass extracts every record's key (and its index), the (key, index) pairs are
+ * sorted stably, the records are gathered by index into sorter-owned scratch and copied back,
+ * so d_records[0..n) ends up sorted in place.  Needs a sorter created with a payload; the key
+ * width is the sorter's (u32 / u64).
+ *   GRS_EXTRACT_FIELD    key = the key-width field at byte `offset` of the record, through
+ *                        `transform` (GRS_KEYS_UNSIGNED / SIGNED / FLOAT: signed and IEEE
+ *                        fields sort in their own order)
+ *   GRS_EXTRACT_MORTON3  key = Morton (Z-order) code of the float x, y, z at `offset`,
+ *                        offset + 4, offset + 8: each axis mapped to [0, 2^B) by
+ *                        floor((v - lo) / (hi - lo) * 2^B), clamped (NaN -> 0), B = 10 for
+ *                        u32 keys, 21 for u64; bits interleaved x-y-z from the top
+ * Scratch (keys + index + one copy of the records) is allocated on first use and kept. */
+#define GRS_EXTRACT_FIELD 0
+#define GRS_EXTRACT_MORTON3 1
+typedef struct grs_key_extract {
+  int kind;           /* GRS_EXTRACT_* */
+  uint32_t offset;    /* byte offset of the field (FIELD) or of x (MORTON3) in the record */
+  int transform;      /* FIELD: GRS_KEYS_UNSIGNED / SIGNED / FLOAT */
+  float lo[3];        /* MORTON3: lower bounds of x, y, z */
+  float hi[3];        /* MORTON3: upper bounds of x, y, z */
+} grs_key_extract;
+grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t record_bytes,
+                            const grs_key_extract* key, void* stream);
+
 /* Stand-alone device-wide exclusive prefix sum of uint32 (sums wrap mod 2^32), the
  * reference's K3a + K3b (ParallelPrefixScan.comp:41-196, ParallelSort.cpp:253-274) as one
  * reduce-then-scan (three launches).  d_out may equal d_in; both 16-byte aligned.  d_total (nullable) receives the sum of all

@@ -96,16 +96,99 @@ class OriginalDataSsbo {
   OriginalData* _data = nullptr;
 };
 
-// The compute controller: bound to one OriginalDataSsbo, owns the sort scratch.
+// Device buffer of user records of any size (a Particle struct, ...): the record form of
+// OriginalDataSsbo for ParallelSort's record constructor.
+template <typename Record>
+class RecordSsbo {
+ public:
+  typedef std::shared_ptr<RecordSsbo<Record>> SHARED_PTR;
+
+  explicit RecordSsbo(unsigned int numItems) : _numItems(numItems) {
+    if (numItems) {
+      grs::check_hip(hipMalloc(&_data, sizeof(Record) * numItems), "RecordSsbo");
+      grs::check_hip(hipMemset(_data, 0, sizeof(Record) * numItems), "RecordSsbo");
+    }
+  }
+  ~RecordSsbo() {
+    if (_data) (void)hipFree(_data);
+  }
+  RecordSsbo(const RecordSsbo&) = delete;
+  RecordSsbo& operator=(const RecordSsbo&) = delete;
+
+  unsigned int NumItems() const { return _numItems; }
+  Record* DevicePtr() const { return _data; }
+  void Upload(const std::vector<Record>& v) {
+    if (v.size() != _numItems) throw std::invalid_argument("RecordSsbo::Upload: size mismatch");
+    if (_numItems)
+      grs::check_hip(hipMemcpy(_data, v.data(), sizeof(Record) * _numItems, hipMemcpyHostToDevice),
+                     "RecordSsbo::Upload");
+  }
+  std::vector<Record> Download() const {
+    std::vector<Record> v(_numItems);
+    if (_numItems)
+      grs::check_hip(hipMemcpy(v.data(), _data, sizeof(Record) * _numItems, hipMemcpyDeviceToHost),
+                     "RecordSsbo::Download");
+    return v;
+  }
+
+ private:
+  unsigned int _numItems = 0;
+  Record* _data = nullptr;
+};
+
+// Key-extraction specs for the record constructor (the K1 hook, grs_sort_records).
+namespace grs {
+inline grs_key_extract FieldKey(uint32_t offset, int transform = GRS_KEYS_UNSIGNED) {
+  grs_key_extract k{};
+  k.kind = GRS_EXTRACT_FIELD;
+  k.offset = offset;
+  k.transform = transform;
+  return k;
+}
+inline grs_key_extract MortonKey(uint32_t offset, const float lo[3], const float hi[3]) {
+  grs_key_extract k{};
+  k.kind = GRS_EXTRACT_MORTON3;
+  k.offset = offset;
+  for (int i = 0; i < 3; ++i) {
+    k.lo[i] = lo[i];
+    k.hi[i] = hi[i];
+  }
+  return k;
+}
+}  // namespace grs
+
+// The compute controller: bound to one data buffer, owns the sort scratch.
+//  * ParallelSort(OriginalDataSsbo)           the reference's constructor (ParallelSort.h:46):
+//                                             4-byte records whose key is the record
+//  * ParallelSort(RecordSsbo<Record>, key)    records of any size sorted by a key extracted
+//                                             from each record (a field, or a Morton code of a
+//                                             float3 position: "sort the particles ... by Morton
+//                                             codes", ParallelSort.h:13-31)
 class ParallelSort {
  public:
   explicit ParallelSort(const OriginalDataSsbo::SHARED_PTR& dataToSort, void* stream = nullptr)
-      : _originalDataSsbo(dataToSort), _stream(stream) {
+      : _keep(dataToSort), _stream(stream) {
     if (!dataToSort) throw std::invalid_argument("ParallelSort: null OriginalDataSsbo");
+    _data = dataToSort->DevicePtr();
+    _numItems = dataToSort->NumItems();
     int dev = 0;
     grs::check_hip(hipGetDevice(&dev), "ParallelSort");
     // 4-byte records whose key is the record itself: a keys-only u32 sort at 8-bit digits.
-    grs::check(grs_create(&_sorter, dataToSort->NumItems(), GRS_KEY_U32, 0, 8, dev),
+    grs::check(grs_create(&_sorter, _numItems, GRS_KEY_U32, 0, 8, dev), "ParallelSort: grs_create");
+  }
+
+  // u32 keys (key_bits = 32) or u64 keys (64) extracted by `key`; stable.
+  template <typename Record>
+  ParallelSort(const std::shared_ptr<RecordSsbo<Record>>& dataToSort, const grs_key_extract& key,
+               int key_bits = 32, void* stream = nullptr)
+      : _keep(dataToSort), _stream(stream), _records(true), _recordBytes(sizeof(Record)), _key(key) {
+    if (!dataToSort) throw std::invalid_argument("ParallelSort: null RecordSsbo");
+    if (key_bits != 32 && key_bits != 64) throw std::invalid_argument("ParallelSort: key_bits 32 or 64");
+    _data = dataToSort->DevicePtr();
+    _numItems = dataToSort->NumItems();
+    int dev = 0;
+    grs::check_hip(hipGetDevice(&dev), "ParallelSort");
+    grs::check(grs_create(&_sorter, _numItems, key_bits == 64 ? GRS_KEY_U64 : GRS_KEY_U32, 1, 8, dev),
                "ParallelSort: grs_create");
   }
   ~ParallelSort() { grs_destroy(_sorter); }
@@ -121,9 +204,11 @@ class ParallelSort {
     CheckError();
   }
   void SortAsync() {
-    grs::check(grs_sort(_sorter, _originalDataSsbo->DevicePtr(), nullptr,
-                        _originalDataSsbo->NumItems(), _stream),
-               "ParallelSort::Sort");
+    if (_records)
+      grs::check(grs_sort_records(_sorter, _data, _numItems, _recordBytes, &_key, _stream),
+                 "ParallelSort::Sort");
+    else
+      grs::check(grs_sort(_sorter, _data, nullptr, _numItems, _stream), "ParallelSort::Sort");
   }
   void CheckError() { grs::check(grs_stream_check_error(_sorter, _stream), "ParallelSort::CheckError"); }
 
@@ -136,7 +221,48 @@ class ParallelSort {
   }
 
  private:
-  OriginalDataSsbo::SHARED_PTR _originalDataSsbo;
+  std::shared_ptr<void> _keep;   // the bound buffer stays alive as long as the controller
+  void* _data = nullptr;
+  unsigned int _numItems = 0;
   grs_sorter* _sorter = nullptr;
+  void* _stream = nullptr;
+  bool _records = false;
+  size_t _recordBytes = 4;
+  grs_key_extract _key{};
+};
+
+// Multi-GPU controller (one process per GPU): sorts this rank's shard as part
+// of the global input over an RCCL communicator (grs_sort_sharded).  Output: this rank's
+// contiguous range of the global stable order.
+class ShardedParallelSort {
+ public:
+  // capacity: max(shard, received run) items; nccl_comm: an initialised ncclComm_t
+  ShardedParallelSort(size_t capacity, void* nccl_comm, int key_bits = 32, bool pairs = false,
+                      void* stream = nullptr)
+      : _comm(nccl_comm), _stream(stream) {
+    int dev = 0;
+    grs::check_hip(hipGetDevice(&dev), "ShardedParallelSort");
+    grs::check(grs_create(&_sorter, capacity, key_bits == 64 ? GRS_KEY_U64 : GRS_KEY_U32,
+                          pairs ? 1 : 0, 8, dev),
+               "ShardedParallelSort: grs_create");
+  }
+  ~ShardedParallelSort() { grs_destroy(_sorter); }
+  ShardedParallelSort(const ShardedParallelSort&) = delete;
+  ShardedParallelSort& operator=(const ShardedParallelSort&) = delete;
+
+  // Returns the number of items this rank holds after the sort (in d_keys_out / d_vals_out).
+  size_t Sort(const void* d_keys_in, const uint32_t* d_vals_in, size_t n_local, void* d_keys_out,
+              uint32_t* d_vals_out, size_t out_capacity) {
+    size_t n_out = 0;
+    grs::check(grs_sort_sharded(_sorter, d_keys_in, d_vals_in, n_local, d_keys_out, d_vals_out,
+                                out_capacity, &n_out, _comm, _stream),
+               "ShardedParallelSort::Sort");
+    grs::check(grs_stream_check_error(_sorter, _stream), "ShardedParallelSort::Sort");
+    return n_out;
+  }
+
+ private:
+  grs_sorter* _sorter = nullptr;
+  void* _comm = nullptr;
   void* _stream = nullptr;
 };

@@ -12,8 +12,12 @@ Contents (each restates the reference, amdreallyfast/GpuRadixSort, file:line cit
   * cpu_sort               std::sort / __gnu_parallel::sort (BASELINE.md §4 CPU baseline)
   * ref_device_scan        K3a + K3b composed as ParallelSort.cpp:253-274 drives them
   * key_transform_np,
-    segmented_sort_np      checkers for the §8f extensions (order-preserving key bits,
-                           segmented sort): numpy restatements, no reference counterpart
+    segmented_sort_np,
+    morton3_np,
+    extract_keys_np        checkers for the §8f extensions (order-preserving key bits,
+                           segmented sort, the K1 key-extraction hook): numpy restatements;
+                           the reference names Morton codes as its purpose (ParallelSort.h:13-31)
+                           but defines none, so these are "parity unpinned"
 """
 from __future__ import annotations
 
@@ -211,3 +215,48 @@ def cpu_sort(keys: np.ndarray, threads: int = 1) -> None:
 
 def cpu_stable_sort_pairs(keys: np.ndarray, vals: np.ndarray, threads: int = 1) -> None:
     lib().cpu_stable_sort_pairs_u32(keys, vals, keys.size, threads)
+
+
+def _spread(v: np.ndarray, bits: int) -> np.ndarray:
+    """Spread the low `bits` bits of v to every third bit (Morton interleave)."""
+    v = v.astype(np.uint64) & np.uint64((1 << bits) - 1)
+    out = np.zeros_like(v)
+    for b in range(bits):
+        out |= ((v >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b)
+    return out
+
+
+def morton3_np(xyz: np.ndarray, lo, hi, key_bits: int = 32) -> np.ndarray:
+    """Morton code of float32 positions (N, 3): per axis floor((v - lo) / (hi - lo) * 2^B)
+    clamped to [0, 2^B) with NaN / non-positive -> 0 (B = 10 for u32 keys, 21 for u64),
+    bits interleaved x, y, z from the top — grs_sort_records' GRS_EXTRACT_MORTON3, computed
+    in float32 exactly as the device does."""
+    bits = 10 if key_bits == 32 else 21
+    xyz = np.asarray(xyz, np.float32)
+    cells = []
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        for a in range(3):
+            t = (xyz[:, a] - np.float32(lo[a])) / (np.float32(hi[a]) - np.float32(lo[a]))
+            q = np.zeros(t.shape, np.uint64)
+            pos = t > np.float32(0)
+            top = t >= np.float32(1)
+            mid = pos & ~top
+            q[mid] = (t[mid] * np.float32(1 << bits)).astype(np.uint64)
+            q[top] = (1 << bits) - 1
+            q = np.minimum(q, np.uint64((1 << bits) - 1))
+            cells.append(q)
+    code = (_spread(cells[0], bits) << np.uint64(2)) | (_spread(cells[1], bits) << np.uint64(1)) \
+        | _spread(cells[2], bits)
+    return code.astype(np.uint32 if key_bits == 32 else np.uint64)
+
+
+def extract_keys_np(records: np.ndarray, offset: int, key_bits: int = 32, transform: int = 0):
+    """Key field of every record (uint8 array (N, record_bytes)) at byte `offset`, as the
+    unsigned key grs_sort_records sorts by (transform: 0 unsigned, 1 signed, 2 IEEE float)."""
+    kb = key_bits // 8
+    raw = np.ascontiguousarray(records[:, offset:offset + kb]).view(
+        np.uint32 if kb == 4 else np.uint64).reshape(-1)
+    if transform == 0:
+        return raw.copy()
+    return key_transform_np(raw.view(
+        (np.int32 if kb == 4 else np.int64) if transform == 1 else (np.float32 if kb == 4 else np.float64)))

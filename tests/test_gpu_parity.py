@@ -68,8 +68,8 @@ def distributions(n, kb, rng):
 
 
 # Tile edges of the pass (grs_capi.hip BigTile / SmallTile): small tiles 4096 (u32 keys),
-# 2048 (u32 pairs, u64 keys), 1536 (u64 pairs); big tiles 32768 / 16384 / 10240; look-back
-# groups of 8 tiles.  Sizes up to 2^20 run the small tiles by default; test_tile_shapes pins
+# 2048 (u32 pairs, u64 keys), 1536 (u64 pairs); big tiles 36864 / 17408 / 11264 (ballot-match
+# fallback 32768 / 16384 / 10240); look-back groups of 8 tiles.  Sizes up to 2^20 run the small tiles by default; test_tile_shapes pins
 # the big ones.
 SIZES = [0, 1, 2, 63, 64, 65, 1023, 1024, 1025, 1535, 1537, 2047, 2049, 4095, 4096, 4097,
          12289, 16383, 16385, 32769, 36865, 65536, 98305, 131073, 262145, 1 << 20]
@@ -123,7 +123,7 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_TILE", tile)
-    big = {(32, False): 32768, (32, True): 16384, (64, False): 16384, (64, True): 10240}
+    big = {(32, False): 36864, (32, True): 17408, (64, False): 17408, (64, True): 11264}
     small = {(32, False): 4096, (32, True): 2048, (64, False): 2048, (64, True): 1536}
     t = (big if tile == "big" else small)[(kb, pairs)]
     rng = np.random.default_rng(kb * 10 + pairs)
@@ -176,9 +176,9 @@ def test_ballot_match_fallback(gpu, monkeypatch):
 
 @pytest.mark.parametrize("choice", ["1", "2", "3", "4"])
 def test_u32_pass_alternatives(gpu, monkeypatch, choice):
-    """GRS_U32_PASS pins one of the lab variants of the big u32-keys pass (look-back after the
-    reorder / 512 x 72 tiles / 16-bit wave counters with 36K-key tiles / default-policy
-    loads): same bit-exact results across tile edges."""
+    """GRS_U32_PASS pins one of the lab variants of the big u32-keys pass (32-bit wave
+    counters with 32K-key tiles / 512 x 72 tiles / look-back before the reorder / the round's
+    first default): same bit-exact results across tile edges."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_U32_PASS", choice)

@@ -117,6 +117,9 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 1024, 32, 1, 128) V(32, 1, 1024, 16, 1, 144) V(64, 0, 1024, 16, 1, 144)
     V(64, 1, 1024, 10, 1, 144) V(32, 1, 1024, 18, 1, 400) V(64, 0, 1024, 18, 1, 400)
     V(32, 0, 1024, 36, 1, 272)
+    V(64, 1, 1024, 10, 1, 528) V(64, 1, 1024, 10, 1, 512) V(64, 1, 1024, 10, 1, 16)
+    V(64, 0, 1024, 16, 1, 528) V(32, 1, 1024, 16, 1, 528) V(32, 0, 1024, 32, 1, 528)
+    V(64, 1, 1024, 11, 1, 272)
 #undef V
     default:
       return -1;
@@ -147,6 +150,32 @@ int lab2_v5(int kb, int pairs, int block, int items, int minw, int ch, int opt, 
     V(32, 0, 256, 72, 2, 8, 144) V(32, 0, 256, 72, 2, 16, 144) V(32, 0, 512, 72, 1, 8, 152)
     V(32, 1, 512, 36, 1, 8, 144) V(64, 0, 512, 36, 1, 8, 144)
     V(32, 0, 512, 72, 1, 4, 144) V(32, 0, 512, 72, 1, 2, 144)
+#undef V
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// v4 pass at 4-bit digits (BASELINE C2): block, items, minw, opt
+int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* out, uint32_t n,
+               const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err,
+               void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = ((block * 1000L + items) * 10 + minw) * 1000 + opt;
+  switch (code) {
+#define V(B, I, M, O)                                                                          \
+  case ((B * 1000L + I) * 10 + M) * 1000 + O: {                                                \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
+    hipLaunchKernelGGL((grs::grs_onesweep_v4<uint32_t, false, 4, B, I, M, O>), dim3(tiles),     \
+                       dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
+                       grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
+                       (const grs::RadixDigit<uint32_t>*)nullptr);                             \
+  } break;
+    V(256, 16, 4, 0) V(256, 16, 4, 512) V(256, 16, 4, 16) V(512, 16, 2, 0) V(512, 16, 2, 512)
+    V(1024, 16, 1, 0) V(1024, 16, 1, 512) V(1024, 8, 1, 0) V(1024, 8, 1, 512) V(256, 32, 4, 0)
+    V(256, 32, 4, 512) V(512, 32, 2, 0) V(512, 32, 2, 512) V(1024, 32, 1, 0) V(1024, 32, 1, 512)
+    V(256, 8, 8, 0) V(256, 8, 8, 512) V(128, 16, 8, 0) V(128, 16, 8, 512) V(512, 8, 4, 512)
 #undef V
     default:
       return -1;

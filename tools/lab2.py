@@ -39,6 +39,7 @@ def main():
         f = v.split(":")
         variants.append((f[0],) + tuple(int(x) for x in f[1:]))
     bufs = {}
+    hist4 = {}
     for kb in sorted({v[1] for v in variants}):
         dt = torch.uint32 if kb == 32 else torch.uint64
         keys = torch.empty(n, dtype=dt, device=dev)
@@ -46,6 +47,7 @@ def main():
         k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
         hist = torch.bincount(k64 & 255, minlength=256).to(torch.int32).view(torch.uint32)
         bufs[kb] = (keys, torch.empty_like(keys), hist.contiguous())
+        hist4[kb] = torch.bincount(k64 & 15, minlength=16).to(torch.int32).view(torch.uint32).contiguous()
     vin = torch.arange(n, dtype=torch.int64, device=dev).to(torch.int32).view(torch.uint32)
     vout = torch.empty_like(vin)
     ticket = torch.zeros(64, dtype=torch.uint32, device=dev)   # also the v5 XcdSched (32 words)
@@ -60,7 +62,10 @@ def main():
         keys, out, hist = bufs[kb]
         args = (P(keys), P(out), P(vin), P(vout), ctypes.c_uint32(n), P(hist), P(ticket), P(st),
                 P(st2), P(err), 0, sp)
-        if kind == "v4":
+        if kind == "r4":   # r4:32:0:block:items:minw:opt  (4-bit digits, low nibble)
+            rc = L.lab2_v4rb4(block, items, v[5], v[6], P(keys), P(out), ctypes.c_uint32(n),
+                              P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
+        elif kind == "v4":
             rc = L.lab2_v4(kb, pairs, block, items, v[5], v[6], *args)
         elif kind == "v5":   # v5:kb:pairs:block:items:minw:chunk:opt:grid
             rc = L.lab2_v5(kb, pairs, block, items, v[5], v[6], v[7], v[8], *args)
@@ -128,7 +133,7 @@ def main():
             run(v)
             torch.cuda.synchronize()
             k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
-            _, idx = torch.sort(k64 & 255, stable=True)
+            _, idx = torch.sort(k64 & (15 if v[0] == "r4" else 255), stable=True)
             o64 = out.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
             ok = torch.equal(o64, k64[idx])
             okv = (not pairs) or torch.equal(vout.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, idx)
