@@ -197,7 +197,7 @@ struct grs_sorter {
   size_t rec_bytes = 0;
   uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
-  int hist_grid_cap = 1024;        // GRS_HIST_GRID: cap of the upfront histogram grid
+  int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the upfront histogram grid
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
   int u32_variant = 0;             // GRS_U32_PASS: u32-keys pass variant (0 = default; lab A/B)
   bool pass_nt = false;            // GRS_PASS_NT=1: nontemporal tile loads in the big pass (A/B)
@@ -449,7 +449,12 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   {
     // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout)
     // 1024 blocks: 5 % faster than 2048 alone (tools/histlab.py); GRS_HIST_GRID overrides the cap
-    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(s->hist_grid_cap, (n + 4095) / 4096));
+    // grid ~ n / 2^17 between 512 and 2048 blocks (same box, tools/ab_hist.sh: C2 2^24 keys
+    // 512 blocks 0.039 ms vs 1024 0.044; C3 2^28 2048 blocks 0.297 ms vs 1024 0.349), and
+    // > n / 2^18 so every 16-bit bank-private counter stays below 2^16 (HistLayout);
+    // GRS_HIST_GRID overrides the cap
+    const int want = std::min<int>(s->hist_grid_cap, std::max<int>(512, static_cast<int>(n >> 17)));
+    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(want, (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
                        stream, keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words));

@@ -1,14 +1,17 @@
-"""HBM traffic of the pass kernel from rocprofv3 PMC runs of bench.py -> profiles/pmc_traffic.json.
+"""HBM traffic per launch of the pass kernel, from rocprofv3 PMC runs -> a JSON that
+bench.py --traffic-json reads (only when it names the same config and size).
 
-usage: python tools/bench_pmc.py TAG CONFIG N
-  reads gpurun_out/TAG_fetch/**/*counter_collection.csv and gpurun_out/TAG_write/... (one
-  counter per rocprofv3 run, as MI355X_MICROARCH.md's HBM section prescribes) and records the
-  mean bytes per launch of the onesweep pass kernel.
+usage: python tools/bench_pmc.py TAG CONFIG N OUT.json
+  gpurun_out/TAG_fetch, TAG_write          FETCH_SIZE / WRITE_SIZE runs of bench.py (one
+                                           counter per rocprofv3 run, MI355X_MICROARCH.md HBM)
+  gpurun_out/TAG_cfetch, TAG_cwrite        the same counters over the calibration kernel
+                                           (tools/lab2.py --emu 1024:36:0: the pass's exact
+                                           load/store instructions, contiguous, known bytes)
 
-FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
-FETCH_SIZE reports half of the bytes of a wide (16 B/lane) coalesced streaming read, which is
-how the pass reads its keys (global_load_lds_dwordx4), so fetched bytes = 2 x FETCH_SIZE;
-WRITE_SIZE is exact for streaming stores.
+MI355X_MICROARCH.md: FETCH_SIZE reads 1/2 of the bytes of a 16-B/lane streaming read; other
+widths are uncalibrated.  The pass loads 4 B/lane (global_load_dword) and stores 4 B/lane, so
+the correction factors are measured here on the calibration kernel, which moves exactly
+2^27 x 4 B each way: factor = known bytes / counter bytes.
 """
 import csv
 import glob
@@ -20,35 +23,35 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(tag_dir: str, counter: str) -> float:
+def per_launch(tag_dir: str, counter: str, name_part: str) -> float:
     vals = []
     for path in glob.glob(os.path.join(REPO, "gpurun_out", tag_dir, "**", "*counter_collection.csv"),
                           recursive=True):
         for r in csv.DictReader(open(path)):
-            if "onesweep" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if name_part in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     if not vals:
-        raise SystemExit(f"no {counter} rows for an onesweep kernel under gpurun_out/{tag_dir}")
-    return statistics.mean(vals) * 1024.0
+        raise SystemExit(f"no {counter} rows for {name_part} under gpurun_out/{tag_dir}")
+    return statistics.mean(vals) * 1024.0   # KiB -> bytes
 
 
 def main():
-    tag, config, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    fetch = per_launch(f"{tag}_fetch", "FETCH_SIZE")
-    write = per_launch(f"{tag}_write", "WRITE_SIZE")
-    out_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    db = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    db[f"{config}:{n}"] = {
-        "hbm_bytes_per_launch": round(2 * fetch + write),
-        "fetch_size_bytes_raw": round(fetch), "write_size_bytes": round(write),
-        "correction": "fetched = 2 x FETCH_SIZE (gfx950 16-B/lane streaming reads), WRITE_SIZE exact",
-        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py --config {config} ({tag})",
-    }
-    json.dump(db, open(out_path, "w"), indent=1)
-    # the box's profiles/ does not travel back: a copy under gpurun_out/ is merged home
-    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    json.dump(db, open(os.path.join(REPO, "gpurun_out", "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(db[f"{config}:{n}"]))
+    tag, config, n, out_path = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    fetch = per_launch(f"{tag}_fetch", "FETCH_SIZE", "onesweep_v4")
+    write = per_launch(f"{tag}_write", "WRITE_SIZE", "onesweep_v4")
+    known = (1 << 27) * 4
+    cf = known / per_launch(f"{tag}_cfetch", "FETCH_SIZE", "scatter_emu")
+    cw = known / per_launch(f"{tag}_cwrite", "WRITE_SIZE", "scatter_emu")
+    rec = {"config": config, "n": n,
+           "hbm_bytes_per_launch": round(cf * fetch + cw * write),
+           "read_bytes": round(cf * fetch), "write_bytes": round(cw * write),
+           "fetch_size_raw": round(fetch), "write_size_raw": round(write),
+           "read_factor": round(cf, 4), "write_factor": round(cw, 4),
+           "algorithmic_bytes_per_launch": n * 8,
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over bench.py --config {config} "
+                     f"and the calibration kernel ({tag})"}
+    json.dump(rec, open(out_path, "w"), indent=1)
+    print(json.dumps(rec))
 
 
 if __name__ == "__main__":

@@ -48,7 +48,9 @@ __global__ __launch_bounds__(256) void read_u(const uint4* __restrict__ in, uint
 //   MODE 0: T*TILE + i (contiguous), MODE 1: 256 equal digit runs of RUN = TILE/256 keys:
 //   dst = (i / RUN) * (n / 256) + T * RUN + i % RUN (the uniform-key scatter of a pass);
 //   MODE 2: as 1, with consecutive tiles on one XCD (block b -> tile (b%8)*tiles/8 + b/8)
-template <int BLOCK, int ITEMS, int MODE>
+// POL (store policy): 0 default, 1 nontemporal, 2 agent-scope (sc1, write-through),
+// 3 nontemporal for lines inside a run and default for the run's partial head / tail lines
+template <int BLOCK, int ITEMS, int MODE, int POL = 0>
 __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict__ in,
                                                      uint32_t* __restrict__ out, uint32_t n) {
   constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 256;
@@ -66,7 +68,18 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict_
   for (int k = 0; k < ITEMS; ++k) {
     const uint32_t i = k * BLOCK + threadIdx.x;
     const uint32_t dst = MODE == 0 ? T * TILE + i : (i / RUN) * (n / 256) + T * RUN + i % RUN;
-    out[dst] = key[k];
+    if constexpr (POL == 0) {
+      out[dst] = key[k];
+    } else if constexpr (POL == 1) {
+      __builtin_nontemporal_store(key[k], &out[dst]);
+    } else if constexpr (POL == 2) {
+      __hip_atomic_store(&out[dst], key[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint32_t rs = dst - i % RUN, re = rs + RUN;   // run [rs, re)
+      const uint32_t ls = dst & ~31u;                     // 128-B line of dst
+      if (ls >= rs && ls + 32 <= re) __builtin_nontemporal_store(key[k], &out[dst]);
+      else out[dst] = key[k];
+    }
   }
 }
 
@@ -77,13 +90,36 @@ extern "C" {
 // pass memory-pattern emulation: block, items, mode, dynamic LDS bytes (occupancy control)
 int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out, uint32_t n,
              void* stream) {
+  // mode = layout (0 contiguous, 1 runs, 2 runs + XCD-local tiles) + 10 * store policy
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint32_t tiles = n / (block * items);
-#define E(B, I, M)                                                                              if (block == B && items == I && mode == M) {                                                    hipLaunchKernelGGL((scatter_emu<B, I, M>), dim3(tiles), dim3(B), lds, s,                                         (const uint32_t*)in, (uint32_t*)out, n);                                   return hipGetLastError() == hipSuccess ? 0 : -2;                                            }
-  E(512, 72, 0) E(512, 72, 1) E(512, 64, 0) E(512, 64, 1) E(1024, 32, 0) E(1024, 32, 1)
-  E(256, 72, 1) E(512, 66, 1) E(512, 72, 2) E(512, 66, 2) E(512, 64, 2) E(256, 72, 2)
-#undef E
-  return -1;
+  const uint32_t* i = static_cast<const uint32_t*>(in);
+  uint32_t* o = static_cast<uint32_t*>(out);
+  const void* k = nullptr;
+  const int code = block * 100000 + items * 100 + mode;
+  switch (code) {
+    case 51207200: k = (const void*)scatter_emu<512, 72, 0>; break;
+    case 51207201: k = (const void*)scatter_emu<512, 72, 1>; break;
+    case 51207202: k = (const void*)scatter_emu<512, 72, 2>; break;
+    case 51207211: k = (const void*)scatter_emu<512, 72, 1, 1>; break;
+    case 51207221: k = (const void*)scatter_emu<512, 72, 1, 2>; break;
+    case 51207231: k = (const void*)scatter_emu<512, 72, 1, 3>; break;
+    case 51206401: k = (const void*)scatter_emu<512, 64, 1>; break;
+    case 51206411: k = (const void*)scatter_emu<512, 64, 1, 1>; break;
+    case 51206421: k = (const void*)scatter_emu<512, 64, 1, 2>; break;
+    case 51206601: k = (const void*)scatter_emu<512, 66, 1>; break;
+    case 51206611: k = (const void*)scatter_emu<512, 66, 1, 1>; break;
+    case 51206621: k = (const void*)scatter_emu<512, 66, 1, 2>; break;
+    case 51206631: k = (const void*)scatter_emu<512, 66, 1, 3>; break;
+    case 102403600: k = (const void*)scatter_emu<1024, 36, 0>; break;
+    case 102403601: k = (const void*)scatter_emu<1024, 36, 1>; break;
+    case 102403621: k = (const void*)scatter_emu<1024, 36, 1, 2>; break;
+    case 102403631: k = (const void*)scatter_emu<1024, 36, 1, 3>; break;
+    default: return -1;
+  }
+  void* args[] = {&i, &o, &n};
+  if (hipLaunchKernel(k, dim3(tiles), dim3(block), args, lds, s) != hipSuccess) return -2;
+  return 0;
 }
 
 // v4 pass: kb, pairs, block, items, minw, opt
