@@ -197,7 +197,9 @@ struct grs_sorter {
   size_t rec_bytes = 0;
   uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
-  int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the upfront histogram grid
+  int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the round-1 histogram grid
+  int hist_variant = 2;            // GRS_HIST: 1 = grs_upfront_hist, 2 = grs_upfront_hist2
+  int hist2_grid = 0;              // GRS_HIST2_GRID: grs_upfront_hist2 grid (0 = auto)
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
   int u32_variant = 0;             // GRS_U32_PASS: u32-keys pass variant (0 = default; lab A/B)
   bool pass_nt = false;            // GRS_PASS_NT=1: nontemporal tile loads in the big pass (A/B)
@@ -308,6 +310,8 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   s->rank_mode = device_rank_mode(device);
   (void)hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device);
   if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("GRS_HIST")) s->hist_variant = std::atoi(e) == 1 ? 1 : 2;
+  if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
   if (const char* e = std::getenv("GRS_U32_PASS")) s->u32_variant = std::max(0, std::atoi(e));
@@ -446,18 +450,26 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   if ((r = mark()) != GRS_OK) return r;
   // zero histograms + tickets (the error word is sticky: only the checks clear it)
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
-  {
-    // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout)
-    // 1024 blocks: 5 % faster than 2048 alone (tools/histlab.py); GRS_HIST_GRID overrides the cap
-    // grid ~ n / 2^17 between 512 and 2048 blocks (same box, tools/ab_hist.sh: C2 2^24 keys
-    // 512 blocks 0.039 ms vs 1024 0.044; C3 2^28 2048 blocks 0.297 ms vs 1024 0.349), and
-    // > n / 2^18 so every 16-bit bank-private counter stays below 2^16 (HistLayout);
-    // GRS_HIST_GRID overrides the cap
+  if (s->hist_variant == 1) {
+    // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout);
+    // grid ~ n / 2^17 between 512 and 2048 blocks (round-1 layout, kept for A/B)
     const int want = std::min<int>(s->hist_grid_cap, std::max<int>(512, static_cast<int>(n >> 17)));
     const int grid = std::max<int>((n >> 18) + 1, std::min<int>(want, (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
                        stream, keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words));
+    GRS_HIP(hipGetLastError());
+  } else {
+    // grs_upfront_hist2: 2 blocks of 512 per CU; a multiple of the resident slots so the
+    // grid-stride loop ends evenly, and > n >> kHist2GridShift blocks (16-bit counters)
+    const int slots = 2 * s->cus;
+    const int need = static_cast<int>(n >> grs::kHist2GridShift<K>) + 1;
+    int grid = s->hist2_grid > 0 ? s->hist2_grid : (n <= (1u << 25) ? s->cus : slots);
+    if (grid < need) grid = (need + slots - 1) / slots * slots;
+    const bool full = begin_bit == 0 && end_bit == static_cast<int>(8 * sizeof(K));
+    auto kern = full ? grs::grs_upfront_hist2<K, RB, true> : grs::grs_upfront_hist2<K, RB, false>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream, keys, n,
+                       begin_bit, end_bit, passes, hist, st0, static_cast<uint32_t>(words));
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;

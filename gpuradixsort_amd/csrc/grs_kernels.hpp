@@ -282,6 +282,164 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// upfront histogram, issue-lean layout (grs_upfront_hist2)
+// ----------------------------------------------------------------------------------------
+//
+// grs_upfront_hist spends 6 VALU per key digit (shift, mask, two shifts for the 16-bit half
+// chosen by the digit's low bit, and-or, variable shift of the add value) and a scalar branch
+// per digit position; at 2^30 keys that issue, not HBM, sets its 0.91 ms.  Here the 16-bit
+// half is chosen by the POSITION's parity instead: super digits 2p and 2p+1 share the word
+// of (pair p, digit value d), so the add value is a compile-time 1 or 0x10000 and a digit
+// costs v_bfe_u32 + v_lshl_add_u32 (+ the ds_add_u32, whose pair offset is an immediate).
+// Copy c of each counter sits in bank c (COPIES = 32 for u32 keys: every 32-lane LDS group
+// conflict-free; 16 for u64 keys, 2-way at most).  64 KB per 512-thread block, 2 blocks per
+// CU.  A copy counts at most (512 / COPIES) * VEC * ceil(n / VEC / (grid * 512)) keys per
+// counter, which the launch keeps below 2^16 (grid > n >> kHist2GridShift).
+// FULL: the bit range is the whole key (begin_bit 0, every super digit 8 bits wide), so the
+// field offsets are immediates; otherwise they are SGPR operands (one 64-bit shift more for
+// u64 keys).  Super digits past the range are counted into digit 0 of their position and
+// never read.  A used position shares its word with an unused one only as the low half
+// (supers odd); the unused high half's overflow carries out of bit 31, so it cannot corrupt
+// the used count.
+template <typename K>
+struct Hist2Layout {
+  static constexpr int MAXQ = static_cast<int>(sizeof(K));   // super digits per key
+  static constexpr int PAIRS = MAXQ / 2;
+  static constexpr int COPIES = 16384 / (PAIRS * 256);         // u32: 32, u64: 16
+  static constexpr int WORDS = PAIRS * 256 * COPIES;           // 16384 words = 64 KB
+  static constexpr int BLOCK = 512;
+};
+template <typename K>
+constexpr int kHist2GridShift = sizeof(K) == 4 ? 20 : 19;
+
+template <typename K, int RB, bool FULL>
+__global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
+    const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
+    uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words) {
+  static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
+  using HL = Hist2Layout<K>;
+  constexpr int MAXQ = HL::MAXQ;
+  constexpr int COPIES = HL::COPIES;
+  constexpr uint32_t HB = HL::BLOCK;
+  __shared__ __attribute__((aligned(16))) uint32_t s_hist[HL::WORDS];
+
+  const uint32_t t = threadIdx.x;
+  {
+    uint4* z = reinterpret_cast<uint4*>(s_hist);
+    for (uint32_t i = t; i < HL::WORDS / 4; i += HB) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t i = blockIdx.x * HB + t; i < clear_words; i += gridDim.x * HB) clear[i] = 0;
+  __syncthreads();
+
+  const int supers = (end_bit - begin_bit + 7) / 8;
+  int shifts[MAXQ], widths[MAXQ];
+#pragma unroll
+  for (int q = 0; q < MAXQ; ++q) {
+    const int s = begin_bit + q * 8;
+    shifts[q] = s;
+    const int w = end_bit - s;
+    widths[q] = q < supers ? (w < 8 ? w : 8) : 0;
+  }
+  uint32_t* const base = s_hist + (t & (COPIES - 1));
+  auto count = [&](K k) {
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      uint32_t d;
+      if constexpr (FULL) {
+        if constexpr (sizeof(K) == 4) d = __builtin_amdgcn_ubfe(static_cast<uint32_t>(k), 8 * q, 8);
+        else d = __builtin_amdgcn_ubfe(static_cast<uint32_t>(k >> (q < 4 ? 0 : 32)), 8 * (q & 3), 8);
+      } else {
+        if constexpr (sizeof(K) == 4) d = __builtin_amdgcn_ubfe(static_cast<uint32_t>(k), shifts[q], widths[q]);
+        else d = __builtin_amdgcn_ubfe(static_cast<uint32_t>(k >> shifts[q]), 0, widths[q]);
+      }
+      atomicAdd(base + ((q / 2) * 256 + d) * COPIES, (q & 1) ? 0x10000u : 1u);
+    }
+  };
+
+  constexpr int VEC = 16 / sizeof(K);
+  using V = uint4;
+  const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : n / VEC;
+  const V* kv = reinterpret_cast<const V*>(keys);
+  const uint32_t stride = gridDim.x * HB;
+  uint32_t v = blockIdx.x * HB + t;
+  constexpr int U = 4;   // 16-B loads in flight per thread, plus the next group's while counting
+  if (v + (U - 1) * stride < nvec) {
+    V cur[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = kv[v + u * stride];
+    for (;;) {
+      const uint32_t nv = v + U * stride;
+      const bool more = nv + (U - 1) * stride < nvec;
+      V nxt[U];
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = kv[nv + u * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const K* kk = reinterpret_cast<const K*>(&cur[u]);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) count(kk[e]);
+      }
+      v = nv;
+      if (!more) break;
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+  }
+  for (; v < nvec; v += stride) {
+    const V x = kv[v];
+    const K* kk = reinterpret_cast<const K*>(&x);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) count(kk[e]);
+  }
+  for (uint32_t i = nvec * VEC + blockIdx.x * HB + t; i < n; i += stride) count(keys[i]);
+  __syncthreads();
+
+  // reduce the copies: count of super digit value d at position q (rotated start: the 32
+  // lanes of a group read 32 different banks)
+  auto total8 = [&](uint32_t q, uint32_t d) {
+    const uint32_t* row = &s_hist[((q / 2) * 256 + d) * COPIES];
+    const uint32_t sh = (q & 1u) * 16u;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < COPIES; ++k) c += (row[(k + t) & (COPIES - 1)] >> sh) & 0xFFFFu;
+    return c;
+  };
+  if constexpr (RB == 8) {
+    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 256); i += HB) {
+      const uint32_t c = total8(i / 256, i % 256);
+      if (c) atomicAdd(&g_hist[i], c);
+    }
+  } else {
+    // 4-bit passes read their counts off the 8-bit super digits (see grs_upfront_hist)
+    constexpr int R = (MAXQ * 256 + HB - 1) / HB;
+    uint32_t tot[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = t + r * HB;
+      tot[r] = i < static_cast<uint32_t>(supers * 256) ? total8(i / 256, i % 256) : 0u;
+    }
+    __syncthreads();
+    uint32_t* s_red = s_hist;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = t + r * HB;
+      if (i < static_cast<uint32_t>(supers * 256)) s_red[i] = tot[r];
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 16); i += HB) {
+      const uint32_t p = i / 16, d = i % 16, q = p / 2;
+      const uint32_t* r8 = &s_red[q * 256];
+      uint32_t c = 0;
+#pragma unroll
+      for (int h = 0; h < 16; ++h) c += (p & 1u) ? r8[d * 16 + h] : r8[h * 16 + d];
+      if (c) atomicAdd(&g_hist[i], c);
+    }
+  }
+}
+
 // Digit of key k at shard-local index i, for plain and indexed digit functors.
 template <typename DigitF, typename K>
 __device__ __forceinline__ uint32_t digit_call(const DigitF& dig, K k, uint32_t i) {

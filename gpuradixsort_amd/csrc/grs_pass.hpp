@@ -140,20 +140,25 @@ struct Lb3 {
 };
 
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
-          bool IDX = false>
+          bool IDX = false, int ROUNDS = 1>
 struct V4Smem {
   static constexpr int RADIX = 1 << RB;
   static constexpr int WAVES = BLOCK / GRS_WAVE;
   static constexpr int TILE = BLOCK * ITEMS;
+  static constexpr int LTILE = TILE / ROUNDS;   // reordered positions held at once
   // per-wave digit counters -> tile position of (wave, digit); CNT16: 16-bit, two per word
   uint32_t cnt[WAVES * RADIX / (CNT16 ? 2 : 1)];
   uint32_t base[RADIX];         // global destination of tile position 0 of digit d
   uint32_t wsum[2 * WAVES];     // wave totals of the two digit scans
   uint32_t ticket;
-  alignas(16) K keys[TILE];
-  uint32_t vals[PAIRS ? TILE : 1];
-  uint8_t dig8[IDX ? TILE : 1];  // indexed digits: digit of each reordered position
+  uint32_t next;                // persistent kernel: the next tile's ticket
+  alignas(16) K keys[LTILE];
+  uint32_t vals[PAIRS ? LTILE : 1];
+  uint8_t dig8[IDX ? LTILE : 1];  // indexed digits: digit of each reordered position
 };
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
+using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
+                         (OPT & 1024) != 0 ? 2 : 1>;
 
 // OPT bits (lab ablations; the library uses OPT = 0):
 //   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
@@ -163,23 +168,122 @@ struct V4Smem {
 //   256 16-bit wave counters (two digits per LDS word: half the counter LDS)
 //   512 ballot-match ranking instead of lane-ordered LDS atomics (the fallback when the
 //       device probe of the lane order fails, grs_capi.hip)
+//   1024 two-round reorder: the keys stay in registers and LDS holds half the tile at a
+//       time (positions [0, TILE/2) are reordered and stored, then [TILE/2, TILE)), so a
+//       tile can be twice what LDS holds: longer digit runs per tile, fewer partial lines
 
-// One tile, start to finish.  Precondition: sm.cnt is zero and sm.ticket holds `tile`, and
-// every thread passed a barrier since both were written and since the previous tile's last
+// ---------------------------------------------------------------------------------------
+// XCD-chunked tickets (lab option of grs_onesweep_v6)
+// ---------------------------------------------------------------------------------------
+// The digit runs of tiles T and T+1 meet inside one 64-B segment; written from two XCDs the
+// segment leaves two L2s as two partial writes.  Handing out tiles in chunks of CH
+// consecutive tiles per XCD puts both halves in one L2.  Each XCD has a word {chunk id + 1,
+// tiles taken}; a workgroup adds 1 to its XCD's word; the one that finds the chunk full (or
+// no chunk yet) claims the next chunk from a global chunk counter and installs it.  Chunks
+// are claimed in increasing order and an XCD hands out its chunk's tiles in increasing
+// order, so with persistent workgroups the lowest unfinished tile is always being processed
+// or is the next its XCD hands out.
+struct XcdSched {
+  unsigned long long xw[8];  // per XCD: (chunk id + 1) << 32 | tiles taken from it
+  uint32_t gchunk;           // chunks claimed so far
+  uint32_t pad[15];
+};
+static_assert(sizeof(XcdSched) == 128, "XcdSched is 32 words");
+
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x & 7u;
+}
+
+template <int CH>
+__device__ __forceinline__ uint32_t xcd_ticket(XcdSched* sc, uint32_t x, uint32_t* error_word) {
+  unsigned long long v = atomicAdd(&sc->xw[x], 1ull);
+  uint32_t spins = 0;
+  while (true) {
+    const uint32_t c1 = static_cast<uint32_t>(v >> 32);
+    const uint32_t j = static_cast<uint32_t>(v);
+    if (c1 != 0u && j < static_cast<uint32_t>(CH)) return (c1 - 1u) * CH + j;
+    if (c1 == 0u ? j == 0u : j == static_cast<uint32_t>(CH)) {  // exactly one installer per chunk
+      const uint32_t g = atomicAdd(&sc->gchunk, 1u);
+      __hip_atomic_exchange(&sc->xw[x], (static_cast<unsigned long long>(g + 1u) << 32) | 1ull,
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return g * CH;
+    }
+    // another workgroup installs the next chunk: wait for it, then draw again
+    unsigned long long v2;
+    do {
+      if (++spins > GRS_SPIN_LIMIT) {
+        atomicOr(error_word, 2u);
+        return 0xFFFFFFFFu;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v2 = __hip_atomic_load(&sc->xw[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while (static_cast<uint32_t>(v2 >> 32) == c1);
+    v = atomicAdd(&sc->xw[x], 1ull);
+  }
+}
+
+// Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
+// Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
+template <typename K, bool PAIRS, int BLOCK, int ITEMS, int OPT>
+__device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS],
+                                          const K* __restrict__ keys_in,
+                                          const uint32_t* __restrict__ vals_in, uint32_t n,
+                                          uint32_t tile, uint32_t t) {
+  constexpr uint32_t TILE = BLOCK * ITEMS;
+  const uint32_t lane = t & (GRS_WAVE - 1);
+  const uint32_t w = t >> 6;
+  const uint32_t tile_base = tile * TILE;
+  const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS) + lane;
+  auto ld = [&](const auto* p, uint32_t i) {
+    if constexpr ((OPT & 128) != 0) return __builtin_nontemporal_load(p + i);
+    else return p[i];
+  };
+  if (n - tile_base >= TILE) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) key[j] = ld(keys_in, wbase + j * GRS_WAVE);
+    if constexpr (PAIRS) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) val[j] = ld(vals_in, wbase + j * GRS_WAVE);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = wbase + j * GRS_WAVE;
+      key[j] = i < n ? keys_in[i] : static_cast<K>(~static_cast<K>(0));
+      if constexpr (PAIRS) val[j] = i < n ? vals_in[i] : 0u;
+    }
+  }
+}
+
+// One tile, from its loaded (or in-flight) keys to its stores.  Precondition: sm.cnt is zero
+// and every thread passed a barrier since it was written and since the previous tile's last
 // LDS access.  Leaves sm.cnt dirty.
-template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
-__device__ __forceinline__ void onesweep_tile(
-    V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>& sm, uint32_t tile, const K* __restrict__ keys_in,
+// PF (persistent workgroups, grs_onesweep_v6): thread 0 draws the next ticket during the
+// ranking; after the reorder has moved this tile into LDS, the next tile's loads are issued
+// into key/val — their latency hides behind the look-back and the stores.  Returns the next
+// tile (>= tiles: none); without PF returns tiles.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, bool PF = false,
+          int CH = 0, typename DigitF>
+__device__ __forceinline__ uint32_t onesweep_tile(
+    V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>& sm, uint32_t tile, K (&key)[ITEMS],
+    uint32_t (&val)[ITEMS], const K* __restrict__ keys_in,
     K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
-    uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, uint64_t t_begin) {
-  using SM = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>;
+    uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, uint64_t t_begin) {
+  using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr int RADIX = SM::RADIX;
   constexpr int WAVES = SM::WAVES;
   constexpr int TILE = SM::TILE;
+  constexpr int ROUNDS = TILE / SM::LTILE;
+  constexpr int LTILE = SM::LTILE;
+  constexpr int LITEMS = ITEMS / ROUNDS;   // store-loop items per round
+  static_assert(LITEMS * ROUNDS == ITEMS, "ITEMS divisible by the rounds");
   static_assert(!C16 || TILE < 65536, "16-bit tile positions");
+  static_assert(ROUNDS == 1 || TILE < 65536, "two-round reorder keeps 16-bit positions");
   uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
   constexpr bool IDX = DigitF::kIndexed;
   auto cnt_ld = [&](uint32_t i) -> uint32_t { if constexpr (C16) return c16[i]; else return sm.cnt[i]; };
@@ -211,33 +315,6 @@ __device__ __forceinline__ void onesweep_tile(
             static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);                 \
     }                                                                                      \
   } while (0)
-
-  // ---- load, wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l ----
-  K key[ITEMS];
-  uint32_t val[ITEMS];
-  {
-    const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS) + lane;
-    auto ld = [&](const auto* p, uint32_t i) {
-      if constexpr ((OPT & 128) != 0) return __builtin_nontemporal_load(p + i);
-      else return p[i];
-    };
-    if (valid == static_cast<uint32_t>(TILE)) {
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) key[j] = ld(keys_in, wbase + j * GRS_WAVE);
-      if constexpr (PAIRS) {
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) val[j] = ld(vals_in, wbase + j * GRS_WAVE);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const uint32_t i = wbase + j * GRS_WAVE;
-        // padding sorts after every valid key of its digit: all-ones digit, highest index
-        key[j] = i < n ? keys_in[i] : static_cast<K>(~static_cast<K>(0));
-        if constexpr (PAIRS) val[j] = i < n ? vals_in[i] : 0u;
-      }
-    }
-  }
 
   // digit of item j (indexed digits: of (key, shard-local index); padding: the largest)
   auto dig_of = [&](int j) -> uint32_t {
@@ -279,6 +356,14 @@ __device__ __forceinline__ void onesweep_tile(
       rank[j / 2] = r;
   }
   V4_STAMP(0);
+  if constexpr (PF) {
+    if (t == 0) {   // read after B2
+      if constexpr (CH > 0)
+        sm.next = xcd_ticket<CH>(reinterpret_cast<XcdSched*>(ticket), xcc_id(), error_word);
+      else
+        sm.next = atomicAdd(ticket, 1u);
+    }
+  }
   // this tile's (and its group's) words of the next pass's status buffer
   if (t < static_cast<uint32_t>(RADIX)) {
     status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
@@ -324,7 +409,7 @@ __device__ __forceinline__ void onesweep_tile(
     }
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
-    if constexpr ((OPT & (16 | 64)) == 0) lb.issue(status, gacc, ginc, tile, t);
+    if constexpr ((OPT & (16 | 64)) == 0 && !PF) lb.issue(status, gacc, ginc, tile, t);
   }
   lds_barrier();  // B3
   V4_STAMP(3);
@@ -339,16 +424,31 @@ __device__ __forceinline__ void onesweep_tile(
     const uint32_t r = (j & 1) ? rank[j / 2] >> 16 : rank[j / 2] & 0xFFFFu;
     const uint32_t d = dig_of(j);
     const uint32_t pos = cnt_ld(w * RADIX + d) + r;
-    sm.keys[pos] = key[j];
-    if constexpr (IDX) sm.dig8[pos] = static_cast<uint8_t>(d);
-    if constexpr (PAIRS) sm.vals[pos] = val[j];
+    if (ROUNDS == 1 || pos < static_cast<uint32_t>(LTILE)) {
+      sm.keys[pos] = key[j];
+      if constexpr (IDX) sm.dig8[pos] = static_cast<uint8_t>(d);
+      if constexpr (PAIRS) sm.vals[pos] = val[j];
+    }
+    if constexpr (ROUNDS > 1) {   // the rank register now holds the tile position
+      if (j & 1)
+        rank[j / 2] = (rank[j / 2] & 0xFFFFu) | (pos << 16);
+      else
+        rank[j / 2] = (rank[j / 2] & 0xFFFF0000u) | pos;
+    }
+  }
+  if constexpr ((OPT & 16) != 0 || PF) {
+    if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t);
+  }
+  uint32_t next = tiles;
+  if constexpr (PF) {
+    next = __builtin_amdgcn_readfirstlane(sm.next);
+    if (next < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
   if (t < static_cast<uint32_t>(RADIX)) {
     uint32_t prefix;
     if constexpr ((OPT & 64) != 0) {
       prefix = static_cast<uint32_t>((static_cast<uint64_t>(gh) * tile) / tiles);
     } else {
-      if constexpr ((OPT & 16) != 0) lb.issue(status, gacc, ginc, tile, t);
       prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
     }
     sm.base[t] = gstart + prefix - lstart;
@@ -361,26 +461,45 @@ __device__ __forceinline__ void onesweep_tile(
     if constexpr (IDX) return sm.dig8[i];
     else return dig(kk);
   };
-  if (valid == static_cast<uint32_t>(TILE)) {
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const uint32_t i = k * BLOCK + t;
-      const K kk = sm.keys[i];
-      uint32_t dst = sm.base[dig_at(i, kk)] + i;
-      if constexpr ((OPT & 64) != 0) dst = min(dst, n - 1);
-      if constexpr ((OPT & 32) != 0) dst = tile_base + i;
-      keys_out[dst] = kk;
-      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+  for (int rr = 0; rr < ROUNDS; ++rr) {
+    if (rr > 0) {
+      // round rr: every thread has read the previous round's positions; write this round's
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t pos = (j & 1) ? rank[j / 2] >> 16 : rank[j / 2] & 0xFFFFu;
+        const uint32_t lp = pos - static_cast<uint32_t>(rr * LTILE);
+        if (lp < static_cast<uint32_t>(LTILE)) {
+          sm.keys[lp] = key[j];
+          if constexpr (IDX) sm.dig8[lp] = static_cast<uint8_t>(dig_of(j));
+          if constexpr (PAIRS) sm.vals[lp] = val[j];
+        }
+      }
+      lds_barrier();
     }
-  } else {
+    const uint32_t roff = static_cast<uint32_t>(rr * LTILE);
+    if (valid == static_cast<uint32_t>(TILE)) {
 #pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const uint32_t i = k * BLOCK + t;
-      if (i < valid) {
+      for (int k = 0; k < LITEMS; ++k) {
+        const uint32_t i = k * BLOCK + t;
         const K kk = sm.keys[i];
-        const uint32_t dst = sm.base[dig_at(i, kk)] + i;
+        uint32_t dst = sm.base[dig_at(i, kk)] + roff + i;
+        if constexpr ((OPT & 64) != 0) dst = min(dst, n - 1);
+        if constexpr ((OPT & 32) != 0) dst = tile_base + roff + i;
         keys_out[dst] = kk;
         if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < LITEMS; ++k) {
+        const uint32_t i = k * BLOCK + t;
+        if (roff + i < valid) {
+          const K kk = sm.keys[i];
+          const uint32_t dst = sm.base[dig_at(i, kk)] + roff + i;
+          keys_out[dst] = kk;
+          if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+        }
       }
     }
   }
@@ -390,6 +509,7 @@ __device__ __forceinline__ void onesweep_tile(
     if (t == 0) error_word[64 + static_cast<size_t>(tile) * 8 + 7] = static_cast<uint32_t>(t_begin >> 8);
   }
 #undef V4_STAMP
+  return next;
 }
 
 // One tile per workgroup (grid = tiles), tile ids from a ticket counter.  dig_dev: when not
@@ -402,7 +522,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
     uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
-  using SM = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>;
+  using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
   const uint32_t t = threadIdx.x;
@@ -412,94 +532,63 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   __syncthreads();
   // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
-  onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, sm.ticket, keys_in, keys_out, vals_in,
-                                                 vals_out, n, dg, gh, status, status_next,
+  uint32_t tt = t;
+  asm volatile("" : "+v"(tt));
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
+  onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, key, val, keys_in, keys_out, vals_in,
+                                                 vals_out, n, dg, gh, ticket, status, status_next,
                                                  error_word, t_begin);
 }
 
 // ---------------------------------------------------------------------------------------
-// XCD-chunked tile schedule
+// persistent pass with next-tile prefetch
 // ---------------------------------------------------------------------------------------
-// A digit run of tile T and the run of tile T+1 meet inside one 128-B line (and so do runs
-// with a few keys).  Written by two workgroups on two XCDs, such a line leaves two L2s as two
-// partial writes; measured (tools/lab2.py --emu): the uniform-key scatter of 36K-key tiles
-// with 576-B runs runs at 4.56 TB/s against 5.47 for 512-B (line-aligned) runs, and at 4.91
-// when consecutive tiles share an XCD (their partial lines merge in its L2).  So tiles are
-// handed out in chunks of CH consecutive tiles per XCD: each XCD has a word {chunk id + 1,
-// tiles taken}; a workgroup adds 1 to its XCD's word; the one that finds the chunk full (or
-// no chunk yet) claims the next chunk from a global chunk counter and installs it.  Chunks
-// are claimed in increasing order and an XCD hands out its chunk's tiles in increasing
-// order, so the lowest unfinished tile is always being processed or is the next one its
-// XCD hands out: with persistent workgroups (each loops until it draws a tile >= tiles) the
-// grid cannot deadlock, whatever the residency, as long as an XCD that claimed a chunk keeps
-// one workgroup (the claimer itself).
-struct XcdSched {
-  unsigned long long xw[8];  // per XCD: (chunk id + 1) << 32 | tiles taken from it
-  uint32_t gchunk;           // chunks claimed so far
-  uint32_t pad[15];
-};
-static_assert(sizeof(XcdSched) == 128, "XcdSched is 32 words");
-
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x & 7u;
-}
-
-template <int CH>
-__device__ __forceinline__ uint32_t xcd_ticket(XcdSched* sc, uint32_t x, uint32_t* error_word) {
-  unsigned long long v = atomicAdd(&sc->xw[x], 1ull);
-  uint32_t spins = 0;
-  while (true) {
-    const uint32_t c1 = static_cast<uint32_t>(v >> 32);
-    const uint32_t j = static_cast<uint32_t>(v);
-    if (c1 != 0u && j < static_cast<uint32_t>(CH)) return (c1 - 1u) * CH + j;
-    if (c1 == 0u ? j == 0u : j == static_cast<uint32_t>(CH)) {  // exactly one installer per chunk
-      const uint32_t g = atomicAdd(&sc->gchunk, 1u);
-      __hip_atomic_exchange(&sc->xw[x], (static_cast<unsigned long long>(g + 1u) << 32) | 1ull,
-                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return g * CH;
-    }
-    // another workgroup installs the next chunk: wait for it, then draw again
-    unsigned long long v2;
-    do {
-      if (++spins > GRS_SPIN_LIMIT) {
-        atomicOr(error_word, 2u);
-        return 0xFFFFFFFFu;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      v2 = __hip_atomic_load(&sc->xw[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } while (static_cast<uint32_t>(v2 >> 32) == c1);
-    v = atomicAdd(&sc->xw[x], 1ull);
-  }
-}
-
-// Persistent workgroups over the XCD-chunked schedule (grid = resident workgroups).
-template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int CH, int OPT = 0,
-          typename DigitF = RadixDigit<K>>
-__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v5(
+// grs_onesweep_v4 runs one tile per workgroup, and with one 36K-key tile per CU (LDS) the
+// CU's HBM traffic stops between the last store of one tile and the first key of the next:
+// the workgroup exits, the next is dispatched, and its loads pay the full HBM latency before
+// ranking can start.  Here grid = resident workgroups; each loops over tickets and issues
+// tile T+1's loads as soon as tile T sits in LDS, so they fly during T's look-back and
+// stores.  Tickets are drawn in increasing order by running workgroups only, and a workgroup
+// finishes T before it starts T+1, so the lowest unfinished tile never waits on an unstarted
+// one (no residency assumption).  Every workgroup leaves once it draws a ticket >= tiles.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT = 0,
+          int CH = 0, typename DigitF = RadixDigit<K>>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
-    const uint32_t* __restrict__ pass_hist, XcdSched* __restrict__ sched,
+    const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word) {
-  using SM = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed>;
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
+  using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
-  const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
-  const uint32_t x = xcc_id();
+  if (t == 0) {
+    if constexpr (CH > 0)
+      sm.ticket = xcd_ticket<CH>(reinterpret_cast<XcdSched*>(ticket), xcc_id(), error_word);
+    else
+      sm.ticket = atomicAdd(ticket, 1u);
+  }
+  for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
-  while (true) {
+  __syncthreads();
+  const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
+  const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
+  uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);
+  while (tile < tiles) {
     const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
-    if (t == 0) sm.ticket = xcd_ticket<CH>(sched, x, error_word);
+    tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true, CH>(
+        sm, tile, key, val, keys_in, keys_out, vals_in, vals_out, n, dg, gh, ticket, status,
+        status_next, error_word, t_begin);
+    // every LDS read of the finished tile is done before the counters are reset
+    lds_barrier();
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
     lds_barrier();
-    const uint32_t tile = sm.ticket;
-    if (tile >= tiles) break;
-    onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, keys_in, keys_out, vals_in, vals_out,
-                                                   n, dig, gh, status, status_next, error_word,
-                                                   t_begin);
-    lds_barrier();  // every LDS read of this tile is done before the counters are reset
   }
 }
 

@@ -48,6 +48,8 @@ __global__ __launch_bounds__(256) void read_u(const uint4* __restrict__ in, uint
 //   MODE 0: T*TILE + i (contiguous), MODE 1: 256 equal digit runs of RUN = TILE/256 keys:
 //   dst = (i / RUN) * (n / 256) + T * RUN + i % RUN (the uniform-key scatter of a pass);
 //   MODE 2: as 1, with consecutive tiles on one XCD (block b -> tile (b%8)*tiles/8 + b/8)
+//   MODE 3: as 1, every destination shifted by one key (run boundaries 4 B past a 64-B line:
+//   the unaligned boundaries of real digit runs); MODE 5: as 3 with MODE 2's tile mapping
 // POL (store policy): 0 default, 1 nontemporal, 2 agent-scope (sc1, write-through),
 // 3 nontemporal for lines inside a run and default for the run's partial head / tail lines
 template <int BLOCK, int ITEMS, int MODE, int POL = 0>
@@ -56,8 +58,10 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict_
   constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 256;
   extern __shared__ uint32_t pad_lds[];
   const uint32_t tiles8 = (n / TILE) / 8 * 8;
-  const uint32_t T = MODE == 2 ? (blockIdx.x % 8) * (tiles8 / 8) + blockIdx.x / 8 : blockIdx.x;
-  if (MODE == 2 && blockIdx.x >= tiles8) return;
+  constexpr bool XL = MODE == 2 || MODE == 5 || MODE == 6;
+  const uint32_t T = MODE == 6 ? ((blockIdx.x / 8) / 32 * 8 + blockIdx.x % 8) * 32 + (blockIdx.x / 8) % 32
+                   : XL ? (blockIdx.x % 8) * (tiles8 / 8) + blockIdx.x / 8 : blockIdx.x;
+  if (XL && blockIdx.x >= tiles8) return;
   if ((T + 1) * TILE > n) return;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t key[ITEMS];
@@ -67,7 +71,8 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict_
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     const uint32_t i = k * BLOCK + threadIdx.x;
-    const uint32_t dst = MODE == 0 ? T * TILE + i : (i / RUN) * (n / 256) + T * RUN + i % RUN;
+    uint32_t dst = MODE == 0 ? T * TILE + i : (i / RUN) * (n / 256) + T * RUN + i % RUN;
+    if (MODE >= 3) dst = dst + 1 == n ? 0u : dst + 1;
     if constexpr (POL == 0) {
       out[dst] = key[k];
     } else if constexpr (POL == 1) {
@@ -115,6 +120,16 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
     case 102403601: k = (const void*)scatter_emu<1024, 36, 1>; break;
     case 102403621: k = (const void*)scatter_emu<1024, 36, 1, 2>; break;
     case 102403631: k = (const void*)scatter_emu<1024, 36, 1, 3>; break;
+    case 102403603: k = (const void*)scatter_emu<1024, 36, 3>; break;
+    case 102403605: k = (const void*)scatter_emu<1024, 36, 5>; break;
+    case 102403602: k = (const void*)scatter_emu<1024, 36, 2>; break;
+    case 102403606: k = (const void*)scatter_emu<1024, 36, 6>; break;
+    case 102404801: k = (const void*)scatter_emu<1024, 48, 1>; break;
+    case 102404803: k = (const void*)scatter_emu<1024, 48, 3>; break;
+    case 102404805: k = (const void*)scatter_emu<1024, 48, 5>; break;
+    case 102407201: k = (const void*)scatter_emu<1024, 72, 1>; break;
+    case 102407203: k = (const void*)scatter_emu<1024, 72, 3>; break;
+    case 102407205: k = (const void*)scatter_emu<1024, 72, 5>; break;
     default: return -1;
   }
   void* args[] = {&i, &o, &n};
@@ -138,24 +153,11 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
                        grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
                        (const grs::RadixDigit<KT>*)nullptr);                                  \
   } break;
-    V(32, 0, 256, 72, 2, 0) V(32, 0, 256, 64, 2, 0)
-    V(32, 0, 256, 32, 4, 0) V(32, 0, 512, 36, 2, 0) V(32, 0, 512, 72, 1, 0)
-    V(32, 0, 1024, 32, 1, 0) V(32, 0, 256, 72, 2, 16) V(32, 0, 256, 72, 2, 8)
-    V(32, 0, 512, 72, 1, 8) V(32, 0, 256, 40, 3, 0)
-    V(32, 0, 512, 72, 1, 32) V(32, 0, 512, 72, 1, 64) V(32, 0, 512, 72, 1, 96)
-    V(32, 0, 512, 72, 1, 128) V(32, 0, 1024, 32, 1, 32) V(32, 0, 1024, 32, 1, 64)
-    V(32, 0, 1024, 32, 1, 96) V(32, 0, 1024, 32, 1, 8) V(32, 0, 1024, 32, 1, 16)
-    V(32, 0, 512, 72, 1, 16) V(32, 0, 512, 72, 1, 144) V(32, 0, 1024, 32, 1, 144)
-    V(32, 0, 256, 72, 2, 144) V(32, 0, 512, 72, 1, 24)
-    V(32, 1, 256, 36, 2, 0) V(32, 1, 256, 32, 2, 0) V(64, 0, 256, 36, 2, 0)
-    V(64, 1, 256, 24, 2, 0)
-    V(32, 0, 1024, 36, 1, 400) V(32, 0, 1024, 32, 1, 400) V(32, 0, 1024, 34, 1, 144)
-    V(32, 0, 1024, 32, 1, 128) V(32, 1, 1024, 16, 1, 144) V(64, 0, 1024, 16, 1, 144)
-    V(64, 1, 1024, 10, 1, 144) V(32, 1, 1024, 18, 1, 400) V(64, 0, 1024, 18, 1, 400)
-    V(32, 0, 1024, 36, 1, 272)
-    V(64, 1, 1024, 10, 1, 528) V(64, 1, 1024, 10, 1, 512) V(64, 1, 1024, 10, 1, 16)
-    V(64, 0, 1024, 16, 1, 528) V(32, 1, 1024, 16, 1, 528) V(32, 0, 1024, 32, 1, 528)
-    V(64, 1, 1024, 11, 1, 272)
+    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 32, 1, 528)
+    V(32, 0, 1024, 48, 1, 1296) V(32, 0, 1024, 56, 1, 1296) V(32, 0, 1024, 62, 1, 1296)
+    V(32, 0, 768, 64, 1, 1296) V(32, 0, 768, 80, 1, 1296) V(32, 0, 512, 96, 1, 1296)
+    V(32, 0, 512, 120, 1, 1296) V(32, 0, 1024, 48, 1, 1040) V(32, 0, 1024, 48, 1, 1280)
+    V(64, 1, 1024, 11, 1, 272) V(32, 1, 1024, 17, 1, 272) V(64, 0, 1024, 17, 1, 272)
 #undef V
     default:
       return -1;
@@ -163,29 +165,49 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// v5 (persistent, XCD-chunked): kb, pairs, block, items, minw, chunk, opt, grid
-int lab2_v5(int kb, int pairs, int block, int items, int minw, int ch, int opt, int grid,
-            const void* in, void* out, const uint32_t* vin, uint32_t* vout, uint32_t n,
-            const uint32_t* hist, void* sched, uint32_t* st, uint32_t* st2, uint32_t* err,
-            int shift, void* stream) {
+// v6 (persistent, next-tile prefetch): kb, pairs, block, items, minw, opt, grid
+int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid, int ch, const void* in,
+            void* out, const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
+            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code =
-      ((((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 100 + ch) * 1000 + opt;
+  const long code = ((((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000 + opt) * 100 + ch;
   switch (code) {
-#define V(KB, P, B, I, M, C, O)                                                                  \
-  case ((((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 100 + C) * 1000 + O: {        \
-    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                 \
-    hipLaunchKernelGGL((grs::grs_onesweep_v5<KT, P != 0, 8, B, I, M, C, O>), dim3(grid), dim3(B), \
-                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                              \
-                       grs::RadixDigit<KT>{shift, 255u}, hist, (grs::XcdSched*)sched, st, st2,   \
-                       err);                                                                     \
+#define V(KB, P, B, I, M, O, C)                                                                 \
+  case ((((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000 + O) * 100 + C: {       \
+    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                           \
+    const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
+    hipLaunchKernelGGL((grs::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O, C>), dim3(g), dim3(B), 0, \
+                       s, (const KT*)in, (KT*)out, vin, vout, n, grs::RadixDigit<KT>{shift, 255u}, \
+                       hist, ticket, st, st2, err, (const grs::RadixDigit<KT>*)nullptr);        \
   } break;
-    V(32, 0, 512, 72, 1, 4, 0) V(32, 0, 512, 72, 1, 8, 0) V(32, 0, 512, 72, 1, 16, 0)
-    V(32, 0, 512, 72, 1, 8, 16) V(32, 0, 512, 72, 1, 8, 128) V(32, 0, 512, 72, 1, 8, 144)
-    V(32, 0, 512, 72, 1, 16, 144) V(32, 0, 512, 72, 1, 32, 144) V(32, 0, 1024, 32, 1, 8, 144)
-    V(32, 0, 256, 72, 2, 8, 144) V(32, 0, 256, 72, 2, 16, 144) V(32, 0, 512, 72, 1, 8, 152)
-    V(32, 1, 512, 36, 1, 8, 144) V(64, 0, 512, 36, 1, 8, 144)
-    V(32, 0, 512, 72, 1, 4, 144) V(32, 0, 512, 72, 1, 2, 144)
+    V(32, 0, 1024, 36, 1, 256, 0) V(32, 0, 1024, 36, 1, 256, 8) V(32, 0, 1024, 36, 1, 256, 16)
+    V(32, 0, 1024, 36, 1, 256, 32) V(32, 0, 1024, 36, 1, 264, 32)
+    V(64, 1, 1024, 11, 1, 256, 0) V(64, 1, 1024, 11, 1, 256, 32)
+#undef V
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// v6 pass at 4-bit digits: block, items, minw, opt, grid
+int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in, void* out,
+               uint32_t n, const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2,
+               uint32_t* err, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long code = ((block * 1000L + items) * 10 + minw) * 1000 + opt;
+  switch (code) {
+#define V(B, I, M, O)                                                                          \
+  case ((B * 1000L + I) * 10 + M) * 1000 + O: {                                                \
+    const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
+    const uint32_t g = std::min<uint32_t>(tiles, grid);                                        \
+    hipLaunchKernelGGL((grs::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
+                       dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
+                       grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
+                       (const grs::RadixDigit<uint32_t>*)nullptr);                             \
+  } break;
+    V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
 #undef V
     default:
       return -1;
@@ -208,10 +230,7 @@ int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* ou
                        grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
                        (const grs::RadixDigit<uint32_t>*)nullptr);                             \
   } break;
-    V(256, 16, 4, 0) V(256, 16, 4, 512) V(256, 16, 4, 16) V(512, 16, 2, 0) V(512, 16, 2, 512)
-    V(1024, 16, 1, 0) V(1024, 16, 1, 512) V(1024, 8, 1, 0) V(1024, 8, 1, 512) V(256, 32, 4, 0)
-    V(256, 32, 4, 512) V(512, 32, 2, 0) V(512, 32, 2, 512) V(1024, 32, 1, 0) V(1024, 32, 1, 512)
-    V(256, 8, 8, 0) V(256, 8, 8, 512) V(128, 16, 8, 0) V(128, 16, 8, 512) V(512, 8, 4, 512)
+    V(1024, 32, 1, 0) V(1024, 32, 1, 16) V(512, 32, 2, 0) V(1024, 16, 1, 0)
 #undef V
     default:
       return -1;

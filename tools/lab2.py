@@ -50,7 +50,7 @@ def main():
         hist4[kb] = torch.bincount(k64 & 15, minlength=16).to(torch.int32).view(torch.uint32).contiguous()
     vin = torch.arange(n, dtype=torch.int64, device=dev).to(torch.int32).view(torch.uint32)
     vout = torch.empty_like(vin)
-    ticket = torch.zeros(64, dtype=torch.uint32, device=dev)   # also the v5 XcdSched (32 words)
+    ticket = torch.zeros(64, dtype=torch.uint32, device=dev)   
     max_tiles = n // 4096 + 64
     err = torch.zeros(64 + 8 * max_tiles + 64, dtype=torch.uint32, device=dev)
     st = torch.zeros(3 * max_tiles * 256, dtype=torch.uint32, device=dev)
@@ -65,10 +65,13 @@ def main():
         if kind == "r4":   # r4:32:0:block:items:minw:opt  (4-bit digits, low nibble)
             rc = L.lab2_v4rb4(block, items, v[5], v[6], P(keys), P(out), ctypes.c_uint32(n),
                               P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
+        elif kind == "r6":   # r6:32:0:block:items:minw:opt:grid  (4-bit digits, persistent)
+            rc = L.lab2_v6rb4(block, items, v[5], v[6], v[7], P(keys), P(out), ctypes.c_uint32(n),
+                              P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
         elif kind == "v4":
             rc = L.lab2_v4(kb, pairs, block, items, v[5], v[6], *args)
-        elif kind == "v5":   # v5:kb:pairs:block:items:minw:chunk:opt:grid
-            rc = L.lab2_v5(kb, pairs, block, items, v[5], v[6], v[7], v[8], *args)
+        elif kind == "v6":   # v6:kb:pairs:block:items:minw:opt:grid:chunk (ticket buffer = XcdSched)
+            rc = L.lab2_v6(kb, pairs, block, items, v[5], v[6], v[7], v[8], *args)
         else:
             rc = L.lab2_ar(kb, pairs, block, items, v[5], *args)
         assert rc == 0, (v, rc)
@@ -133,7 +136,7 @@ def main():
             run(v)
             torch.cuda.synchronize()
             k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
-            _, idx = torch.sort(k64 & (15 if v[0] == "r4" else 255), stable=True)
+            _, idx = torch.sort(k64 & (15 if v[0] in ("r4", "r6") else 255), stable=True)
             o64 = out.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
             ok = torch.equal(o64, k64[idx])
             okv = (not pairs) or torch.equal(vout.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, idx)
@@ -146,7 +149,7 @@ def main():
         print(f"{':'.join(str(x) for x in v):28s} median {med:8.4f} ms  min {mn:8.4f}  "
               f"{alg / med / 1e6:8.1f} GB/s", flush=True)
     for v in variants:
-        stamped = (v[0] == "v4" and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v5" and v[7] & 8)
+        stamped = (v[0] == "v4" and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v6" and v[6] & 8)
         if not stamped:
             continue
         err.zero_()
@@ -156,7 +159,7 @@ def main():
         torch.cuda.synchronize()
         tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
-        if v[0] in ("v4", "v5"):
+        if v[0] in ("v4", "v6"):
             m = a_[:, :6].mean(0)
             d = np.diff(np.concatenate([[0.0], m]))
             names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
