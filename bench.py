@@ -13,7 +13,7 @@ STRONG scaling: at N = 1 one MI355X sorts all 2^30 keys in one call; at N > 1 ra
 xGMI, local sort; gpuradixsort_amd/sharded.py).  `value` = 2^30 keys x steps / wall time.
 
 Rank 0 prints ONE JSON line with the driver contract plus:
-  roofline      dominant kernel (grs_onesweep_v4, the pass): algorithmic bytes per launch
+  roofline      dominant kernel (the pass: grs_onesweep_v4, or v6 on small grids): algorithmic bytes per launch
                 (n_local x 2 x (key + value bytes)) / its mean duration from
                 hipEvents recorded on the sort's stream during the timed steps; `traffic` is
                 the PMC-measured HBM bytes per launch when --traffic-json names the output of

@@ -90,7 +90,6 @@ struct PartTile {
 constexpr uint32_t kBigOpt = 256 | 16;
 constexpr uint32_t kBig4Opt = 0;
 constexpr uint32_t kSmallOpt = 16;
-constexpr uint32_t kNtOpt = 256 | 16 | 128;            // GRS_PASS_NT=1 (A/B)
 constexpr uint32_t kMatchOpt = 512 | 16;               // ballot-match ranking (fallback)
 
 // Status words of one look-back buffer for `tiles` tiles of radix `radix`.
@@ -201,8 +200,7 @@ struct grs_sorter {
   int hist_variant = 2;            // GRS_HIST: 1 = grs_upfront_hist, 2 = grs_upfront_hist2
   int hist2_grid = 0;              // GRS_HIST2_GRID: grs_upfront_hist2 grid (0 = auto)
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
-  int u32_variant = 0;             // GRS_U32_PASS: u32-keys pass variant (0 = default; lab A/B)
-  bool pass_nt = false;            // GRS_PASS_NT=1: nontemporal tile loads in the big pass (A/B)
+  int pass_mode = 0;               // GRS_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
 };
 
 extern "C" {
@@ -261,6 +259,16 @@ bool use_big_tiles(const grs_sorter* s, size_t n, size_t big_tile) {
   return (n + big_tile - 1) / big_tile >= static_cast<size_t>(std::max(1, s->cus));
 }
 
+// Big-tile pass kernel: the persistent one (grs_onesweep_v6: the next tile's loads fly behind
+// the current tile's look-back and stores) where a CU sees only a few tiles, so the exposed
+// load of each tile dominates; one tile per workgroup (grs_onesweep_v4) otherwise.  Same box,
+// tools/ab_pass.sh, Gkeys/s v6 vs v4: C2 49.8 vs 45.3; C4 119.3 vs 124.2, C3 56.5 vs 61.1,
+// C5 32.5 vs 34.3.
+bool use_persistent(const grs_sorter* s, size_t tiles, int rb) {
+  if (s->pass_mode != 0) return s->pass_mode == 6;
+  return rb == 4 || tiles <= 4u * static_cast<size_t>(std::max(1, s->cus));
+}
+
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
 template <typename K, bool PAIRS>
 size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
@@ -314,8 +322,8 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
-  if (const char* e = std::getenv("GRS_U32_PASS")) s->u32_variant = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("GRS_PASS_NT")) s->pass_nt = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GRS_PASS"))
+    s->pass_mode = std::strcmp(e, "v6") == 0 ? 6 : std::strcmp(e, "v4") == 0 ? 4 : 0;
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(capacity, 1);
   const size_t radix = std::max<size_t>(size_t(1) << radix_bits, 16);
@@ -389,8 +397,10 @@ grs_status grs_set_profiling(grs_sorter* s, int ring) {
 
 namespace {
 
-// One pass launch: grid = tiles, one tile per workgroup (grs_pass.hpp).
-template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, typename DigitF>
+// One pass launch (grs_pass.hpp): grs_onesweep_v4, grid = tiles, one tile per workgroup; or
+// PERSIST: grs_onesweep_v6, grid = resident workgroups looping over tickets with prefetch.
+template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERSIST = false,
+          typename DigitF>
 grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
                        uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
                        uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream,
@@ -400,19 +410,21 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
     return set_err(GRS_ECAPACITY, "status buffer too small");
   if (expect_tile != 0 && expect_tile != static_cast<uint32_t>(Tile::TILE))
     return set_err(GRS_EINVAL, "internal: pass tile differs from the zeroed status layout");
-  hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW, OPT,
-                                           DigitF>),
-                     dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                     ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+  if constexpr (PERSIST) {
+    const uint32_t grid = std::min<uint32_t>(tiles, static_cast<uint32_t>(s->cus * Tile::MINW));
+    hipLaunchKernelGGL((grs::grs_onesweep_v6<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
+                                             OPT, DigitF>),
+                       dim3(grid), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+  } else {
+    hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
+                                             OPT, DigitF>),
+                       dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+  }
   GRS_HIP(hipGetLastError());
   return GRS_OK;
 }
-
-// Lab variants of the u32-keys pass, selected by GRS_U32_PASS=1..4 at grs_create (A/B only).
-template <int B, int I, int O>
-struct U32Var {
-  static constexpr int BLOCK = B, ITEMS = I, MINW = 1, TILE = B * I, OPT = O;
-};
 
 template <typename K, bool PAIRS, int RB>
 grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begin_bit,
@@ -427,12 +439,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   // group words) that the histogram kernel zeroes for pass 0 and every pass for the next one
   uint32_t tile = big ? Big::TILE : Small::TILE;
   if (s->rank_mode != 0 && big) tile = MatchTile<K, PAIRS>::TILE;
-  if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) {
-    if (s->rank_mode == 0 && big && s->u32_variant != 0)
-      tile = s->u32_variant == 1 ? 1024 * 32 : s->u32_variant == 2 ? 512 * 72
-             : s->u32_variant == 3 ? 1024 * 36 : 1024 * 32;
-  }
   const uint32_t tiles = (n + tile - 1) / tile;
+  const bool persist = use_persistent(s, tiles, RB);
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
@@ -479,10 +487,6 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   uint32_t* vsrc = vals;
   uint32_t* vdst = s->alt_vals;
   using Dig = grs::RadixDigit<K>;
-  auto u32_lab = [&](bool big_tiles) {
-    if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) return big_tiles && s->u32_variant != 0;
-    else return false;
-  };
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
     const int bits = std::min(RB, end_bit - shift);
@@ -493,21 +497,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     if (s->rank_mode != 0) {
       r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-    } else if (u32_lab(big)) {
-      using V1 = U32Var<1024, 32, 16>;    // 32-bit wave counters, 32K-key tiles
-      using V2 = U32Var<512, 72, 16>;     // 8 waves, 36K-key tiles
-      using V3 = U32Var<1024, 36, 256>;   // look-back issued before the reorder
-      using V4 = U32Var<1024, 32, 0>;     // round-2 first default: 32-bit counters, early look-back
-#define GRS_U32V(V) r = launch_pass<K, PAIRS, RB, V, V::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
-      if constexpr (!PAIRS && sizeof(K) == 4 && RB == 8) switch (s->u32_variant) {
-        case 1: GRS_U32V(V1); break;
-        case 2: GRS_U32V(V2); break;
-        case 3: GRS_U32V(V3); break;
-        default: GRS_U32V(V4); break;
-      }
-#undef GRS_U32V
-    } else if (s->pass_nt && big) {
-      r = launch_pass<K, PAIRS, RB, Big, kNtOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+    } else if (persist && big) {
+      r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else {
       r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
@@ -1383,8 +1374,18 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
 }
 
 const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
-  (void)n;
-  return s ? "grs_onesweep_v4" : "";
+  if (!s || n == 0) return "";
+  auto pick = [&](size_t big_tile) -> const char* {
+    if (s->rank_mode != 0 || !use_big_tiles(s, n, big_tile)) return "grs_onesweep_v4";
+    return use_persistent(s, (n + big_tile - 1) / big_tile, s->radix_bits) ? "grs_onesweep_v6"
+                                                                              : "grs_onesweep_v4";
+  };
+  const bool u32 = s->key_type == GRS_KEY_U32;
+  if (s->radix_bits == 4)
+    return u32 ? (s->pairs ? pick(BigTile4<uint32_t, true>::TILE) : pick(BigTile4<uint32_t, false>::TILE))
+               : (s->pairs ? pick(BigTile4<uint64_t, true>::TILE) : pick(BigTile4<uint64_t, false>::TILE));
+  return u32 ? (s->pairs ? pick(BigTile<uint32_t, true>::TILE) : pick(BigTile<uint32_t, false>::TILE))
+             : (s->pairs ? pick(BigTile<uint64_t, true>::TILE) : pick(BigTile<uint64_t, false>::TILE));
 }
 
 }  // extern "C"

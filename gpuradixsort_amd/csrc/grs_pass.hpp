@@ -172,58 +172,6 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //       time (positions [0, TILE/2) are reordered and stored, then [TILE/2, TILE)), so a
 //       tile can be twice what LDS holds: longer digit runs per tile, fewer partial lines
 
-// ---------------------------------------------------------------------------------------
-// XCD-chunked tickets (lab option of grs_onesweep_v6)
-// ---------------------------------------------------------------------------------------
-// The digit runs of tiles T and T+1 meet inside one 64-B segment; written from two XCDs the
-// segment leaves two L2s as two partial writes.  Handing out tiles in chunks of CH
-// consecutive tiles per XCD puts both halves in one L2.  Each XCD has a word {chunk id + 1,
-// tiles taken}; a workgroup adds 1 to its XCD's word; the one that finds the chunk full (or
-// no chunk yet) claims the next chunk from a global chunk counter and installs it.  Chunks
-// are claimed in increasing order and an XCD hands out its chunk's tiles in increasing
-// order, so with persistent workgroups the lowest unfinished tile is always being processed
-// or is the next its XCD hands out.
-struct XcdSched {
-  unsigned long long xw[8];  // per XCD: (chunk id + 1) << 32 | tiles taken from it
-  uint32_t gchunk;           // chunks claimed so far
-  uint32_t pad[15];
-};
-static_assert(sizeof(XcdSched) == 128, "XcdSched is 32 words");
-
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x & 7u;
-}
-
-template <int CH>
-__device__ __forceinline__ uint32_t xcd_ticket(XcdSched* sc, uint32_t x, uint32_t* error_word) {
-  unsigned long long v = atomicAdd(&sc->xw[x], 1ull);
-  uint32_t spins = 0;
-  while (true) {
-    const uint32_t c1 = static_cast<uint32_t>(v >> 32);
-    const uint32_t j = static_cast<uint32_t>(v);
-    if (c1 != 0u && j < static_cast<uint32_t>(CH)) return (c1 - 1u) * CH + j;
-    if (c1 == 0u ? j == 0u : j == static_cast<uint32_t>(CH)) {  // exactly one installer per chunk
-      const uint32_t g = atomicAdd(&sc->gchunk, 1u);
-      __hip_atomic_exchange(&sc->xw[x], (static_cast<unsigned long long>(g + 1u) << 32) | 1ull,
-                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return g * CH;
-    }
-    // another workgroup installs the next chunk: wait for it, then draw again
-    unsigned long long v2;
-    do {
-      if (++spins > GRS_SPIN_LIMIT) {
-        atomicOr(error_word, 2u);
-        return 0xFFFFFFFFu;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      v2 = __hip_atomic_load(&sc->xw[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } while (static_cast<uint32_t>(v2 >> 32) == c1);
-    v = atomicAdd(&sc->xw[x], 1ull);
-  }
-}
-
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
 template <typename K, bool PAIRS, int BLOCK, int ITEMS, int OPT>
@@ -265,7 +213,7 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
 // into key/val — their latency hides behind the look-back and the stores.  Returns the next
 // tile (>= tiles: none); without PF returns tiles.
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, bool PF = false,
-          int CH = 0, typename DigitF>
+          typename DigitF>
 __device__ __forceinline__ uint32_t onesweep_tile(
     V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>& sm, uint32_t tile, K (&key)[ITEMS],
     uint32_t (&val)[ITEMS], const K* __restrict__ keys_in,
@@ -357,12 +305,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   }
   V4_STAMP(0);
   if constexpr (PF) {
-    if (t == 0) {   // read after B2
-      if constexpr (CH > 0)
-        sm.next = xcd_ticket<CH>(reinterpret_cast<XcdSched*>(ticket), xcc_id(), error_word);
-      else
-        sm.next = atomicAdd(ticket, 1u);
-    }
+    if (t == 0) sm.next = atomicAdd(ticket, 1u);   // read after B2
   }
   // this tile's (and its group's) words of the next pass's status buffer
   if (t < static_cast<uint32_t>(RADIX)) {
@@ -555,7 +498,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
 // finishes T before it starts T+1, so the lowest unfinished tile never waits on an unstarted
 // one (no residency assumption).  Every workgroup leaves once it draws a ticket >= tiles.
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT = 0,
-          int CH = 0, typename DigitF = RadixDigit<K>>
+          typename DigitF = RadixDigit<K>>
 __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
@@ -565,12 +508,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
-  if (t == 0) {
-    if constexpr (CH > 0)
-      sm.ticket = xcd_ticket<CH>(reinterpret_cast<XcdSched*>(ticket), xcc_id(), error_word);
-    else
-      sm.ticket = atomicAdd(ticket, 1u);
-  }
+  if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   __syncthreads();
@@ -582,7 +520,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);
   while (tile < tiles) {
     const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
-    tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true, CH>(
+    tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true>(
         sm, tile, key, val, keys_in, keys_out, vals_in, vals_out, n, dg, gh, ticket, status,
         status_next, error_word, t_begin);
     // every LDS read of the finished tile is done before the counters are reset

@@ -110,8 +110,12 @@ def test_rank_mode_is_atomic_on_gfx950(gpu):
     """The LDS lane-order probe passes on MI355X, so the atomic-rank pass runs."""
     s = sorter(32, False, 8, 1 << 20)
     assert s.rank_mode == "atomic"
-    assert s.pass_kernel_for(1 << 20) == "grs_onesweep_v4"
+    assert s.pass_kernel_for(1 << 20) == "grs_onesweep_v4"   # small tiles
     assert sorter(32, True, 8, 1 << 20).pass_kernel == "grs_onesweep_v4"
+    # big tiles: persistent pass where a CU sees at most 4 tiles or digits are 4-bit
+    assert s.pass_kernel_for(1 << 24) == "grs_onesweep_v6"
+    assert s.pass_kernel_for(1 << 27) == "grs_onesweep_v4"
+    assert sorter(32, False, 4, 1 << 20).pass_kernel_for(1 << 24) == "grs_onesweep_v6"
 
 
 @pytest.mark.parametrize("tile", ["big", "small"])
@@ -174,24 +178,31 @@ def test_ballot_match_fallback(gpu, monkeypatch):
             s.close()
 
 
-@pytest.mark.parametrize("choice", ["1", "2", "3", "4"])
-def test_u32_pass_alternatives(gpu, monkeypatch, choice):
-    """GRS_U32_PASS pins one of the lab variants of the big u32-keys pass (32-bit wave
-    counters with 32K-key tiles / 512 x 72 tiles / look-back before the reorder / the round's
-    first default): same bit-exact results across tile edges."""
+@pytest.mark.parametrize("kb,pairs,rb", [(32, False, 8), (32, True, 8), (64, False, 8),
+                                          (64, True, 8), (32, False, 4), (64, True, 4)])
+def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb):
+    """GRS_PASS=v6: the persistent big-tile pass (grs_onesweep_v6: resident workgroups loop
+    over tickets, the next tile's loads issued behind the reorder) gives the same bit-exact
+    results across tile edges, for every key/payload type and both digit widths."""
     import gpuradixsort_amd as grs
 
-    monkeypatch.setenv("GRS_U32_PASS", choice)
+    monkeypatch.setenv("GRS_PASS", "v6")
     monkeypatch.setenv("GRS_TILE", "big")
-    rng = np.random.default_rng(11)
-    for n in (1, 16383, 32769, 36865, 8 * 36864 + 1, 1_000_003):
-        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-        keys[::7] = 0xFFFFFFFF
-        s = grs.RadixSorter(n, key_bits=32, radix_bits=8)
+    rng = np.random.default_rng(11 + kb + pairs + rb)
+    dt = np.uint32 if kb == 32 else np.uint64
+    for n in (1, 16383, 32769, 36865, 8 * 36864 + 1, 1_000_003, 3 * 1024 * 1024 + 7):
+        keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        keys[::7] = np.iinfo(dt).max
+        keys[1::13] = 3
+        perm = oracle.stable_argsort(keys)
+        s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb)
         k = to_dev(keys, gpu)
-        s.sort(k)
+        v = to_dev(np.arange(n, dtype=np.uint32), gpu) if pairs else None
+        s.sort(k, v)
         s.check_error()
-        assert np.array_equal(k.cpu().numpy(), np.sort(keys)), (choice, n)
+        assert np.array_equal(k.cpu().numpy(), keys[perm]), n
+        if pairs:
+            assert np.array_equal(v.cpu().numpy(), perm), n
         s.close()
 
 

@@ -1,7 +1,7 @@
 """HBM traffic per launch of the pass kernel, from rocprofv3 PMC runs -> a JSON that
 bench.py --traffic-json reads (only when it names the same config and size).
 
-usage: python tools/bench_pmc.py TAG CONFIG N OUT.json
+usage: python tools/bench_pmc.py TAG CONFIG N OUT.json [KERNEL]
   gpurun_out/TAG_fetch, TAG_write          FETCH_SIZE / WRITE_SIZE runs of bench.py (one
                                            counter per rocprofv3 run, MI355X_MICROARCH.md HBM)
   gpurun_out/TAG_cfetch, TAG_cwrite        the same counters over the calibration kernel
@@ -37,8 +37,9 @@ def per_launch(tag_dir: str, counter: str, name_part: str) -> float:
 
 def main():
     tag, config, n, out_path = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    fetch = per_launch(f"{tag}_fetch", "FETCH_SIZE", "onesweep_v4")
-    write = per_launch(f"{tag}_write", "WRITE_SIZE", "onesweep_v4")
+    kern = sys.argv[5] if len(sys.argv) > 5 else "grs_onesweep_v4"
+    fetch = per_launch(f"{tag}_fetch", "FETCH_SIZE", kern)
+    write = per_launch(f"{tag}_write", "WRITE_SIZE", kern)
     known = (1 << 27) * 4
     cf = known / per_launch(f"{tag}_cfetch", "FETCH_SIZE", "scatter_emu")
     cw = known / per_launch(f"{tag}_cwrite", "WRITE_SIZE", "scatter_emu")

@@ -153,7 +153,9 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
                        grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
                        (const grs::RadixDigit<KT>*)nullptr);                                  \
   } break;
-    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 32, 1, 528)
+    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 32, 1, 528) V(32, 0, 1024, 36, 1, 304)
+    V(32, 0, 1024, 36, 1, 336) V(32, 0, 1024, 36, 1, 368) V(32, 0, 1024, 40, 1, 1296)
+    V(32, 0, 1024, 44, 1, 1296) V(32, 0, 1024, 40, 1, 1040)
     V(32, 0, 1024, 48, 1, 1296) V(32, 0, 1024, 56, 1, 1296) V(32, 0, 1024, 62, 1, 1296)
     V(32, 0, 768, 64, 1, 1296) V(32, 0, 768, 80, 1, 1296) V(32, 0, 512, 96, 1, 1296)
     V(32, 0, 512, 120, 1, 1296) V(32, 0, 1024, 48, 1, 1040) V(32, 0, 1024, 48, 1, 1280)
@@ -166,24 +168,23 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
 }
 
 // v6 (persistent, next-tile prefetch): kb, pairs, block, items, minw, opt, grid
-int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid, int ch, const void* in,
+int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid, const void* in,
             void* out, const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
             uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = ((((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000 + opt) * 100 + ch;
+  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000 + opt;
   switch (code) {
-#define V(KB, P, B, I, M, O, C)                                                                 \
-  case ((((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000 + O) * 100 + C: {       \
+#define V(KB, P, B, I, M, O)                                                                    \
+  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000 + O: {                   \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                           \
     const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
-    hipLaunchKernelGGL((grs::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O, C>), dim3(g), dim3(B), 0, \
+    hipLaunchKernelGGL((grs::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O>), dim3(g), dim3(B), 0,   \
                        s, (const KT*)in, (KT*)out, vin, vout, n, grs::RadixDigit<KT>{shift, 255u}, \
                        hist, ticket, st, st2, err, (const grs::RadixDigit<KT>*)nullptr);        \
   } break;
-    V(32, 0, 1024, 36, 1, 256, 0) V(32, 0, 1024, 36, 1, 256, 8) V(32, 0, 1024, 36, 1, 256, 16)
-    V(32, 0, 1024, 36, 1, 256, 32) V(32, 0, 1024, 36, 1, 264, 32)
-    V(64, 1, 1024, 11, 1, 256, 0) V(64, 1, 1024, 11, 1, 256, 32)
+    V(32, 0, 1024, 36, 1, 256) V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 288)
+    V(64, 1, 1024, 11, 1, 256) V(32, 1, 1024, 17, 1, 256) V(64, 0, 1024, 17, 1, 256)
 #undef V
     default:
       return -1;
@@ -230,7 +231,8 @@ int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* ou
                        grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
                        (const grs::RadixDigit<uint32_t>*)nullptr);                             \
   } break;
-    V(1024, 32, 1, 0) V(1024, 32, 1, 16) V(512, 32, 2, 0) V(1024, 16, 1, 0)
+    V(1024, 32, 1, 0) V(1024, 32, 1, 16) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(1024, 32, 1, 8)
+    V(1024, 32, 1, 24) V(1024, 32, 1, 64) V(1024, 32, 1, 72)
 #undef V
     default:
       return -1;

@@ -70,8 +70,8 @@ def main():
                               P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
         elif kind == "v4":
             rc = L.lab2_v4(kb, pairs, block, items, v[5], v[6], *args)
-        elif kind == "v6":   # v6:kb:pairs:block:items:minw:opt:grid:chunk (ticket buffer = XcdSched)
-            rc = L.lab2_v6(kb, pairs, block, items, v[5], v[6], v[7], v[8], *args)
+        elif kind == "v6":   # v6:kb:pairs:block:items:minw:opt:grid
+            rc = L.lab2_v6(kb, pairs, block, items, v[5], v[6], v[7], *args)
         else:
             rc = L.lab2_ar(kb, pairs, block, items, v[5], *args)
         assert rc == 0, (v, rc)
@@ -149,7 +149,7 @@ def main():
         print(f"{':'.join(str(x) for x in v):28s} median {med:8.4f} ms  min {mn:8.4f}  "
               f"{alg / med / 1e6:8.1f} GB/s", flush=True)
     for v in variants:
-        stamped = (v[0] == "v4" and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v6" and v[6] & 8)
+        stamped = (v[0] in ("v4", "r4") and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v6" and v[6] & 8)
         if not stamped:
             continue
         err.zero_()
@@ -159,7 +159,7 @@ def main():
         torch.cuda.synchronize()
         tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
-        if v[0] in ("v4", "v6"):
+        if v[0] in ("v4", "v6", "r4"):
             m = a_[:, :6].mean(0)
             d = np.diff(np.concatenate([[0.0], m]))
             names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
