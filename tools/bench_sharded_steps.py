@@ -1,0 +1,121 @@
+"""Local steps of the multi-GPU sort (grs_sort_sharded) measured on one MI355X, for the
+DESIGN.md §6 scaling estimate of BASELINE config C4 at N ranks (strong scaling, 2^30 / N keys
+per rank).
+
+python tools/bench_sharded_steps.py [--ranks 8] [--reps 10]
+Prints one JSON line per step:
+  partition      grs_partition_ranges of one rank's shard into N buckets with tie-breaking
+                 splitters (the splitters of rank 0, from the host twin over all ranks' samples)
+  local_sort     grs_sort of the received run (2^30 / N keys)
+  sharded_world1 grs_sort_sharded on a one-rank RCCL communicator (samples, device splitters,
+                 partition into one bucket, count all-gather, the one host sync, the self copy,
+                 local sort): its difference to local_sort is the fixed orchestration cost
+"""
+import argparse
+import ctypes
+import json
+import os
+import socket
+import statistics
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import gpuradixsort_amd as grs  # noqa: E402
+from gpuradixsort_amd._lib import check, lib  # noqa: E402
+
+
+def timed(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--total", type=int, default=1 << 30)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L = lib()
+    G, n = a.ranks, a.total // a.ranks
+    seed = 0x6A09E667F3BCC908 + 4
+    S = L.grs_shard_samples_per_rank(G)
+    shard = torch.empty(n, dtype=torch.uint32, device=dev)
+    pos = (torch.arange(S, dtype=torch.int64) * n) // S
+    ak, ap_ = [], []
+    for r in range(G):
+        grs.fill_splitmix(shard, seed, first_index=r * n)
+        ak.append(shard.index_select(0, pos.to(dev)).cpu().numpy())
+        ap_.append(pos.numpy().astype(np.uint32))
+    ak, ap_ = np.concatenate(ak), np.ascontiguousarray(np.concatenate(ap_))
+    order = np.lexsort((np.arange(G * S), ak))
+    sk = np.ascontiguousarray(ak[order])
+    sj = np.ascontiguousarray(order.astype(np.uint32))
+    spl = np.zeros(max(G - 1, 1), np.uint32)
+    th = np.zeros(max(G - 1, 1), np.uint32)
+    check(L.grs_shard_splitters_host(sk.ctypes.data, sj.ctypes.data, ap_.ctypes.data, 4, G, S, 0,
+                                     spl.ctypes.data, th.ctypes.data), "splitters")
+    grs.fill_splitmix(shard, seed, first_index=0)
+    s = grs.RadixSorter(n, key_bits=32)
+    out = torch.empty_like(shard)
+    cnt = torch.zeros(16, dtype=torch.uint32, device=dev)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def part():
+        check(L.grs_partition_ranges(s._h, ctypes.c_void_p(shard.data_ptr()), None,
+                                     ctypes.c_void_p(out.data_ptr()), None, n, spl.ctypes.data,
+                                     th.ctypes.data, G - 1, ctypes.c_void_p(cnt.data_ptr()), sp),
+              "partition")
+    ms = timed(part, a.reps)
+    s.check_error()
+    print(json.dumps({"step": "partition", "ranks": G, "n_local": n, "ms": round(ms, 4),
+                      "GB/s": round(n * 8 / ms / 1e6, 1)}), flush=True)
+
+    bufs = [torch.empty_like(shard) for _ in range(a.reps + 1)]
+    for b in bufs:
+        grs.fill_splitmix(b, seed)
+    it = iter(bufs)
+    ms = timed(lambda: s.sort(next(it)), a.reps)
+    s.check_error()
+    print(json.dumps({"step": "local_sort", "n": n, "ms": round(ms, 4),
+                      "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
+    del bufs
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    sh = ShardedSorter(n, key_bits=32, device=dev)
+    bufs = [torch.empty_like(shard) for _ in range(a.reps + 1)]
+    for b in bufs:
+        grs.fill_splitmix(b, seed)
+    it = iter(bufs)
+    ms = timed(lambda: sh.sort(next(it), check_error=False), a.reps)
+    sh.sorter.check_error()
+    assert sh.count_inversions() == 0
+    print(json.dumps({"step": "sharded_world1", "n": n, "ms": round(ms, 4),
+                      "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
+    sh.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
