@@ -75,12 +75,14 @@ struct MatchTile {
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 32) : (PAIRS ? 10 : 16);
   static constexpr int TILE = BLOCK * ITEMS;
 };
-// Partition pass (key-range buckets for the multi-GPU exchange): its digit needs the element
-// index, so the reordered digits are kept in LDS (one byte per key) beside the tile.
+// Partition pass (key-range buckets for the multi-GPU exchange): the big tiles (its digit
+// needs the element index, so the store phase reads a position's digit off the tile-local
+// digit starts instead of the key).  36K-key tiles: 2^27 keys into 8 buckets 0.38 -> 0.xx ms
+// against round 1's 24K tiles with one digit byte per key in LDS.
 template <typename K, bool PAIRS>
 struct PartTile {
   static constexpr int BLOCK = 1024, MINW = 1;
-  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 24) : (PAIRS ? 8 : 16);
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 11 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
 };
 // Pass options (grs_pass.hpp OPT bits): big tiles 16-bit wave counters + look-back after the
@@ -201,6 +203,7 @@ struct grs_sorter {
   int hist2_grid = 0;              // GRS_HIST2_GRID: grs_upfront_hist2 grid (0 = auto)
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
   int pass_mode = 0;               // GRS_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
+  bool sharded_general = false;    // GRS_SHARDED=general: one rank takes the G-rank path too (tests)
 };
 
 extern "C" {
@@ -322,6 +325,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
+  if (const char* e = std::getenv("GRS_SHARDED")) s->sharded_general = std::strcmp(e, "general") == 0;
   if (const char* e = std::getenv("GRS_PASS"))
     s->pass_mode = std::strcmp(e, "v6") == 0 ? 6 : std::strcmp(e, "v4") == 0 ? 4 : 0;
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
@@ -1125,7 +1129,6 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
                       al(static_cast<size_t>(g) * g * 4) + al(sizeof(Dig));
   if (s->shard_bytes < need) {
     if (s->shard_buf) (void)hipFree(s->shard_buf);
-  if (s->rec_buf) (void)hipFree(s->rec_buf);
     s->shard_buf = nullptr;
     s->shard_bytes = 0;
     if (hipMalloc(&s->shard_buf, need) != hipSuccess) {
@@ -1244,7 +1247,22 @@ grs_status grs_sort_sharded(grs_sorter* s, const void* d_keys_in, const uint32_t
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint32_t n32 = static_cast<uint32_t>(n_local);
   grs_status r;
-  if (s->key_type == GRS_KEY_U32)
+  if (g == 1 && !s->sharded_general) {   // one rank: nothing to partition or exchange
+    if (out_capacity < n_local) {
+      r = set_err(GRS_ECAPACITY, "grs_sort_sharded: out_capacity below n_local");
+    } else {
+      const size_t kb = s->key_type == GRS_KEY_U32 ? 4 : 8;
+      r = GRS_OK;
+      if (n_local && d_keys_out != d_keys_in &&
+          hipMemcpyAsync(d_keys_out, d_keys_in, n_local * kb, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        r = set_err(GRS_EHIP, "grs_sort_sharded: copy");
+      if (r == GRS_OK && s->pairs && n_local && d_vals_out != d_vals_in &&
+          hipMemcpyAsync(d_vals_out, d_vals_in, n_local * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        r = set_err(GRS_EHIP, "grs_sort_sharded: copy");
+      if (r == GRS_OK) r = grs_sort(s, d_keys_out, s->pairs ? d_vals_out : nullptr, n_local, stream);
+      if (r == GRS_OK) *n_out = n_local;
+    }
+  } else if (s->key_type == GRS_KEY_U32)
     r = s->pairs ? run_sharded<uint32_t, true>(s, (const uint32_t*)d_keys_in, d_vals_in, n32, (uint32_t*)d_keys_out, d_vals_out, out_capacity, n_out, comm, g, me, st)
                  : run_sharded<uint32_t, false>(s, (const uint32_t*)d_keys_in, nullptr, n32, (uint32_t*)d_keys_out, nullptr, out_capacity, n_out, comm, g, me, st);
   else

@@ -250,7 +250,8 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
     for (int e = 0; e < VEC; ++e) count(kk[e]);
   }
   // ragged tail (fewer than VEC keys)
-  for (uint32_t i = nvec * VEC + blockIdx.x * GRS_HIST_BLOCK + t; i < n;
+  // 64-bit index: i + stride can pass 2^32 when n is near GRS_MAX_N
+  for (uint64_t i = static_cast<uint64_t>(nvec) * VEC + blockIdx.x * GRS_HIST_BLOCK + t; i < n;
        i += gridDim.x * GRS_HIST_BLOCK)
     count(keys[i]);
   __syncthreads();
@@ -394,7 +395,8 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
 #pragma unroll
     for (int e = 0; e < VEC; ++e) count(kk[e]);
   }
-  for (uint32_t i = nvec * VEC + blockIdx.x * HB + t; i < n; i += stride) count(keys[i]);
+  for (uint64_t i = static_cast<uint64_t>(nvec) * VEC + blockIdx.x * HB + t; i < n; i += stride)
+    count(keys[i]);   // 64-bit index: i + stride can pass 2^32 near GRS_MAX_N
   __syncthreads();
 
   // reduce the copies: count of super digit value d at position q (rotated start: the 32
@@ -465,8 +467,35 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_digit_hist(
   for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < clear_words; i += gridDim.x * GRS_HIST_BLOCK)
     clear[i] = 0;
   __syncthreads();
-  for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < n; i += gridDim.x * GRS_HIST_BLOCK)
-    atomicAdd(&s_hist[digit_call(dg, keys[i], i) * GRS_WAVE + lane], 1u);
+  auto count = [&](K k, uint32_t i) { atomicAdd(&s_hist[digit_call(dg, k, i) * GRS_WAVE + lane], 1u); };
+  // 16-B loads, U in flight per thread (a scalar 4-B load per key left the partition's
+  // histogram latency-bound); the ragged tail and unaligned bases take scalar loads
+  constexpr int VEC = 16 / sizeof(K);
+  constexpr int U = 4;
+  const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : n / VEC;
+  const uint4* kv = reinterpret_cast<const uint4*>(keys);
+  const uint32_t stride = gridDim.x * GRS_HIST_BLOCK;
+  uint32_t v = blockIdx.x * GRS_HIST_BLOCK + t;
+  for (; v + (U - 1) * stride < nvec; v += U * stride) {
+    uint4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = kv[v + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const K* kk = reinterpret_cast<const K*>(&x[u]);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) count(kk[e], (v + u * stride) * VEC + e);
+    }
+  }
+  for (; v < nvec; v += stride) {
+    const uint4 x = kv[v];
+    const K* kk = reinterpret_cast<const K*>(&x);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) count(kk[e], v * VEC + e);
+  }
+  for (uint64_t i = static_cast<uint64_t>(nvec) * VEC + blockIdx.x * GRS_HIST_BLOCK + t; i < n;
+       i += stride)
+    count(keys[i], static_cast<uint32_t>(i));   // 64-bit index: no wrap near GRS_MAX_N
   __syncthreads();
   if (t < static_cast<uint32_t>(NB)) {
     uint32_t c = 0;

@@ -154,7 +154,9 @@ struct V4Smem {
   uint32_t next;                // persistent kernel: the next tile's ticket
   alignas(16) K keys[LTILE];
   uint32_t vals[PAIRS ? LTILE : 1];
-  uint8_t dig8[IDX ? LTILE : 1];  // indexed digits: digit of each reordered position
+  // indexed digits (partition): tile-local start of every digit, from which the store phase
+  // reads off the digit of a reordered position (the key alone does not determine it)
+  uint32_t lstart[IDX ? RADIX + 1 : 1];
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
@@ -196,11 +198,15 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
       for (int j = 0; j < ITEMS; ++j) val[j] = ld(vals_in, wbase + j * GRS_WAVE);
     }
   } else {
+    // the last tile: compare tile-local offsets, never global indices (tile_base + TILE can
+    // pass 2^32 when n is near GRS_MAX_N, and a wrapped index would read as in range)
+    const uint32_t valid = n - tile_base;
+    const uint32_t lbase = w * (GRS_WAVE * ITEMS) + lane;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const uint32_t i = wbase + j * GRS_WAVE;
-      key[j] = i < n ? keys_in[i] : static_cast<K>(~static_cast<K>(0));
-      if constexpr (PAIRS) val[j] = i < n ? vals_in[i] : 0u;
+      const bool in = lbase + j * GRS_WAVE < valid;
+      key[j] = in ? keys_in[wbase + j * GRS_WAVE] : static_cast<K>(~static_cast<K>(0));
+      if constexpr (PAIRS) val[j] = in ? vals_in[wbase + j * GRS_WAVE] : 0u;
     }
   }
 }
@@ -267,20 +273,37 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // digit of item j (indexed digits: of (key, shard-local index); padding: the largest)
   auto dig_of = [&](int j) -> uint32_t {
     if constexpr (IDX) {
-      const uint32_t i = tile_base + w * (GRS_WAVE * ITEMS) + j * GRS_WAVE + lane;
-      return (valid == static_cast<uint32_t>(TILE) || i < n) ? dig(key[j], i) : dmask;
+      const uint32_t local = w * (GRS_WAVE * ITEMS) + j * GRS_WAVE + lane;
+      return local < valid ? dig(key[j], tile_base + local) : dmask;
     } else {
       return dig(key[j]);
     }
   };
 
-  // ---- rank ----  (two 16-bit ranks per register: a wave ranks at most 64 * ITEMS keys)
+  // ---- rank ----  (two 16-bit ranks per register: a wave ranks at most 64 * ITEMS keys).
+  // Indexed digits cost tens of VALU each (the splitter compares), so theirs is computed once
+  // and kept in the rank field's top 4 bits for the reorder (ranks < 2^12, digits < 16).
   static_assert(GRS_WAVE * ITEMS < 65536, "16-bit ranks");
+  static_assert(!IDX || (GRS_WAVE * ITEMS <= 4096 && RADIX <= 16 && ROUNDS == 1 && !C16),
+                "indexed digits ride in the rank field, with 32-bit wave counters");
   uint32_t rank[(ITEMS + 1) / 2];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     uint32_t r;
-    if constexpr ((OPT & 512) != 0) {
+    if constexpr (IDX) {
+      const uint32_t d = dig_of(j);
+      if constexpr ((OPT & 512) != 0) {
+        const uint64_t m = match_digit<RB>(d);
+        const uint32_t below = mbcnt64(m);
+        uint32_t* c = &sm.cnt[w * RADIX + d];
+        const uint32_t old = *c;
+        if (below == 0) atomicAdd(c, static_cast<uint32_t>(__popcll(m)));
+        r = old + below;
+      } else {
+        r = atomicAdd(&sm.cnt[w * RADIX + d], 1u);
+      }
+      r |= d << 12;
+    } else if constexpr ((OPT & 512) != 0) {
       // peers of this lane's digit in this item: the lowest one adds their count; LDS runs a
       // wave's instructions in order, so the plain read sees items < j exactly
       static_assert(!C16, "match ranking uses 32-bit counters");
@@ -352,6 +375,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     }
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
+    if constexpr (IDX) {
+      sm.lstart[t] = lstart;
+      if (t == static_cast<uint32_t>(RADIX - 1)) sm.lstart[RADIX] = TILE;
+    }
     if constexpr ((OPT & (16 | 64)) == 0 && !PF) lb.issue(status, gacc, ginc, tile, t);
   }
   lds_barrier();  // B3
@@ -364,12 +391,17 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   for (int j = 0; j < ITEMS; ++j) asm volatile("" : "+v"(key[j]));
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t r = (j & 1) ? rank[j / 2] >> 16 : rank[j / 2] & 0xFFFFu;
-    const uint32_t d = dig_of(j);
+    uint32_t r = (j & 1) ? rank[j / 2] >> 16 : rank[j / 2] & 0xFFFFu;
+    uint32_t d;
+    if constexpr (IDX) {
+      d = r >> 12;
+      r &= 0xFFFu;
+    } else {
+      d = dig_of(j);
+    }
     const uint32_t pos = cnt_ld(w * RADIX + d) + r;
     if (ROUNDS == 1 || pos < static_cast<uint32_t>(LTILE)) {
       sm.keys[pos] = key[j];
-      if constexpr (IDX) sm.dig8[pos] = static_cast<uint8_t>(d);
       if constexpr (PAIRS) sm.vals[pos] = val[j];
     }
     if constexpr (ROUNDS > 1) {   // the rank register now holds the tile position
@@ -400,9 +432,17 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   V4_STAMP(4);
 
   // ---- store: consecutive threads write consecutive slots of each digit run ----
-  auto dig_at = [&](uint32_t i, K kk) -> uint32_t {  // digit of reordered position i
-    if constexpr (IDX) return sm.dig8[i];
-    else return dig(kk);
+  // digit of reordered position i.  Indexed digits: a thread visits increasing positions, so
+  // its digit only moves forward through the tile-local digit starts (at most RADIX - 1 steps
+  // per tile, over empty digits too).
+  uint32_t dcur = 0;
+  auto dig_at = [&](uint32_t i, K kk) -> uint32_t {
+    if constexpr (IDX) {
+      while (i >= sm.lstart[dcur + 1]) ++dcur;
+      return dcur;
+    } else {
+      return dig(kk);
+    }
   };
 #pragma unroll
   for (int rr = 0; rr < ROUNDS; ++rr) {
@@ -415,7 +455,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         const uint32_t lp = pos - static_cast<uint32_t>(rr * LTILE);
         if (lp < static_cast<uint32_t>(LTILE)) {
           sm.keys[lp] = key[j];
-          if constexpr (IDX) sm.dig8[lp] = static_cast<uint8_t>(dig_of(j));
           if constexpr (PAIRS) sm.vals[lp] = val[j];
         }
       }
@@ -427,7 +466,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       for (int k = 0; k < LITEMS; ++k) {
         const uint32_t i = k * BLOCK + t;
         const K kk = sm.keys[i];
-        uint32_t dst = sm.base[dig_at(i, kk)] + roff + i;
+        uint32_t dst = sm.base[dig_at(roff + i, kk)] + roff + i;
         if constexpr ((OPT & 64) != 0) dst = min(dst, n - 1);
         if constexpr ((OPT & 32) != 0) dst = tile_base + roff + i;
         keys_out[dst] = kk;
@@ -439,7 +478,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         const uint32_t i = k * BLOCK + t;
         if (roff + i < valid) {
           const K kk = sm.keys[i];
-          const uint32_t dst = sm.base[dig_at(i, kk)] + roff + i;
+          const uint32_t dst = sm.base[dig_at(roff + i, kk)] + roff + i;
           keys_out[dst] = kk;
           if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
         }

@@ -111,3 +111,48 @@ def test_c4_eight_shard_pipeline_on_one_gpu(gpu):
     local.close()
     del parts, shard
     torch.cuda.empty_cache()
+
+
+def _checksums(k: torch.Tensor):
+    """Order-independent checksums of a uint32 tensor: the sum of its values and the sum of
+    their images under a multiplicative hash, both as int32 reinterpretations summed in int64."""
+    v = k.view(torch.int32)
+    s1 = int(v.sum(dtype=torch.int64).item())
+    h = v * -1640531535                         # 0x9E3779B1, wrapping in int32
+    s2 = int(h.sum(dtype=torch.int64).item())
+    del h
+    return s1, s2
+
+
+def test_max_n_one_call(gpu):
+    """GRS_MAX_N = 2^32 - 2^16 keys in ONE call (the largest the +1-encoded 32-bit look-back
+    prefixes and 32-bit tile positions allow): sorted, and the same multiset (checksums), at
+    the size where any 32-bit index overflow in the kernels would show."""
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd._lib import GRS_MAX_N
+
+    import time
+
+    n = GRS_MAX_N
+    t0 = time.time()
+
+    def note(what):
+        print(f"  max_n: {what} at {time.time() - t0:.2f} s", flush=True)
+
+    k = torch.empty(n, dtype=torch.uint32, device=gpu)
+    grs.fill_splitmix(k, 0x6A09E667F3BCC908 + 4, first_index=1 << 40)
+    torch.cuda.synchronize()
+    note("filled")
+    before = _checksums(k)
+    note("checksummed")
+    s = grs.RadixSorter(n, key_bits=32)
+    note("sorter created")
+    s.sort(k)
+    s.check_error()
+    note("sorted")
+    assert grs.count_inversions(k) == 0
+    note("inversions counted")
+    assert _checksums(k) == before
+    s.close()
+    del k
+    torch.cuda.empty_cache()

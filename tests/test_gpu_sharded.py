@@ -33,11 +33,18 @@ def world1(gpu):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("path", ["general", "one_rank"])
 @pytest.mark.parametrize("key_bits,pairs,dist_name", [(32, False, "uniform"), (32, True, "ties"),
                                                       (64, True, "uniform"), (64, False, "ties"),
                                                       (32, True, "all_equal")])
-def test_sharded_sort_world1_rccl(gpu, world1, key_bits, pairs, dist_name):
+def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pairs, dist_name):
+    """path "general": GRS_SHARDED=general makes the one-rank call take the G-rank path
+    (samples, all-gathers, device splitters, partition, count matrix, host sync, grouped
+    send/recv with the self copy, local sort); "one_rank": the copy + local sort fast path."""
     from gpuradixsort_amd.sharded import ShardedSorter
+
+    if path == "general":
+        monkeypatch.setenv("GRS_SHARDED", "general")
 
     rng = np.random.default_rng(key_bits + pairs)
     dt = np.uint32 if key_bits == 32 else np.uint64
@@ -58,6 +65,32 @@ def test_sharded_sort_world1_rccl(gpu, world1, key_bits, pairs, dist_name):
         if pairs:
             assert np.array_equal(vo.cpu().numpy(), perm)
     assert s.count_inversions() == 0
+    s.sorter.close()
+
+
+def test_records_then_sharded_scratch(gpu, world1, monkeypatch):
+    """A record sort, then sharded sorts on the same sorter (their scratch buffers are
+    allocated on first use and must not free each other's), then the record sort again."""
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    monkeypatch.setenv("GRS_SHARDED", "general")
+    n = 200_003
+    s = ShardedSorter(n, key_bits=32, pairs=True, device=gpu, comm=world1)
+    rs = grs.RecordSort(n, key_bits=32)
+    rs._sorter.close()
+    rs._sorter = s.sorter                      # one libgrs sorter for both entry points
+    rng = np.random.default_rng(3)
+    rec = rng.integers(0, 2**32, (n, 3), dtype=np.uint64).astype(np.uint32)
+    for _ in range(2):
+        r = torch.from_numpy(rec.copy()).to(gpu)
+        rs.sort(r, field=4)
+        perm = oracle.stable_argsort(rec[:, 1].copy())
+        assert np.array_equal(r.cpu().numpy(), rec[perm])
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        ko, vo = s.sort(torch.from_numpy(keys).to(gpu),
+                        torch.arange(n, dtype=torch.int64, device=gpu).to(torch.uint32))
+        assert np.array_equal(ko.cpu().numpy(), np.sort(keys, kind="stable"))
     s.sorter.close()
 
 

@@ -90,6 +90,29 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict_
 
 }  // namespace
 
+
+// LDS returning-atomic throughput by same-address multiplicity: each wave does ITER returning
+// ds_add_u32 on counter (lane % DISTINCT) of its own 256-word region (+ a per-iteration rotation
+// so that consecutive instructions hit different words); cycles per wave-instruction from
+// s_memtime.  DISTINCT = 64: no two lanes share an address; 16: 4 lanes per address; 1: all.
+template <int DISTINCT>
+__global__ __launch_bounds__(1024) void lds_atomic_rate(uint32_t* out, int iters) {
+  __shared__ uint32_t c[16 * 256];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (uint32_t i = t; i < 16 * 256; i += 1024) c[i] = 0;
+  __syncthreads();
+  uint32_t acc = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    const uint32_t a = w * 256 + ((lane % DISTINCT) * 4 + it) % 256;
+    acc += atomicAdd(&c[a], 1u);
+  }
+  __syncthreads();
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (t == 0) out[blockIdx.x] = static_cast<uint32_t>(t1 - t0);
+  if (acc == 0xFFFFFFFFu) out[1023] = acc;
+}
+
 extern "C" {
 
 // pass memory-pattern emulation: block, items, mode, dynamic LDS bytes (occupancy control)
@@ -265,6 +288,20 @@ int lab2_ar(int kb, int pairs, int block, int items, int dbg, const void* in, vo
 }
 
 // copy / read ceilings: kind 0 = copy, 1 = read; unroll 1/4/8; grid
+// cycles per returning ds_add wave-instruction (16 waves per CU) for DISTINCT addresses per wave
+int lab2_lds_atomic(int distinct, int iters, uint32_t* out, int blocks, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (distinct) {
+    case 64: hipLaunchKernelGGL(lds_atomic_rate<64>, dim3(blocks), dim3(1024), 0, s, out, iters); break;
+    case 32: hipLaunchKernelGGL(lds_atomic_rate<32>, dim3(blocks), dim3(1024), 0, s, out, iters); break;
+    case 16: hipLaunchKernelGGL(lds_atomic_rate<16>, dim3(blocks), dim3(1024), 0, s, out, iters); break;
+    case 8: hipLaunchKernelGGL(lds_atomic_rate<8>, dim3(blocks), dim3(1024), 0, s, out, iters); break;
+    case 1: hipLaunchKernelGGL(lds_atomic_rate<1>, dim3(blocks), dim3(1024), 0, s, out, iters); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int lab2_stream(int kind, int unroll, int grid, const void* in, void* out, uint64_t bytes,
                 void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);

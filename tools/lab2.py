@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--variants", default="v4:32:0:256:72:2:0")
     ap.add_argument("--copy", action="store_true")
+    ap.add_argument("--lds-atomic", action="store_true", help="returning ds_add rate by address multiplicity")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
     a = ap.parse_args()
@@ -94,6 +95,16 @@ def main():
             if r == 0:
                 print(f"   {times[v][-1]:.4f} ms  err={int(err[0].item())}", flush=True)
     print(f"n={n}  error word={int(err[0].item())}", flush=True)
+    if a.lds_atomic:
+        o = torch.zeros(1024, dtype=torch.uint32, device=dev)
+        for d in (64, 32, 16, 8, 1):
+            for _ in range(2):
+                assert L.lab2_lds_atomic(d, 4096, P(o), 256, sp) == 0
+                torch.cuda.synchronize()
+            cyc = o[:256].to(torch.float64).mean().item()
+            # s_memtime ticks at 100 MHz on gfx9: convert with the shader clock estimate below
+            print(f"lds_atomic distinct={d:2d}: {cyc / 4096:8.3f} memtime ticks per wave-iteration "
+                  f"(16 waves per CU)", flush=True)
     if a.copy:
         src = torch.empty(n * 2, dtype=torch.uint32, device=dev)
         src.fill_(7)
