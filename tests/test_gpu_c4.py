@@ -156,3 +156,32 @@ def test_max_n_one_call(gpu):
     s.close()
     del k
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+def test_max_n_pairs_one_call(gpu, kb):
+    """GRS_MAX_N (key, index) pairs in one call, u32 and u64 keys: keys sorted and
+    keys_in[payload] == keys_out (the payload is the stable permutation)."""
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd._lib import GRS_MAX_N
+
+    n = GRS_MAX_N
+    kdt = torch.uint32 if kb == 32 else torch.uint64
+    k = torch.empty(n, dtype=kdt, device=gpu)
+    grs.fill_splitmix(k, 0x6A09E667F3BCC908 + 3, first_index=1 << 41)
+    orig = k.clone()
+    v = torch.empty(n, dtype=torch.uint32, device=gpu)
+    grs.iota_u32(v)
+    s = grs.RadixSorter(n, key_bits=kb, pairs=True)
+    s.sort(k, v)
+    s.check_error()
+    s.close()                                   # frees the sorter's scratch before the check
+    assert grs.count_inversions(k) == 0
+    iv = torch.int32 if kb == 32 else torch.int64
+    idx = v.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    del v
+    gathered = orig.view(iv)[idx]
+    del idx, orig
+    assert torch.equal(gathered, k.view(iv))
+    del k, gathered
+    torch.cuda.empty_cache()
