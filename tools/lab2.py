@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--variants", default="v4:32:0:256:72:2:0")
     ap.add_argument("--copy", action="store_true")
     ap.add_argument("--lds-atomic", action="store_true", help="returning ds_add rate by address multiplicity")
+    ap.add_argument("--rot", type=int, default=0, help="OPT 2048 store-sweep rotation per tile (keys)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
     a = ap.parse_args()
@@ -54,6 +55,7 @@ def main():
     ticket = torch.zeros(64, dtype=torch.uint32, device=dev)   
     max_tiles = n // 4096 + 64
     err = torch.zeros(64 + 8 * max_tiles + 64, dtype=torch.uint32, device=dev)
+    err[63] = a.rot
     st = torch.zeros(3 * max_tiles * 256, dtype=torch.uint32, device=dev)
     st2 = torch.zeros_like(st)
     torch.cuda.synchronize()
@@ -84,6 +86,7 @@ def main():
             st.zero_()
             ticket.zero_()
             err.zero_()
+            err[63] = a.rot
             torch.cuda.synchronize()
             if r == 0:
                 print("run", v, flush=True)
@@ -144,6 +147,7 @@ def main():
             st.zero_()
             ticket.zero_()
             err.zero_()
+            err[63] = a.rot
             run(v)
             torch.cuda.synchronize()
             k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64)
@@ -164,6 +168,7 @@ def main():
         if not stamped:
             continue
         err.zero_()
+        err[63] = a.rot
         st.zero_()
         ticket.zero_()
         run(v)
