@@ -48,11 +48,17 @@ grs_status set_err(grs_status s, const std::string& msg) {
 // 32-bit counters, early look-back), 125.2 (512 x 72), 107.7 (nontemporal tile loads); C3
 // 59.9 vs 59.2, C5 33.4 vs 32.8.  Big: one 1024-thread workgroup per CU.  Small (grids of
 // less than one big tile per CU): 256-thread workgroups of 1.5K-4K keys, four per CU.
+// u64 pairs: a tile twice what LDS holds, reordered in two rounds (the keys and payloads stay
+// in VGPRs, LDS takes half the tile at a time; 32-bit wave counters): 22K-pair tiles, same
+// process (tools/lab2.py, 2^28 pairs, ms per pass) 1.37 vs 1.48 and 1.45 vs 1.72 on two boxes
+// against one-round 11K tiles.  u32 pairs (26K tiles) and u64 keys (28K-32K) measured no gain.
 template <typename K, bool PAIRS>
 struct BigTile {
   static constexpr int BLOCK = 1024, MINW = 1;
-  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 11 : 17);
+  static constexpr bool TWO_ROUNDS = sizeof(K) == 8 && PAIRS;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 22 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
+  static constexpr uint32_t OPT = TWO_ROUNDS ? (1024u | 16u) : (256u | 16u);
 };
 // 4-bit digits (BASELINE C2): 32-bit wave counters (16-bit ones put 64 lanes on 8 words) and
 // the look-back before the reorder (tools/lab2.py at 2^24 keys: 1024 x 32 0.042 ms per pass).
@@ -61,12 +67,14 @@ struct BigTile4 {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 32) : (PAIRS ? 10 : 16);
   static constexpr int TILE = BLOCK * ITEMS;
+  static constexpr bool TWO_ROUNDS = false;
 };
 template <typename K, bool PAIRS>
 struct SmallTile {
   static constexpr int BLOCK = 256, MINW = 4;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 8 : 16) : (PAIRS ? 6 : 8);
   static constexpr int TILE = BLOCK * ITEMS;
+  static constexpr bool TWO_ROUNDS = false;
 };
 // Ballot-match fallback (32-bit wave counters): the round's first 16-wave shapes.
 template <typename K, bool PAIRS>
@@ -74,6 +82,7 @@ struct MatchTile {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 16 : 32) : (PAIRS ? 10 : 16);
   static constexpr int TILE = BLOCK * ITEMS;
+  static constexpr bool TWO_ROUNDS = false;
 };
 // Partition pass (key-range buckets for the multi-GPU exchange): the big tiles (its digit
 // needs the element index, so the store phase reads a position's digit off the tile-local
@@ -84,12 +93,12 @@ struct PartTile {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 11 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
+  static constexpr bool TWO_ROUNDS = false;
 };
 // Pass options (grs_pass.hpp OPT bits): big tiles 16-bit wave counters + look-back after the
 // reorder; small tiles the look-back after the reorder.  Default-policy tile loads:
 // nontemporal loads made the pass alone faster in tools/lab2.py but the sort slower (C4 2^30
 // keys, same box: 107.5 vs 122.4 Gkeys/s), the pass reading what the previous pass just wrote.
-constexpr uint32_t kBigOpt = 256 | 16;
 constexpr uint32_t kBig4Opt = 0;
 constexpr uint32_t kSmallOpt = 16;
 constexpr uint32_t kMatchOpt = 512 | 16;               // ballot-match ranking (fallback)
@@ -435,7 +444,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
                     int end_bit, hipStream_t stream) {
   using Big = std::conditional_t<RB == 8, BigTile<K, PAIRS>, BigTile4<K, PAIRS>>;
   using Small = SmallTile<K, PAIRS>;
-  constexpr uint32_t kBig = RB == 8 ? kBigOpt : kBig4Opt;
+  constexpr uint32_t kBig = RB == 8 ? BigTile<K, PAIRS>::OPT : kBig4Opt;
   constexpr int RADIX = 1 << RB;
   const bool big = use_big_tiles(s, n, Big::TILE);
   const int passes = (end_bit - begin_bit + RB - 1) / RB;
@@ -444,7 +453,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   uint32_t tile = big ? Big::TILE : Small::TILE;
   if (s->rank_mode != 0 && big) tile = MatchTile<K, PAIRS>::TILE;
   const uint32_t tiles = (n + tile - 1) / tile;
-  const bool persist = use_persistent(s, tiles, RB);
+  // the persistent pass prefetches into the registers a two-round reorder still needs
+  const bool persist = !Big::TWO_ROUNDS && use_persistent(s, tiles, RB);
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
@@ -502,7 +512,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
       r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (persist && big) {
-      r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      if constexpr (!Big::TWO_ROUNDS)
+        r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else {
       r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
@@ -1393,8 +1404,8 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
 
 const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
   if (!s || n == 0) return "";
-  auto pick = [&](size_t big_tile) -> const char* {
-    if (s->rank_mode != 0 || !use_big_tiles(s, n, big_tile)) return "grs_onesweep_v4";
+  auto pick = [&](size_t big_tile, bool two_rounds = false) -> const char* {
+    if (s->rank_mode != 0 || !use_big_tiles(s, n, big_tile) || two_rounds) return "grs_onesweep_v4";
     return use_persistent(s, (n + big_tile - 1) / big_tile, s->radix_bits) ? "grs_onesweep_v6"
                                                                               : "grs_onesweep_v4";
   };
@@ -1403,7 +1414,8 @@ const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
     return u32 ? (s->pairs ? pick(BigTile4<uint32_t, true>::TILE) : pick(BigTile4<uint32_t, false>::TILE))
                : (s->pairs ? pick(BigTile4<uint64_t, true>::TILE) : pick(BigTile4<uint64_t, false>::TILE));
   return u32 ? (s->pairs ? pick(BigTile<uint32_t, true>::TILE) : pick(BigTile<uint32_t, false>::TILE))
-             : (s->pairs ? pick(BigTile<uint64_t, true>::TILE) : pick(BigTile<uint64_t, false>::TILE));
+             : (s->pairs ? pick(BigTile<uint64_t, true>::TILE, BigTile<uint64_t, true>::TWO_ROUNDS)
+                         : pick(BigTile<uint64_t, false>::TILE));
 }
 
 }  // extern "C"

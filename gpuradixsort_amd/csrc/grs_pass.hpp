@@ -238,6 +238,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   static_assert(LITEMS * ROUNDS == ITEMS, "ITEMS divisible by the rounds");
   static_assert(!C16 || TILE < 65536, "16-bit tile positions");
   static_assert(ROUNDS == 1 || TILE < 65536, "two-round reorder keeps 16-bit positions");
+  static_assert(ROUNDS == 1 || !PF, "the prefetch reuses the registers round 2 still needs");
   uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
   constexpr bool IDX = DigitF::kIndexed;
   auto cnt_ld = [&](uint32_t i) -> uint32_t { if constexpr (C16) return c16[i]; else return sm.cnt[i]; };

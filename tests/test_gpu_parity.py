@@ -127,12 +127,14 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_TILE", tile)
-    big = {(32, False): 36864, (32, True): 17408, (64, False): 17408, (64, True): 11264}
+    # u64 pairs: 22K-pair tiles reordered in two rounds of 11K (t // 2 is the round edge)
+    big = {(32, False): 36864, (32, True): 17408, (64, False): 17408, (64, True): 22528}
     small = {(32, False): 4096, (32, True): 2048, (64, False): 2048, (64, True): 1536}
     t = (big if tile == "big" else small)[(kb, pairs)]
     rng = np.random.default_rng(kb * 10 + pairs)
     dt = np.uint32 if kb == 32 else np.uint64
-    sizes = (1, t - 1, t + 1, 8 * t - 1, 8 * t + 1, 8 * t * 9 + 3, 17 * t + 5)
+    sizes = (1, t // 2 - 1, t // 2 + 1, t - 1, t + 1, 8 * t - 1, 8 * t + 1, 8 * t * 9 + 3,
+             17 * t + 5)
     s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=8)
     s4 = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=4)
     for n in sizes:
@@ -183,7 +185,9 @@ def test_ballot_match_fallback(gpu, monkeypatch):
 def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb):
     """GRS_PASS=v6: the persistent big-tile pass (grs_onesweep_v6: resident workgroups loop
     over tickets, the next tile's loads issued behind the reorder) gives the same bit-exact
-    results across tile edges, for every key/payload type and both digit widths."""
+    results across tile edges, for every key/payload type and both digit widths (u64 pairs at
+    8-bit digits keep the two-round v4 pass, whose second round needs the registers the
+    prefetch would take)."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_PASS", "v6")

@@ -68,6 +68,29 @@ def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pair
     s.sorter.close()
 
 
+@pytest.mark.parametrize("path", ["general", "one_rank"])
+def test_sharded_prefix_n(gpu, world1, monkeypatch, path):
+    """n < keys.numel(): only the first n items take part (samples, partition, exchange,
+    sort), and the tail of the input tensor is left alone."""
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    if path == "general":
+        monkeypatch.setenv("GRS_SHARDED", "general")
+    rng = np.random.default_rng(9)
+    total, n = 300_000, 123_457
+    keys = rng.integers(0, 2**32, total, dtype=np.uint64).astype(np.uint32)
+    s = ShardedSorter(total, key_bits=32, pairs=True, device=gpu, comm=world1)
+    k = torch.from_numpy(keys).to(gpu)
+    v = torch.arange(total, dtype=torch.int64, device=gpu).to(torch.uint32)
+    ko, vo = s.sort(k, v, n=n)
+    perm = oracle.stable_argsort(keys[:n])
+    assert s.last_n_out == n
+    assert np.array_equal(ko.cpu().numpy(), keys[:n][perm])
+    assert np.array_equal(vo.cpu().numpy(), perm)
+    assert np.array_equal(k[n:].cpu().numpy(), keys[n:])
+    s.sorter.close()
+
+
 def test_records_then_sharded_scratch(gpu, world1, monkeypatch):
     """A record sort, then sharded sorts on the same sorter (their scratch buffers are
     allocated on first use and must not free each other's), then the record sort again."""

@@ -65,13 +65,21 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict_
   if ((T + 1) * TILE > n) return;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t key[ITEMS];
+  if constexpr (MODE == 7) {   // gather: read the 256 runs of a pass's digit-major layout
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) key[j] = in[T * TILE + w * 64 * ITEMS + j * 64 + lane];
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = j * BLOCK + threadIdx.x;
+      key[j] = in[(i / RUN) * (n / 256) + T * RUN + i % RUN];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) key[j] = in[T * TILE + w * 64 * ITEMS + j * 64 + lane];
+  }
   if (n == 0) pad_lds[threadIdx.x] = key[0];
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     const uint32_t i = k * BLOCK + threadIdx.x;
-    uint32_t dst = MODE == 0 ? T * TILE + i : (i / RUN) * (n / 256) + T * RUN + i % RUN;
+    uint32_t dst = (MODE == 0 || MODE == 7) ? T * TILE + i : (i / RUN) * (n / 256) + T * RUN + i % RUN;
     if (MODE >= 3) dst = dst + 1 == n ? 0u : dst + 1;
     if constexpr (POL == 0) {
       out[dst] = key[k];
@@ -140,6 +148,7 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
     case 51206621: k = (const void*)scatter_emu<512, 66, 1, 2>; break;
     case 51206631: k = (const void*)scatter_emu<512, 66, 1, 3>; break;
     case 102403600: k = (const void*)scatter_emu<1024, 36, 0>; break;
+    case 102403607: k = (const void*)scatter_emu<1024, 36, 7>; break;
     case 102403601: k = (const void*)scatter_emu<1024, 36, 1>; break;
     case 102403621: k = (const void*)scatter_emu<1024, 36, 1, 2>; break;
     case 102403631: k = (const void*)scatter_emu<1024, 36, 1, 3>; break;
@@ -183,6 +192,10 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 768, 64, 1, 1296) V(32, 0, 768, 80, 1, 1296) V(32, 0, 512, 96, 1, 1296)
     V(32, 0, 512, 120, 1, 1296) V(32, 0, 1024, 48, 1, 1040) V(32, 0, 1024, 48, 1, 1280)
     V(64, 1, 1024, 11, 1, 272) V(32, 1, 1024, 17, 1, 272) V(64, 0, 1024, 17, 1, 272)
+    V(32, 1, 1024, 34, 1, 1040) V(64, 0, 1024, 34, 1, 1040) V(64, 1, 1024, 22, 1, 1040)
+    V(32, 1, 1024, 30, 1, 1040) V(64, 0, 1024, 30, 1, 1040) V(64, 1, 1024, 20, 1, 1040)
+    V(64, 1, 1024, 11, 1, 16) V(64, 0, 1024, 32, 1, 1040)
+    V(64, 0, 1024, 28, 1, 1040) V(32, 1, 1024, 26, 1, 1040) V(64, 1, 1024, 22, 1, 1024)
 #undef V
     default:
       return -1;
