@@ -60,6 +60,16 @@ struct BigTile {
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr uint32_t OPT = TWO_ROUNDS ? (1024u | 16u) : (256u | 16u);
 };
+// u32 keys at 8-bit digits, large grids: 48K-key tiles of 768 threads x 64 keys reordered in
+// two rounds (LDS takes half the tile; 168 VGPRs at 3 waves per SIMD).  Longer digit runs per
+// tile: the pass alone (tools/lab2.py, 2^30 keys, same box) 1.90 vs 2.03 ms for the 36K tile,
+// 2^29 0.947 vs 0.974; slower at 2^27 (0.278 vs 0.259) and, inside the sort, at 2^28 (118 vs
+// 121.5 Gkeys/s; C4 2^30: 129-130 vs 122-124, tools/ab_xl.sh).  Used from 32 XL tiles per CU.
+struct XLTile {
+  static constexpr int BLOCK = 768, MINW = 1, ITEMS = 64, TILE = BLOCK * ITEMS;
+  static constexpr bool TWO_ROUNDS = true;
+  static constexpr uint32_t OPT = 1024u | 16u;
+};
 // 4-bit digits (BASELINE C2): 32-bit wave counters (16-bit ones put 64 lanes on 8 words) and
 // the look-back before the reorder (tools/lab2.py at 2^24 keys: 1024 x 32 0.042 ms per pass).
 template <typename K, bool PAIRS>
@@ -213,6 +223,7 @@ struct grs_sorter {
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
   int pass_mode = 0;               // GRS_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
   bool sharded_general = false;    // GRS_SHARDED=general: one rank takes the G-rank path too (tests)
+  int xl_mode = 0;                 // GRS_XL: unset = by size, 1 = 48K two-round u32 tiles wherever big tiles run, 0 = never
 };
 
 extern "C" {
@@ -281,6 +292,13 @@ bool use_persistent(const grs_sorter* s, size_t tiles, int rb) {
   return rb == 4 || tiles <= 4u * static_cast<size_t>(std::max(1, s->cus));
 }
 
+// XL tiles (u32 keys, 8-bit digits, big tiles, atomic ranking): forced, or from 32 per CU.
+bool use_xl(const grs_sorter* s, size_t n) {
+  if (s->rank_mode != 0 || s->xl_mode == 2) return false;
+  return s->xl_mode == 1 ||
+         (n + XLTile::TILE - 1) / XLTile::TILE >= 32u * static_cast<size_t>(std::max(1, s->cus));
+}
+
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
 template <typename K, bool PAIRS>
 size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
@@ -334,6 +352,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
+  if (const char* e = std::getenv("GRS_XL")) s->xl_mode = std::atoi(e) != 0 ? 1 : 2;
   if (const char* e = std::getenv("GRS_SHARDED")) s->sharded_general = std::strcmp(e, "general") == 0;
   if (const char* e = std::getenv("GRS_PASS"))
     s->pass_mode = std::strcmp(e, "v6") == 0 ? 6 : std::strcmp(e, "v4") == 0 ? 4 : 0;
@@ -452,9 +471,12 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   // group words) that the histogram kernel zeroes for pass 0 and every pass for the next one
   uint32_t tile = big ? Big::TILE : Small::TILE;
   if (s->rank_mode != 0 && big) tile = MatchTile<K, PAIRS>::TILE;
+  constexpr bool kXlType = !PAIRS && sizeof(K) == 4 && RB == 8;
+  const bool xl = kXlType && big && use_xl(s, n);
+  if (xl) tile = XLTile::TILE;
   const uint32_t tiles = (n + tile - 1) / tile;
   // the persistent pass prefetches into the registers a two-round reorder still needs
-  const bool persist = !Big::TWO_ROUNDS && use_persistent(s, tiles, RB);
+  const bool persist = !xl && !Big::TWO_ROUNDS && use_persistent(s, tiles, RB);
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
@@ -511,6 +533,9 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     if (s->rank_mode != 0) {
       r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+    } else if (xl) {
+      if constexpr (kXlType)
+        r = launch_pass<K, PAIRS, RB, XLTile, XLTile::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
         r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
@@ -1413,7 +1438,8 @@ const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
   if (s->radix_bits == 4)
     return u32 ? (s->pairs ? pick(BigTile4<uint32_t, true>::TILE) : pick(BigTile4<uint32_t, false>::TILE))
                : (s->pairs ? pick(BigTile4<uint64_t, true>::TILE) : pick(BigTile4<uint64_t, false>::TILE));
-  return u32 ? (s->pairs ? pick(BigTile<uint32_t, true>::TILE) : pick(BigTile<uint32_t, false>::TILE))
+  return u32 ? (s->pairs ? pick(BigTile<uint32_t, true>::TILE)
+                         : pick(BigTile<uint32_t, false>::TILE, use_xl(s, n)))
              : (s->pairs ? pick(BigTile<uint64_t, true>::TILE, BigTile<uint64_t, true>::TWO_ROUNDS)
                          : pick(BigTile<uint64_t, false>::TILE));
 }

@@ -154,6 +154,30 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     s4.close()
 
 
+def test_xl_tiles(gpu, monkeypatch):
+    """GRS_XL=1 pins the 48K-key two-round tile (768 threads x 64 keys, LDS holds half the tile
+    per round) of the u32 keys pass at every big-tile size: bit-exact across tile, round and
+    look-back group edges (the library uses it from 32 tiles per CU)."""
+    import gpuradixsort_amd as grs
+
+    monkeypatch.setenv("GRS_XL", "1")
+    monkeypatch.setenv("GRS_TILE", "big")
+    t, h = 49152, 24576
+    rng = np.random.default_rng(48)
+    sizes = (1, h - 1, h + 1, t - 1, t + 1, t + h + 3, 8 * t - 1, 8 * t + 1, 8 * t * 5 + h + 7)
+    s = grs.RadixSorter(max(sizes), key_bits=32)
+    assert s.pass_kernel_for(max(sizes)) == "grs_onesweep_v4"
+    for n in sizes:
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        keys[::29] = keys[0]
+        keys[::101] = 0xFFFFFFFF
+        k = to_dev(keys, gpu)
+        s.sort(k)
+        s.check_error()
+        assert np.array_equal(k.cpu().numpy(), np.sort(keys, kind="stable")), n
+    s.close()
+
+
 def test_ballot_match_fallback(gpu, monkeypatch):
     """GRS_RANK=match forces ballot-match ranking (the path taken if the LDS order probe
     ever fails): same bit-exact results, both tile shapes."""
