@@ -65,8 +65,13 @@ struct BigTile {
 // tile: the pass alone (tools/lab2.py, 2^30 keys, same box) 1.90 vs 2.03 ms for the 36K tile,
 // 2^29 0.947 vs 0.974; slower at 2^27 (0.278 vs 0.259) and, inside the sort, at 2^28 (118 vs
 // 121.5 Gkeys/s; C4 2^30: 129-130 vs 122-124, tools/ab_xl.sh).  Used from 32 XL tiles per CU.
+// The same for u32 pairs (768 x 40: 2^28 pairs 1.01 vs 1.06 ms per pass) and u64 keys
+// (768 x 44: 0.93 vs 0.96), tools/lab2.py.
+template <typename K, bool PAIRS>
 struct XLTile {
-  static constexpr int BLOCK = 768, MINW = 1, ITEMS = 64, TILE = BLOCK * ITEMS;
+  static constexpr int BLOCK = 768, MINW = 1;
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 40 : 64) : (PAIRS ? 28 : 44);
+  static constexpr int TILE = BLOCK * ITEMS;
   static constexpr bool TWO_ROUNDS = true;
   static constexpr uint32_t OPT = 1024u | 16u;
 };
@@ -292,11 +297,11 @@ bool use_persistent(const grs_sorter* s, size_t tiles, int rb) {
   return rb == 4 || tiles <= 4u * static_cast<size_t>(std::max(1, s->cus));
 }
 
-// XL tiles (u32 keys, 8-bit digits, big tiles, atomic ranking): forced, or from 32 per CU.
-bool use_xl(const grs_sorter* s, size_t n) {
+// XL tiles (8-bit digits, big tiles, atomic ranking): forced, or from 32 per CU.
+bool use_xl(const grs_sorter* s, size_t n, size_t xl_tile) {
   if (s->rank_mode != 0 || s->xl_mode == 2) return false;
   return s->xl_mode == 1 ||
-         (n + XLTile::TILE - 1) / XLTile::TILE >= 32u * static_cast<size_t>(std::max(1, s->cus));
+         (n + xl_tile - 1) / xl_tile >= 32u * static_cast<size_t>(std::max(1, s->cus));
 }
 
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
@@ -471,9 +476,10 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   // group words) that the histogram kernel zeroes for pass 0 and every pass for the next one
   uint32_t tile = big ? Big::TILE : Small::TILE;
   if (s->rank_mode != 0 && big) tile = MatchTile<K, PAIRS>::TILE;
-  constexpr bool kXlType = !PAIRS && sizeof(K) == 4 && RB == 8;
-  const bool xl = kXlType && big && use_xl(s, n);
-  if (xl) tile = XLTile::TILE;
+  using XL = XLTile<K, PAIRS>;
+  constexpr bool kXlType = RB == 8 && !(sizeof(K) == 8 && PAIRS);   // u64 pairs: BigTile is already two-round
+  const bool xl = kXlType && big && use_xl(s, n, XL::TILE);
+  if (xl) tile = XL::TILE;
   const uint32_t tiles = (n + tile - 1) / tile;
   // the persistent pass prefetches into the registers a two-round reorder still needs
   const bool persist = !xl && !Big::TWO_ROUNDS && use_persistent(s, tiles, RB);
@@ -535,7 +541,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (xl) {
       if constexpr (kXlType)
-        r = launch_pass<K, PAIRS, RB, XLTile, XLTile::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        r = launch_pass<K, PAIRS, RB, XL, XL::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
         r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
@@ -1438,10 +1444,10 @@ const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
   if (s->radix_bits == 4)
     return u32 ? (s->pairs ? pick(BigTile4<uint32_t, true>::TILE) : pick(BigTile4<uint32_t, false>::TILE))
                : (s->pairs ? pick(BigTile4<uint64_t, true>::TILE) : pick(BigTile4<uint64_t, false>::TILE));
-  return u32 ? (s->pairs ? pick(BigTile<uint32_t, true>::TILE)
-                         : pick(BigTile<uint32_t, false>::TILE, use_xl(s, n)))
+  return u32 ? (s->pairs ? pick(BigTile<uint32_t, true>::TILE, use_xl(s, n, XLTile<uint32_t, true>::TILE))
+                         : pick(BigTile<uint32_t, false>::TILE, use_xl(s, n, XLTile<uint32_t, false>::TILE)))
              : (s->pairs ? pick(BigTile<uint64_t, true>::TILE, BigTile<uint64_t, true>::TWO_ROUNDS)
-                         : pick(BigTile<uint64_t, false>::TILE));
+                         : pick(BigTile<uint64_t, false>::TILE, use_xl(s, n, XLTile<uint64_t, false>::TILE)));
 }
 
 }  // extern "C"

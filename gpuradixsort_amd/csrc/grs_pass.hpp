@@ -54,10 +54,11 @@ __host__ __device__ constexpr size_t lb3_status_words(size_t tiles, size_t radix
 // Exclusive prefix of digit d over tiles [0, tile): own group's earlier tiles (< G words)
 // plus the group-level prefix (newest published group INCLUSIVE + complete accumulators
 // after it).  issue() sends the first round of loads, finish() consumes them.
-template <int RADIX>
+// GW: groups polled per round.  The two-round (XL) tiles use 4: the window's registers are
+// live across the reorder there, beside the tile's keys and positions.
+template <int RADIX, int GW = GRS_LB_GWIN>
 struct Lb3 {
   static constexpr int G = GRS_LB_GROUP;
-  static constexpr int GW = GRS_LB_GWIN;
   uint32_t tw[G - 1];
   uint32_t gi[GW], ga[GW];
   int32_t ph;
@@ -368,7 +369,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   lds_barrier();  // B2
   V4_STAMP(2);
 
-  Lb3<RADIX> lb;
+  Lb3<RADIX, (ROUNDS > 1 ? 4 : GRS_LB_GWIN)> lb;
   if (t < static_cast<uint32_t>(RADIX)) {
     for (uint32_t ww = 0; ww < w; ++ww) {
       lstart += sm.wsum[ww];

@@ -154,27 +154,34 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     s4.close()
 
 
-def test_xl_tiles(gpu, monkeypatch):
-    """GRS_XL=1 pins the 48K-key two-round tile (768 threads x 64 keys, LDS holds half the tile
-    per round) of the u32 keys pass at every big-tile size: bit-exact across tile, round and
-    look-back group edges (the library uses it from 32 tiles per CU)."""
+@pytest.mark.parametrize("kb,pairs,t", [(32, False, 768 * 64), (32, True, 768 * 40),
+                                        (64, False, 768 * 44)])
+def test_xl_tiles(gpu, monkeypatch, kb, pairs, t):
+    """GRS_XL=1 pins the two-round XL tiles (768 threads; LDS holds half the tile per round)
+    at every big-tile size: bit-exact across tile, round and look-back group edges (the
+    library uses them from 32 tiles per CU)."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_XL", "1")
     monkeypatch.setenv("GRS_TILE", "big")
-    t, h = 49152, 24576
-    rng = np.random.default_rng(48)
+    h = t // 2
+    rng = np.random.default_rng(48 + kb + pairs)
+    dt = np.uint32 if kb == 32 else np.uint64
     sizes = (1, h - 1, h + 1, t - 1, t + 1, t + h + 3, 8 * t - 1, 8 * t + 1, 8 * t * 5 + h + 7)
-    s = grs.RadixSorter(max(sizes), key_bits=32)
+    s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs)
     assert s.pass_kernel_for(max(sizes)) == "grs_onesweep_v4"
     for n in sizes:
-        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
         keys[::29] = keys[0]
-        keys[::101] = 0xFFFFFFFF
+        keys[::101] = np.iinfo(dt).max
+        perm = oracle.stable_argsort(keys)
         k = to_dev(keys, gpu)
-        s.sort(k)
+        v = to_dev(np.arange(n, dtype=np.uint32), gpu) if pairs else None
+        s.sort(k, v)
         s.check_error()
-        assert np.array_equal(k.cpu().numpy(), np.sort(keys, kind="stable")), n
+        assert np.array_equal(k.cpu().numpy(), keys[perm]), n
+        if pairs:
+            assert np.array_equal(v.cpu().numpy(), perm), n
     s.close()
 
 

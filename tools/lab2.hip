@@ -199,7 +199,9 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 512, 96, 1, 1040) V(32, 0, 512, 112, 1, 1040) V(32, 0, 768, 64, 1, 1040)
     V(32, 0, 768, 72, 1, 1040) V(32, 0, 512, 72, 1, 16) V(32, 0, 768, 48, 1, 16)
     V(32, 0, 768, 56, 1, 1040) V(32, 0, 768, 60, 1, 1040) V(32, 0, 768, 64, 1, 1024)
-    V(32, 0, 640, 72, 1, 1040) V(32, 0, 896, 56, 1, 1040)
+    V(32, 0, 640, 72, 1, 1040) V(32, 0, 896, 56, 1, 1040) V(32, 0, 768, 68, 1, 1040)
+    V(32, 1, 768, 40, 1, 1040) V(32, 1, 768, 44, 1, 1040) V(32, 1, 768, 48, 1, 1040)
+    V(64, 0, 768, 40, 1, 1040) V(64, 0, 768, 44, 1, 1040) V(64, 1, 768, 28, 1, 1040)
 #undef V
     default:
       return -1;
