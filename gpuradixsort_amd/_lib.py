@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_float, c_int, c_size_t, c_uint32, c_uint64, c_ulonglong, c_void_p
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libgrs.so")
@@ -54,6 +54,7 @@ SIGNATURES = [
     ("grs_destroy", None, [c_void_p]),
     ("grs_scratch_bytes", c_size_t, [c_void_p]),
     ("grs_rank_mode", c_int, [c_void_p]),
+    ("grs_lds_order_check", c_int, [c_int, c_int, c_int, POINTER(c_ulonglong)]),
     ("grs_pass_kernel", c_char_p, [c_void_p, c_size_t]),
     ("grs_sort", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     ("grs_sort_bits", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),

@@ -156,6 +156,48 @@ __global__ void grs_probe_lds_order(uint32_t* out) {
   if (bad) atomicAdd(out, bad);
 }
 
+// At-scale lane-order check (grs_lds_order_check): every wave of 8 ranks `items` digits per
+// lane with returning atomics on its own counters and checks each returned value against
+// ref[d] + (lower lanes of this item with digit d), from a ballot match and a wave-ordered
+// plain LDS count (the LDS runs one wave's instructions in order).
+template <int RB, int PACK>
+__global__ __launch_bounds__(512) void grs_lds_order_scale(uint32_t pattern, uint32_t items,
+                                                           unsigned long long* bad) {
+  constexpr int RADIX = 1 << RB;
+  __shared__ uint32_t cnt[8][RADIX / PACK];
+  __shared__ uint32_t ref[8][RADIX];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t i = threadIdx.x; i < 8u * RADIX / PACK; i += 512) (&cnt[0][0])[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 8u * RADIX; i += 512) (&ref[0][0])[i] = 0;
+  __syncthreads();
+  unsigned long long nbad = 0;
+  const uint64_t seed = (static_cast<uint64_t>(blockIdx.x) * 8 + w) * 0x9E3779B97F4A7C15ull + pattern;
+  for (uint32_t j = 0; j < items; ++j) {
+    const uint64_t r = grs::splitmix64(seed ^ (static_cast<uint64_t>(j) * 64 + lane));
+    uint32_t d;
+    switch (pattern) {
+      case 0: d = static_cast<uint32_t>(r) & (RADIX - 1); break;                 // uniform
+      case 1: d = 7u & (RADIX - 1); break;                                        // all equal
+      case 2: d = (static_cast<uint32_t>(r) & 3u) * (RADIX / 4); break;           // 4 values, one bank
+      case 3: d = lane < 32 ? 3u : static_cast<uint32_t>(r) & (RADIX - 1); break; // half the lanes
+      default: d = ((static_cast<uint32_t>(r) & 15u) * 32u) & (RADIX - 1); break; // 16 values, one bank
+    }
+    const uint64_t m = grs::match_digit<RB>(d);
+    const uint32_t below = grs::mbcnt64(m);
+    const uint32_t expect = ref[w][d] + below;
+    uint32_t got;
+    if constexpr (PACK == 2) {
+      const uint32_t sh = (d & 1u) << 4;
+      got = (atomicAdd(&cnt[w][d >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    } else {
+      got = atomicAdd(&cnt[w][d], 1u);
+    }
+    nbad += got != expect;
+    if (below == 0) ref[w][d] += static_cast<uint32_t>(__popcll(m));
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
 // Rank mode per device: 0 = atomic ranking (probe passed), 1 = ballot-match fallback.
 // GRS_RANK=match in the environment forces the fallback (tests cover both paths).
 int device_rank_mode(int device) {
@@ -1430,6 +1472,34 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
   if (r == GRS_OK && hipMemcpyAsync(d_records, copy, n * record_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     r = set_err(GRS_EHIP, "grs_sort_records: copy back");                          // copy-back
   if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_lds_order_check(int device, int blocks, int items, unsigned long long* mismatches) {
+  if (!mismatches || blocks < 1 || items < 1 || items > 512)
+    return set_err(GRS_EINVAL, "grs_lds_order_check: blocks >= 1, 1 <= items <= 512, non-NULL out");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != device) GRS_HIP(hipSetDevice(device));
+  unsigned long long* d = nullptr;
+  grs_status r = GRS_OK;
+  if (hipMalloc(&d, 8) != hipSuccess) {
+    (void)hipGetLastError();
+    r = set_err(GRS_ENOMEM, "grs_lds_order_check: allocation");
+  }
+  if (r == GRS_OK && hipMemset(d, 0, 8) != hipSuccess) r = set_err(GRS_EHIP, "grs_lds_order_check: memset");
+  for (uint32_t p = 0; r == GRS_OK && p < 5; ++p) {
+    const uint32_t it = static_cast<uint32_t>(items);
+    hipLaunchKernelGGL((grs_lds_order_scale<4, 1>), dim3(blocks), dim3(512), 0, 0, p, it, d);
+    hipLaunchKernelGGL((grs_lds_order_scale<8, 1>), dim3(blocks), dim3(512), 0, 0, p, it, d);
+    hipLaunchKernelGGL((grs_lds_order_scale<8, 2>), dim3(blocks), dim3(512), 0, 0, p, it, d);
+    hipLaunchKernelGGL((grs_lds_order_scale<11, 1>), dim3(blocks), dim3(512), 0, 0, p, it, d);
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_lds_order_check: launch");
+  }
+  if (r == GRS_OK && hipMemcpy(mismatches, d, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_lds_order_check: copy");
+  if (d) (void)hipFree(d);
+  if (prev != device) (void)hipSetDevice(prev);
   return r;
 }
 

@@ -94,8 +94,18 @@ size_t grs_scratch_bytes(const grs_sorter* s);
  * environment variable GRS_RANK=match was set at grs_create).  -1 for a NULL sorter. */
 int grs_rank_mode(const grs_sorter* s);
 
-/* Name of the pass kernel a sort of n items launches ("grs_onesweep_v4"): what profiling
- * and roofline reports attribute the pass time to. */
+/* At-scale check of the property the atomic ranking relies on (the lanes of one returning
+ * ds_add wave-instruction that hit one LDS address see the old values in ascending lane
+ * order), on `device`: for each of 5 digit patterns (uniform, all equal, 4 values on one bank,
+ * half the lanes on one value, 16 values on one bank) and 3 counter layouts (16 / 256 / 2048
+ * bins of 32-bit counters, 256 bins of 16-bit halves), `blocks` 512-thread workgroups rank
+ * `items` digits per lane with returning atomics and compare every returned value with the
+ * rank a ballot match computes independently.  *mismatches = the number that differ (0 on
+ * MI355X).  Synchronises.  New with respect to the reference. */
+grs_status grs_lds_order_check(int device, int blocks, int items, unsigned long long* mismatches);
+
+/* Name of the pass kernel a sort of n items launches ("grs_onesweep_v4" or, on small grids,
+ * "grs_onesweep_v6"): what profiling and roofline reports attribute the pass time to. */
 const char* grs_pass_kernel(const grs_sorter* s, size_t n);
 
 /* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a

@@ -106,6 +106,20 @@ def test_u64_matches_stable_sort(gpu, n, pairs, radix_bits):
             assert np.array_equal(gv, perm), f"{name}: permutation differs"
 
 
+def test_lds_lane_order_at_scale(gpu):
+    """The property the atomic ranking relies on, checked at scale on the device through the
+    C-ABI (grs_lds_order_check): 5 digit patterns x 4 counter layouts x 2048 workgroups x 8
+    waves x 256 items x 64 lanes (5.4 G returning atomics), every returned value compared with
+    a ballot-match rank.  The sorter's create-time probe is a 24-atomic spot check of this."""
+    import ctypes
+
+    from gpuradixsort_amd._lib import check, lib
+
+    bad = ctypes.c_ulonglong(1)
+    check(lib().grs_lds_order_check(gpu.index, 2048, 256, ctypes.byref(bad)), "grs_lds_order_check")
+    assert bad.value == 0
+
+
 def test_rank_mode_is_atomic_on_gfx950(gpu):
     """The LDS lane-order probe passes on MI355X, so the atomic-rank pass runs."""
     s = sorter(32, False, 8, 1 << 20)
