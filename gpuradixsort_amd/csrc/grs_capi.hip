@@ -263,6 +263,8 @@ struct grs_sorter {
   void* rec_buf = nullptr;         // grs_sort_records scratch: keys | index | record copy
   size_t rec_bytes = 0;
   uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
+  void* xbuf = nullptr;            // grs_sort_sharded send buffer: G regions of n_local items
+  size_t xbuf_bytes = 0;
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
   int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the round-1 histogram grid
   int hist_variant = 2;            // GRS_HIST: 1 = grs_upfront_hist, 2 = grs_upfront_hist2
@@ -270,6 +272,7 @@ struct grs_sorter {
   int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
   int pass_mode = 0;               // GRS_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
   bool sharded_general = false;    // GRS_SHARDED=general: one rank takes the G-rank path too (tests)
+  bool sharded_contig = false;     // GRS_SHARDED_SEND=contig: histogram + contiguous send buckets (A/B, tests)
   int xl_mode = 0;                 // GRS_XL: unset = by size, 1 = 48K two-round u32 tiles wherever big tiles run, 0 = never
 };
 
@@ -309,6 +312,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->shard_buf) (void)hipFree(s->shard_buf);
   if (s->rec_buf) (void)hipFree(s->rec_buf);
   if (s->shard_host) (void)hipHostFree(s->shard_host);
+  if (s->xbuf) (void)hipFree(s->xbuf);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   delete[] s->ev;
@@ -401,6 +405,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
   if (const char* e = std::getenv("GRS_XL")) s->xl_mode = std::atoi(e) != 0 ? 1 : 2;
   if (const char* e = std::getenv("GRS_SHARDED")) s->sharded_general = std::strcmp(e, "general") == 0;
+  if (const char* e = std::getenv("GRS_SHARDED_SEND")) s->sharded_contig = std::strcmp(e, "contig") == 0;
   if (const char* e = std::getenv("GRS_PASS"))
     s->pass_mode = std::strcmp(e, "v6") == 0 ? 6 : std::strcmp(e, "v4") == 0 ? 4 : 0;
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
@@ -616,11 +621,15 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
 // whose digit is the bucket (grs::SplitterIdxDigit).  Buckets land contiguously in
 // keys_out / vals_out in bucket order; the count + 1 bucket sizes go to d_counts (device).
 // dig_dev: the functor in device memory (splitters computed on the device) or null.
+// region > 0 (the sharded exchange): no bucket histogram; bucket b goes to
+// keys_out[b * region, ...) instead of after the buckets before it (region >= n, and
+// (count + 1) * region < 2^32), and the bucket sizes come from the look-back's group
+// accumulators afterwards.  That skips one read of the keys.
 template <typename K, bool PAIRS, int N>
 grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
                            uint32_t* vals_out, uint32_t n, const grs::SplitterIdxDigit<K, N>& dig,
                            const grs::SplitterIdxDigit<K, N>* dig_dev, int count,
-                           uint32_t* d_counts, hipStream_t stream) {
+                           uint32_t* d_counts, hipStream_t stream, uint32_t region = 0) {
   using T = PartTile<K, PAIRS>;
   using Dig = grs::SplitterIdxDigit<K, N>;
   const uint32_t tiles = (n + T::TILE - 1) / T::TILE;
@@ -628,10 +637,17 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* hist = s->ctrl;
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
-  const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
-  hipLaunchKernelGGL((grs::grs_digit_hist<K, Dig>), dim3(grid), dim3(GRS_HIST_BLOCK), 0, stream,
-                     keys, n, dig, dig_dev, hist, s->status, static_cast<uint32_t>(words));
-  GRS_HIP(hipGetLastError());
+  if (region) {
+    // "digit counts" of `region` each: the pass's digit-start scan yields b * region
+    GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(hist), static_cast<int>(region),
+                              count + 1, stream));
+    GRS_HIP(hipMemsetAsync(s->status, 0, words * 4, stream));
+  } else {
+    const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
+    hipLaunchKernelGGL((grs::grs_digit_hist<K, Dig>), dim3(grid), dim3(GRS_HIST_BLOCK), 0, stream,
+                       keys, n, dig, dig_dev, hist, s->status, static_cast<uint32_t>(words));
+    GRS_HIP(hipGetLastError());
+  }
   grs_status r;
   if (s->rank_mode == 0)
     r = launch_pass<K, PAIRS, 4, T, kSmallOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
@@ -642,7 +658,15 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
                                               s->ctrl + GRS_CTRL_TICKETS, s->status,
                                               s->status + s->status_words, stream);
   if (r != GRS_OK) return r;
-  GRS_HIP(hipMemcpyAsync(d_counts, hist, (count + 1) * 4, hipMemcpyDeviceToDevice, stream));
+  if (region) {
+    const uint32_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
+    hipLaunchKernelGGL(grs::grs_lb_totals, dim3(1), dim3(64), 0, stream,
+                       s->status + static_cast<size_t>(tiles) * 16, groups, 16u,
+                       static_cast<uint32_t>(count + 1), d_counts);
+    GRS_HIP(hipGetLastError());
+  } else {
+    GRS_HIP(hipMemcpyAsync(d_counts, hist, (count + 1) * 4, hipMemcpyDeviceToDevice, stream));
+  }
   return GRS_OK;
 }
 
@@ -1247,12 +1271,30 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   hipLaunchKernelGGL((grs::grs_shard_splitters<K, N>), dim3(1), dim3(1024), 0, st, ak, ap,
                      static_cast<uint32_t>(g), S, static_cast<uint32_t>(me), dig);
   GRS_HIP(hipGetLastError());
-  // 4. partition into the send buffer (the sorter's ping-pong scratch, free until step 8)
+  // 4. partition into the send buffer: G regions of n items each (bucket b at b * n), so no
+  //    bucket histogram pass is needed (grs_partition's region mode); when G * n reaches 2^32
+  //    the buckets go contiguously into the sorter's ping-pong scratch (free until step 8)
+  const bool regions = n > 0 && static_cast<uint64_t>(g) * n < (1ull << 32) && !s->sharded_contig;
   K* send_k = static_cast<K*>(s->alt_keys);
   uint32_t* send_v = s->alt_vals;
+  if (regions) {
+    const size_t need = static_cast<size_t>(g) * n * (sizeof(K) + (PAIRS ? 4 : 0));
+    if (s->xbuf_bytes < need) {
+      if (s->xbuf) (void)hipFree(s->xbuf);
+      s->xbuf = nullptr;
+      s->xbuf_bytes = 0;
+      if (hipMalloc(&s->xbuf, need) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(GRS_ENOMEM, "grs_sort_sharded: send buffer allocation failed");
+      }
+      s->xbuf_bytes = need;
+    }
+    send_k = static_cast<K*>(s->xbuf);
+    send_v = PAIRS ? reinterpret_cast<uint32_t*>(send_k + static_cast<size_t>(g) * n) : nullptr;
+  }
   if (n > 0) {
     const grs_status r = run_partition_n<K, PAIRS, N>(s, keys, vals, send_k, send_v, n, Dig{}, dig,
-                                                      g - 1, cnt, st);
+                                                      g - 1, cnt, st, regions ? n : 0u);
     if (r != GRS_OK) return r;
   } else {
     GRS_HIP(hipMemsetAsync(cnt, 0, static_cast<size_t>(g) * 4, st));
@@ -1268,6 +1310,8 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   }
   uint64_t soff[16], roff[16], total = 0;
   shard_plan(s->shard_host, g, me, soff, roff, &total);
+  if (regions)
+    for (int p = 0; p < g; ++p) soff[p] = static_cast<uint64_t>(p) * n;
   if (total > out_cap || total > s->capacity)
     return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
                                       " items) exceeds out_capacity or the sorter capacity");

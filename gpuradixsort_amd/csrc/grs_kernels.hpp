@@ -442,6 +442,18 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
   }
 }
 
+// Per-digit totals of a finished pass from its look-back status: every tile added its count to
+// its group's accumulator ((arrivals << 24) | sum), so a digit's total is the sum over groups.
+// One thread per digit (radix <= 16: the partition's buckets).
+__global__ void grs_lb_totals(const uint32_t* __restrict__ gacc, uint32_t groups, uint32_t radix,
+                              uint32_t count, uint32_t* __restrict__ totals) {
+  const uint32_t d = threadIdx.x;
+  if (d >= count) return;
+  uint32_t sum = 0;
+  for (uint32_t g = 0; g < groups; ++g) sum += gacc[static_cast<size_t>(g) * radix + d] & 0xFFFFFFu;
+  totals[d] = sum;
+}
+
 // Digit of key k at shard-local index i, for plain and indexed digit functors.
 template <typename DigitF, typename K>
 __device__ __forceinline__ uint32_t digit_call(const DigitF& dig, K k, uint32_t i) {

@@ -33,18 +33,22 @@ def world1(gpu):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("path", ["general", "one_rank"])
+@pytest.mark.parametrize("path", ["general", "general_contig", "one_rank"])
 @pytest.mark.parametrize("key_bits,pairs,dist_name", [(32, False, "uniform"), (32, True, "ties"),
                                                       (64, True, "uniform"), (64, False, "ties"),
                                                       (32, True, "all_equal")])
 def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pairs, dist_name):
     """path "general": GRS_SHARDED=general makes the one-rank call take the G-rank path
-    (samples, all-gathers, device splitters, partition, count matrix, host sync, grouped
-    send/recv with the self copy, local sort); "one_rank": the copy + local sort fast path."""
+    (samples, all-gathers, device splitters, partition into per-bucket regions of the send
+    buffer, bucket sizes from the look-back, count matrix, host sync, grouped send/recv with
+    the self copy, local sort); "general_contig": the same with the bucket histogram and
+    contiguous send buckets (GRS_SHARDED_SEND=contig); "one_rank": the copy + local sort."""
     from gpuradixsort_amd.sharded import ShardedSorter
 
-    if path == "general":
+    if path.startswith("general"):
         monkeypatch.setenv("GRS_SHARDED", "general")
+    if path == "general_contig":
+        monkeypatch.setenv("GRS_SHARDED_SEND", "contig")
 
     rng = np.random.default_rng(key_bits + pairs)
     dt = np.uint32 if key_bits == 32 else np.uint64
