@@ -77,6 +77,12 @@ SIGNATURES = [
     ("grs_shard_plan_host", c_int, [c_void_p, c_int, c_int, POINTER(c_uint64), POINTER(c_uint64),
                                     POINTER(c_uint64)]),
     ("grs_shard_samples_per_rank", c_int, [c_int]),
+    ("grs_shard_sample", c_int, [c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    ("grs_shard_encode_words_max", c_size_t, [c_size_t, c_int]),
+    ("grs_shard_encode", c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_int,
+                                 c_void_p, c_size_t, c_void_p, c_void_p]),
+    ("grs_shard_decode_merge", c_int, [c_void_p, c_void_p, c_int, POINTER(c_uint64),
+                                       POINTER(c_uint32), c_void_p, c_size_t, c_void_p]),
     ("grs_iota_u32", c_int, [c_void_p, c_size_t, c_uint32, c_void_p]),
     ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),

@@ -22,6 +22,7 @@
 #include "grs_kernels.hpp"
 #include "grs_pass.hpp"
 #include "grs_shard.hpp"
+#include "grs_codec.hpp"
 
 #include <rccl/rccl.h>
 
@@ -265,6 +266,11 @@ struct grs_sorter {
   uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
   void* xbuf = nullptr;            // grs_sort_sharded send buffer: G regions of n_local items
   size_t xbuf_bytes = 0;
+  void* xrbuf = nullptr;           // presorted exchange: the received (encoded) words
+  size_t xrbuf_bytes = 0;
+  void* codec_buf = nullptr;       // presorted exchange: plan, block sizes / offsets, scan, co-ranks
+  size_t codec_bytes = 0;
+  int sharded_exchange = 0;        // GRS_SHARDED_EXCHANGE: 0 auto, 1 partition-first, 2 presorted
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
   int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the round-1 histogram grid
   int hist_variant = 2;            // GRS_HIST: 1 = grs_upfront_hist, 2 = grs_upfront_hist2
@@ -313,6 +319,8 @@ void grs_destroy(grs_sorter* s) {
   if (s->rec_buf) (void)hipFree(s->rec_buf);
   if (s->shard_host) (void)hipHostFree(s->shard_host);
   if (s->xbuf) (void)hipFree(s->xbuf);
+  if (s->xrbuf) (void)hipFree(s->xrbuf);
+  if (s->codec_buf) (void)hipFree(s->codec_buf);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   delete[] s->ev;
@@ -406,6 +414,8 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_XL")) s->xl_mode = std::atoi(e) != 0 ? 1 : 2;
   if (const char* e = std::getenv("GRS_SHARDED")) s->sharded_general = std::strcmp(e, "general") == 0;
   if (const char* e = std::getenv("GRS_SHARDED_SEND")) s->sharded_contig = std::strcmp(e, "contig") == 0;
+  if (const char* e = std::getenv("GRS_SHARDED_EXCHANGE"))
+    s->sharded_exchange = std::strcmp(e, "partition") == 0 ? 1 : std::strcmp(e, "presorted") == 0 ? 2 : 0;
   if (const char* e = std::getenv("GRS_PASS"))
     s->pass_mode = std::strcmp(e, "v6") == 0 ? 6 : std::strcmp(e, "v4") == 0 ? 4 : 0;
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
@@ -510,9 +520,12 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
   return GRS_OK;
 }
 
+// src_in (out-of-place, the presorted exchange): pass 0 reads src_in / vsrc_in instead of
+// keys / vals, and the passes alternate so that the last one writes keys / vals (no copy-back).
 template <typename K, bool PAIRS, int RB>
 grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begin_bit,
-                    int end_bit, hipStream_t stream) {
+                    int end_bit, hipStream_t stream, const K* src_in = nullptr,
+                    const uint32_t* vsrc_in = nullptr) {
   using Big = std::conditional_t<RB == 8, BigTile<K, PAIRS>, BigTile4<K, PAIRS>>;
   using Small = SmallTile<K, PAIRS>;
   constexpr uint32_t kBig = RB == 8 ? BigTile<K, PAIRS>::OPT : kBig4Opt;
@@ -553,7 +566,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     const int want = std::min<int>(s->hist_grid_cap, std::max<int>(512, static_cast<int>(n >> 17)));
     const int grid = std::max<int>((n >> 18) + 1, std::min<int>(want, (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
-                       stream, keys, n, begin_bit, end_bit, passes, hist, st0,
+                       stream, src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words));
     GRS_HIP(hipGetLastError());
   } else {
@@ -565,8 +578,9 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     if (grid < need) grid = (need + slots - 1) / slots * slots;
     const bool full = begin_bit == 0 && end_bit == static_cast<int>(8 * sizeof(K));
     auto kern = full ? grs::grs_upfront_hist2<K, RB, true> : grs::grs_upfront_hist2<K, RB, false>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream, keys, n,
-                       begin_bit, end_bit, passes, hist, st0, static_cast<uint32_t>(words));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream,
+                       src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
+                       static_cast<uint32_t>(words));
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
@@ -575,6 +589,14 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   K* dst = static_cast<K*>(s->alt_keys);
   uint32_t* vsrc = vals;
   uint32_t* vdst = s->alt_vals;
+  if (src_in) {   // out of place: the last pass writes keys
+    src = const_cast<K*>(src_in);
+    vsrc = const_cast<uint32_t*>(vsrc_in);
+    if ((passes & 1) != 0) {
+      dst = keys;
+      vdst = vals;
+    }
+  }
   using Dig = grs::RadixDigit<K>;
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
@@ -598,10 +620,17 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     }
     if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;
+    if (src_in && p == 0) {   // pass 1 on: ping-pong between keys and the sorter's scratch
+      src = dst;
+      vsrc = vdst;
+      dst = src == keys ? static_cast<K*>(s->alt_keys) : keys;
+      vdst = src == keys ? s->alt_vals : vals;
+      continue;
+    }
     std::swap(src, dst);
     std::swap(vsrc, vdst);
   }
-  const bool copy = (passes & 1) != 0;
+  const bool copy = !src_in && (passes & 1) != 0;
   if (copy) {  // result sits in scratch: copy back (ParallelSort.cpp:312-318)
     GRS_HIP(hipMemcpyAsync(keys, src, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToDevice,
                            stream));
@@ -1245,7 +1274,7 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
     }
     s->shard_bytes = need;
   }
-  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), (16 * 16 + 4) * 4,
+  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), (16 * 32 + 4) * 4,
                                       hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     return set_err(GRS_ENOMEM, "grs_sort_sharded: pinned allocation failed");
@@ -1339,10 +1368,249 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   return grs_sort(s, out_k, out_v, static_cast<size_t>(total), st);
 }
 
+// ---- presorted exchange (grs_codec.hpp): sort, encode the buckets, exchange, decode, merge --
+
+// Device buffer grown on demand (contents are not kept).
+grs_status grow_buf(void** p, size_t* have, size_t need, const char* what) {
+  if (*have >= need) return GRS_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  if (hipMalloc(p, need) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(GRS_ENOMEM, std::string(what) + ": allocation failed");
+  }
+  *have = need;
+  return GRS_OK;
+}
+
+size_t codec_blocks_max(size_t n, int g) { return n / grs::kCodecBlock + static_cast<size_t>(g); }
+
+// Codec scratch: plan[2G+2] | sizes[2G] | blk_words[nb+1] | blk_woff[nb+1] | blk_meta[2nb] |
+// scan scratch | co-ranks of the merge rounds
+struct CodecScratch {
+  uint32_t *plan, *sizes, *blk_words, *blk_woff, *blk_meta, *corank;
+  void* scan;
+  size_t scan_bytes;
+};
+
+grs_status codec_scratch(grs_sorter* s, size_t n_enc, size_t n_merge, int g, CodecScratch* cs) {
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t nb = codec_blocks_max(n_enc, g);
+  const size_t scan = grs_scan_scratch_bytes(nb + 1);
+  const size_t cor = n_merge / grs::kMergeTile + 2 * grs::kMaxRanks + 2;
+  const size_t need = al(4 * (2 * g + 2)) + al(4 * 2 * g) + 2 * al(4 * (nb + 1)) + al(8 * nb) +
+                      al(scan) + al(4 * cor);
+  const grs_status r = grow_buf(&s->codec_buf, &s->codec_bytes, need, "presorted exchange scratch");
+  if (r != GRS_OK) return r;
+  char* b = static_cast<char*>(s->codec_buf);
+  cs->plan = reinterpret_cast<uint32_t*>(b);      b += al(4 * (2 * g + 2));
+  cs->sizes = reinterpret_cast<uint32_t*>(b);     b += al(4 * 2 * g);
+  cs->blk_words = reinterpret_cast<uint32_t*>(b); b += al(4 * (nb + 1));
+  cs->blk_woff = reinterpret_cast<uint32_t*>(b);  b += al(4 * (nb + 1));
+  cs->blk_meta = reinterpret_cast<uint32_t*>(b);  b += al(8 * nb);
+  cs->scan = b;                                   b += al(scan);
+  cs->scan_bytes = scan;
+  cs->corank = reinterpret_cast<uint32_t*>(b);
+  return GRS_OK;
+}
+
+// Encode the buckets of a sorted shard (u32 keys) split by the device partition digit `dig`:
+// d_send gets bucket 0's [directory][data], then bucket 1's, ...; cs.sizes[2b] / [2b+1] the
+// keys / words of bucket b (device).
+template <int N>
+grs_status codec_encode(grs_sorter* s, const uint32_t* sorted, uint32_t n,
+                        const grs::SplitterIdxDigit<uint32_t, N>* dig, int g, uint32_t* send,
+                        const CodecScratch& cs, hipStream_t st) {
+  hipLaunchKernelGGL((grs::grs_shard_bounds<uint32_t, N>), dim3(1), dim3(64), 0, st, sorted, n, dig,
+                     static_cast<uint32_t>(g), cs.plan);
+  GRS_HIP(hipGetLastError());
+  const uint32_t nb = static_cast<uint32_t>(codec_blocks_max(n, g));
+  const dim3 grid((nb + 4 * grs::kCodecBPW - 1) / (4 * grs::kCodecBPW));   // 4 waves per workgroup
+  hipLaunchKernelGGL(grs::grs_codec_sizes, grid, dim3(256), 0, st, sorted, cs.plan,
+                     static_cast<uint32_t>(g), nb, cs.blk_words, cs.blk_meta);
+  GRS_HIP(hipGetLastError());
+  GRS_HIP(hipMemsetAsync(cs.blk_words + nb, 0, 4, st));
+  grs_status r = grs_exclusive_scan_u32(cs.blk_words, cs.blk_woff, nb + 1, nullptr, cs.scan,
+                                        cs.scan_bytes, st);
+  if (r != GRS_OK) return r;
+  hipLaunchKernelGGL(grs::grs_codec_pack, grid, dim3(256), 0, st, sorted, cs.plan,
+                     static_cast<uint32_t>(g), nb, cs.blk_meta, cs.blk_woff, send, cs.sizes);
+  GRS_HIP(hipGetLastError());
+  (void)s;
+  return GRS_OK;
+}
+
+// Decode the received runs (source p: lens[p] keys encoded at word_off[p] of d_recv) and merge
+// them, in source order for ties, into out (n_total keys).  Scratch: the sorter's ping-pong
+// buffer (capacity >= n_total).
+grs_status codec_decode_merge(grs_sorter* s, const uint32_t* recv, int g, const uint64_t* word_off,
+                              const uint32_t* lens, uint32_t* out, uint64_t n_total,
+                              const CodecScratch& cs, hipStream_t st) {
+  grs::CodecSources src{};
+  src.g = static_cast<uint32_t>(g);
+  uint32_t blocks = 0, run = 0;
+  for (int p = 0; p < g; ++p) {
+    src.blk_base[p] = blocks;
+    src.len[p] = lens[p];
+    src.run_off[p] = run;
+    src.word_off[p] = word_off[p];
+    blocks += (lens[p] + grs::kCodecBlock - 1) / grs::kCodecBlock;
+    run += lens[p];
+  }
+  src.blk_base[g] = blocks;
+  int rounds = 0;
+  for (int k = g; k > 1; k = (k + 1) / 2) ++rounds;
+  uint32_t* alt = static_cast<uint32_t*>(s->alt_keys);
+  uint32_t* in = (rounds & 1) ? alt : out;   // the last round writes out
+  uint32_t* o = (rounds & 1) ? out : alt;
+  if (blocks > 0) {
+    hipLaunchKernelGGL(grs::grs_codec_unpack, dim3((blocks + 4 * grs::kCodecBPW - 1) / (4 * grs::kCodecBPW)),
+                       dim3(256), 0, st, recv, src, in);
+    GRS_HIP(hipGetLastError());
+  }
+  uint32_t off[grs::kMaxRanks + 2];
+  for (int p = 0; p < g; ++p) off[p] = src.run_off[p];
+  off[g] = static_cast<uint32_t>(n_total);
+  for (int k = g; k > 1;) {
+    grs::MergeRound mr{};
+    mr.pairs = static_cast<uint32_t>((k + 1) / 2);
+    off[k + 1] = off[k];   // an odd last run merges with an empty one
+    uint32_t bnd = 0;
+    for (uint32_t i = 0; i < mr.pairs; ++i) {
+      mr.bbase[i] = bnd;
+      const uint32_t len = off[2 * i + 2] - off[2 * i];
+      bnd += (len + grs::kMergeTile - 1) / grs::kMergeTile + 1;
+    }
+    mr.bbase[mr.pairs] = bnd;
+    for (uint32_t i = 0; i <= 2 * mr.pairs; ++i) mr.off[i] = off[i];
+    hipLaunchKernelGGL(grs::grs_merge_corank, dim3((bnd + 255) / 256), dim3(256), 0, st, in, mr,
+                       cs.corank);
+    GRS_HIP(hipGetLastError());
+    const uint32_t tiles = bnd - mr.pairs;
+    if (tiles > 0) {
+      hipLaunchKernelGGL(grs::grs_merge_tiles, dim3(tiles), dim3(256), 0, st, in, o, mr, cs.corank);
+      GRS_HIP(hipGetLastError());
+    }
+    for (uint32_t i = 0; i < mr.pairs; ++i) off[i] = off[2 * i];
+    off[mr.pairs] = static_cast<uint32_t>(n_total);
+    k = static_cast<int>(mr.pairs);
+    std::swap(in, o);
+  }
+  return GRS_OK;
+}
+
+// grs_sort_sharded, presorted exchange (u32 keys, no payload): local sort into out_k, samples
+// of the sorted shard, splitters, bounds + encode, the count / size matrix (the one host
+// synchronisation), one send / recv of encoded words per peer, decode + merge into out_k.
+template <int N>
+grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n, uint32_t* out_k,
+                                 size_t out_cap, size_t* n_out, ncclComm_t comm, int g, int me,
+                                 hipStream_t st) {
+  using Dig = grs::SplitterIdxDigit<uint32_t, N>;
+  const uint32_t S = static_cast<uint32_t>(grs_shard_samples_per_rank(g));
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t gs = static_cast<size_t>(g) * S;
+  const size_t need = al(S * 4) + al(S * 4) + al(gs * 4) + al(gs * 4) + al(4 * 2 * g * g) + al(sizeof(Dig));
+  grs_status r = grow_buf(&s->shard_buf, &s->shard_bytes, need, "grs_sort_sharded: scratch");
+  if (r != GRS_OK) return r;
+  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), (16 * 32 + 4) * 4,
+                                      hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(GRS_ENOMEM, "grs_sort_sharded: pinned allocation failed");
+  }
+  char* b = static_cast<char*>(s->shard_buf);
+  uint32_t* sk = reinterpret_cast<uint32_t*>(b);  b += al(S * 4);
+  uint32_t* sp = reinterpret_cast<uint32_t*>(b);  b += al(S * 4);
+  uint32_t* ak = reinterpret_cast<uint32_t*>(b);  b += al(gs * 4);
+  uint32_t* ap = reinterpret_cast<uint32_t*>(b);  b += al(gs * 4);
+  uint32_t* mat = reinterpret_cast<uint32_t*>(b); b += al(4 * 2 * g * g);
+  Dig* dig = reinterpret_cast<Dig*>(b);
+  CodecScratch cs;
+  if ((r = codec_scratch(s, n, s->capacity, g, &cs)) != GRS_OK) return r;
+  const size_t send_words = n + grs::kCodecDir * codec_blocks_max(n, g);
+  if ((r = grow_buf(&s->xbuf, &s->xbuf_bytes, 4 * send_words, "grs_sort_sharded: send buffer")) != GRS_OK)
+    return r;
+  uint32_t* send = static_cast<uint32_t*>(s->xbuf);
+
+  // 1. local sort, out of place: the sorted shard lands in out_k
+  if (n > 0 && (r = run_sort<uint32_t, false, 8>(s, out_k, nullptr, n, 0, 32, st, keys)) != GRS_OK)
+    return r;
+  // 2-3. samples of the sorted shard (rank-major gather), splitters on the device
+  hipLaunchKernelGGL((grs::grs_shard_samples<uint32_t>), dim3((S + 255) / 256), dim3(256), 0, st,
+                     out_k, n, S, sk, sp);
+  GRS_HIP(hipGetLastError());
+  GRS_RCCL(ncclGroupStart());
+  GRS_RCCL(ncclAllGather(sk, ak, S, ncclUint32, comm, st));
+  GRS_RCCL(ncclAllGather(sp, ap, S, ncclUint32, comm, st));
+  GRS_RCCL(ncclGroupEnd());
+  hipLaunchKernelGGL((grs::grs_shard_splitters_sorted<uint32_t, N>), dim3(1), dim3(1024), 0, st, ak, ap,
+                     static_cast<uint32_t>(g), S, static_cast<uint32_t>(me), dig);
+  GRS_HIP(hipGetLastError());
+  // 4. bounds + encode
+  if ((r = codec_encode<N>(s, out_k, n, dig, g, send, cs, st)) != GRS_OK) return r;
+  // 5. (keys, words) of every bucket of every rank, then the one host synchronisation
+  GRS_RCCL(ncclAllGather(cs.sizes, mat, 2 * g, ncclUint32, comm, st));
+  GRS_HIP(hipMemcpyAsync(s->shard_host, mat, 4 * 2 * g * g, hipMemcpyDeviceToHost, st));
+  GRS_HIP(hipMemcpyAsync(s->shard_host + 2 * g * g, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st));
+  GRS_HIP(hipStreamSynchronize(st));
+  const uint32_t* h = s->shard_host;
+  if (h[2 * g * g] != 0) {
+    GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
+    return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a look-back spin of the local sort exceeded its bound");
+  }
+  uint64_t soff[grs::kMaxRanks], roff[grs::kMaxRanks], total = 0, so = 0, ro = 0;
+  uint32_t lens[grs::kMaxRanks];
+  for (int p = 0; p < g; ++p) {
+    soff[p] = so;
+    so += h[me * 2 * g + 2 * p + 1];
+    roff[p] = ro;
+    ro += h[p * 2 * g + 2 * me + 1];
+    lens[p] = h[p * 2 * g + 2 * me];
+    total += lens[p];
+  }
+  if (total > out_cap || total > s->capacity)
+    return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
+                                      " items) exceeds out_capacity or the sorter capacity");
+  if ((r = grow_buf(&s->xrbuf, &s->xrbuf_bytes, std::max<size_t>(4 * ro, 4), "grs_sort_sharded: receive buffer")) != GRS_OK)
+    return r;
+  uint32_t* recv = static_cast<uint32_t*>(s->xrbuf);
+  // 6. exchange of encoded words; the self part is a device copy
+  GRS_RCCL(ncclGroupStart());
+  for (int p = 0; p < g; ++p) {
+    if (p == me) continue;
+    const size_t sc = h[me * 2 * g + 2 * p + 1], rc = h[p * 2 * g + 2 * me + 1];
+    if (sc) GRS_RCCL(ncclSend(send + soff[p], sc, ncclUint32, p, comm, st));
+    if (rc) GRS_RCCL(ncclRecv(recv + roff[p], rc, ncclUint32, p, comm, st));
+  }
+  GRS_RCCL(ncclGroupEnd());
+  const size_t self = h[me * 2 * g + 2 * me + 1];
+  if (self)
+    GRS_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], 4 * self, hipMemcpyDeviceToDevice, st));
+  // 7. decode + merge into out_k
+  if ((r = codec_decode_merge(s, recv, g, roff, lens, out_k, total, cs, st)) != GRS_OK) return r;
+  *n_out = static_cast<size_t>(total);
+  return GRS_OK;
+}
+
 template <typename K, bool PAIRS>
 grs_status run_sharded(grs_sorter* s, const K* keys, const uint32_t* vals, uint32_t n, K* out_k,
                        uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
                        int me, hipStream_t st) {
+  if constexpr (sizeof(K) == 4 && !PAIRS) {
+    // presorted exchange: u32 keys without payload, up to 4 ranks (GRS_SHARDED_EXCHANGE=
+    // presorted | partition forces one).  It moves ~1 byte a key instead of 4 but adds the
+    // encode and ceil(log2 G) merge rounds; measured on one MI355X at C4 it is
+    // ahead at 2 and 4 ranks and level at 8.  The sorted shard is staged in the output, and
+    // encoded words count in u32.
+    const bool want = s->sharded_exchange == 2 || (s->sharded_exchange == 0 && g <= 4);
+    if (want && out_cap >= n && n < (1u << 31) && s->capacity < (1ull << 31)) {
+      if (g <= 2) return run_sharded_presorted<1>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+      if (g <= 4) return run_sharded_presorted<3>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+      if (g <= 8) return run_sharded_presorted<7>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+      return run_sharded_presorted<15>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+    }
+  }
   if (g <= 2) return run_sharded_n<K, PAIRS, 1>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
   if (g <= 4) return run_sharded_n<K, PAIRS, 3>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
   if (g <= 8) return run_sharded_n<K, PAIRS, 7>(s, keys, vals, n, out_k, out_v, out_cap, n_out, comm, g, me, st);
@@ -1396,6 +1664,99 @@ grs_status grs_sort_sharded(grs_sorter* s, const void* d_keys_in, const uint32_t
   else
     r = s->pairs ? run_sharded<uint64_t, true>(s, (const uint64_t*)d_keys_in, d_vals_in, n32, (uint64_t*)d_keys_out, d_vals_out, out_capacity, n_out, comm, g, me, st)
                  : run_sharded<uint64_t, false>(s, (const uint64_t*)d_keys_in, nullptr, n32, (uint64_t*)d_keys_out, nullptr, out_capacity, n_out, comm, g, me, st);
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_shard_sample(const void* d_keys, size_t n, int key_bytes, int samples,
+                            void* d_sample_keys, uint32_t* d_sample_pos, void* stream) {
+  if ((key_bytes != 4 && key_bytes != 8) || samples <= 0 || !d_sample_keys || !d_sample_pos ||
+      (n > 0 && !d_keys))
+    return set_err(GRS_EINVAL, "grs_shard_sample: bad argument");
+  if (n > GRS_MAX_N) return set_err(GRS_ECAPACITY, "grs_shard_sample: n too large");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 grid((samples + 255) / 256);
+  const uint32_t n32 = static_cast<uint32_t>(n), S = static_cast<uint32_t>(samples);
+  if (key_bytes == 4)
+    hipLaunchKernelGGL((grs::grs_shard_samples<uint32_t>), grid, dim3(256), 0, st,
+                       static_cast<const uint32_t*>(d_keys), n32, S,
+                       static_cast<uint32_t*>(d_sample_keys), d_sample_pos);
+  else
+    hipLaunchKernelGGL((grs::grs_shard_samples<uint64_t>), grid, dim3(256), 0, st,
+                       static_cast<const uint64_t*>(d_keys), n32, S,
+                       static_cast<uint64_t*>(d_sample_keys), d_sample_pos);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
+size_t grs_shard_encode_words_max(size_t n, int nranks) {
+  return n + grs::kCodecDir * codec_blocks_max(n, std::max(nranks, 1));
+}
+
+grs_status grs_shard_encode(grs_sorter* s, const uint32_t* d_sorted, size_t n,
+                            const uint32_t* d_gathered_keys, const uint32_t* d_gathered_pos,
+                            int nranks, int rank, uint32_t* d_send, size_t send_capacity_words,
+                            uint32_t* d_sizes, void* stream) {
+  if (!s || !d_gathered_keys || !d_gathered_pos || !d_send || !d_sizes || (n > 0 && !d_sorted))
+    return set_err(GRS_EINVAL, "grs_shard_encode: NULL argument");
+  if (nranks < 1 || nranks > grs::kMaxRanks || rank < 0 || rank >= nranks)
+    return set_err(GRS_EINVAL, "grs_shard_encode: 1..16 ranks");
+  if (n >= (1u << 31)) return set_err(GRS_ECAPACITY, "grs_shard_encode: n >= 2^31");
+  if (send_capacity_words < grs_shard_encode_words_max(n, nranks))
+    return set_err(GRS_ECAPACITY, "grs_shard_encode: send buffer below grs_shard_encode_words_max");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int g = nranks;
+  const uint32_t S = static_cast<uint32_t>(grs_shard_samples_per_rank(g));
+  auto go = [&](auto nconst) -> grs_status {
+    constexpr int N = decltype(nconst)::value;
+    using Dig = grs::SplitterIdxDigit<uint32_t, N>;
+    grs_status r = grow_buf(&s->shard_buf, &s->shard_bytes, sizeof(Dig), "grs_shard_encode: scratch");
+    if (r != GRS_OK) return r;
+    Dig* dig = static_cast<Dig*>(s->shard_buf);
+    CodecScratch cs;
+    if ((r = codec_scratch(s, n, s->capacity, g, &cs)) != GRS_OK) return r;
+    hipLaunchKernelGGL((grs::grs_shard_splitters_sorted<uint32_t, N>), dim3(1), dim3(1024), 0, st,
+                       d_gathered_keys, d_gathered_pos, static_cast<uint32_t>(g), S,
+                       static_cast<uint32_t>(rank), dig);
+    GRS_HIP(hipGetLastError());
+    if ((r = codec_encode<N>(s, d_sorted, static_cast<uint32_t>(n), dig, g, d_send, cs, st)) != GRS_OK)
+      return r;
+    GRS_HIP(hipMemcpyAsync(d_sizes, cs.sizes, 4 * 2 * g, hipMemcpyDeviceToDevice, st));
+    return GRS_OK;
+  };
+  grs_status r;
+  if (g <= 2) r = go(std::integral_constant<int, 1>{});
+  else if (g <= 4) r = go(std::integral_constant<int, 3>{});
+  else if (g <= 8) r = go(std::integral_constant<int, 7>{});
+  else r = go(std::integral_constant<int, 15>{});
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_shard_decode_merge(grs_sorter* s, const uint32_t* d_recv, int nranks,
+                                  const uint64_t* recv_word_offsets, const uint32_t* recv_keys,
+                                  uint32_t* d_keys_out, size_t out_capacity, void* stream) {
+  if (!s || !recv_word_offsets || !recv_keys || !d_keys_out)
+    return set_err(GRS_EINVAL, "grs_shard_decode_merge: NULL argument");
+  if (nranks < 1 || nranks > grs::kMaxRanks)
+    return set_err(GRS_EINVAL, "grs_shard_decode_merge: 1..16 sources");
+  if (s->key_type != GRS_KEY_U32) return set_err(GRS_EINVAL, "grs_shard_decode_merge: u32 sorter");
+  uint64_t total = 0;
+  for (int p = 0; p < nranks; ++p) total += recv_keys[p];
+  if (total > out_capacity || total > s->capacity || total >= (1ull << 31))
+    return set_err(GRS_ECAPACITY, "grs_shard_decode_merge: received keys exceed a capacity");
+  if (total > 0 && !d_recv) return set_err(GRS_EINVAL, "grs_shard_decode_merge: NULL d_recv");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  CodecScratch cs;
+  grs_status r = codec_scratch(s, 0, s->capacity, nranks, &cs);
+  if (r == GRS_OK)
+    r = codec_decode_merge(s, d_recv, nranks, recv_word_offsets, recv_keys, d_keys_out, total, cs, st);
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
 }

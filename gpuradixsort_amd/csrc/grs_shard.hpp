@@ -107,4 +107,48 @@ __global__ __launch_bounds__(1024) void grs_shard_splitters(const K* __restrict_
   }
 }
 
+// The same splitters when every rank's samples are SORTED (samples of a sorted shard, the
+// presorted exchange): the rank of gathered sample j = (r, i) in (key, j) order is i plus, for
+// every other rank r', the samples of r' before it -- upper_bound of its key in r' < r,
+// lower_bound in r' > r -- found by binary search in LDS instead of a bitonic sort.  One
+// 1024-thread workgroup; output identical to grs_shard_splitters.
+template <typename K, int N>
+__global__ __launch_bounds__(1024) void grs_shard_splitters_sorted(const K* __restrict__ skeys,
+                                                                   const uint32_t* __restrict__ spos,
+                                                                   uint32_t g, uint32_t s, uint32_t rank,
+                                                                   SplitterIdxDigit<K, N>* __restrict__ out) {
+  __shared__ K lk[GRS_SHARD_SAMPLES_MAX];
+  const uint32_t m = g * s;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < m; i += blockDim.x) lk[i] = skeys[i];
+  if (t < static_cast<uint32_t>(GRS_MAX_SPLITTERS)) {   // unused slots never count
+    out->s[t] = static_cast<K>(~static_cast<K>(0));
+    out->th[t] = 0xFFFFFFFFu;
+    if (t == 0) out->count = N;
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < m; j += blockDim.x) {
+    const uint32_t r = j / s;
+    const K key = lk[j];
+    uint32_t q = j - r * s;
+    for (uint32_t rr = 0; rr < g; ++rr) {
+      if (rr == r) continue;
+      const K* l = lk + rr * s;
+      uint32_t lo = 0, hi = s;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rr < r ? l[mid] <= key : l[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      q += lo;
+    }
+    // sample j is splitter b when its rank is quantile b (ranks are a permutation of [0, m))
+    for (uint32_t b = 0; b + 1 < g && b < static_cast<uint32_t>(N); ++b) {
+      if (shard_quantile(b, m, g) == q) {
+        out->s[b] = key;
+        out->th[b] = shard_threshold(r, rank, spos[j]);
+      }
+    }
+  }
+}
+
 }  // namespace grs

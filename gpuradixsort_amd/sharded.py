@@ -6,7 +6,15 @@ Output: rank r holds a contiguous, sorted range of the global stable order; the 
 over ranks in rank order equals the stable sort of the whole input.
 
 All of it runs in libgrs's C-ABI entry point grs_sort_sharded (include/grs.h) on an RCCL
-communicator that libgrs owns (RcclComm below; a C++ caller passes its own ncclComm_t):
+communicator that libgrs owns (RcclComm below; a C++ caller passes its own ncclComm_t).
+
+u32 keys without payload take the PRESORTED exchange (grs_codec.hpp): local sort first, then
+samples / splitters of the sorted shard, each bucket encoded as bit-packed deltas (about a
+byte per key instead of four), the encoded words exchanged, decoded and merged.  The same
+steps are exported for other transports (shard_sample / shard_encode / shard_decode_merge
+below; the one-device simulation of tests/test_gpu_presorted.py uses them).
+
+Other key types take the PARTITION-FIRST exchange:
   1. samples     S regularly spaced (key, position) samples of the shard, RCCL all-gather
   2. splitters   on the device: the G*S samples sorted by (key, global index) in one
                  workgroup, G-1 quantiles -> this rank's partition digit; ties are broken by
@@ -129,3 +137,44 @@ class ShardedSorter:
     def close(self) -> None:
         self.sorter.close()
         self.comm.close()
+
+
+# ---- presorted-exchange steps (transport-independent; include/grs.h) --------------------------
+
+def shard_sample(keys: torch.Tensor, n: int, samples: int,
+                 stream: Optional[torch.cuda.Stream] = None):
+    """S regularly spaced (key, position) samples of keys[:n] (grs_shard_sample)."""
+    sk = torch.empty(samples, dtype=keys.dtype, device=keys.device)
+    sp = torch.empty(samples, dtype=torch.uint32, device=keys.device)
+    check(lib().grs_shard_sample(_ptr(keys), int(n), keys.element_size(), int(samples), _ptr(sk),
+                                 _ptr(sp), _stream_ptr(stream)), "grs_shard_sample")
+    return sk, sp
+
+
+def shard_encode(sorter: RadixSorter, sorted_keys: torch.Tensor, n: int, gathered_keys: torch.Tensor,
+                 gathered_pos: torch.Tensor, nranks: int, rank: int,
+                 stream: Optional[torch.cuda.Stream] = None):
+    """Encode the G buckets of a sorted u32 shard (grs_shard_encode).  Returns (send, sizes):
+    send holds the buckets back to back (u32 words), sizes[2b] / [2b+1] bucket b's keys / words."""
+    if sorted_keys.element_size() != 4 or sorted_keys.numel() < n:
+        raise ValueError("sorted_keys: a u32 device tensor of >= n keys")
+    L = lib()
+    cap = int(L.grs_shard_encode_words_max(int(n), int(nranks)))
+    send = torch.empty(max(cap, 1), dtype=torch.uint32, device=sorted_keys.device)
+    sizes = torch.empty(2 * nranks, dtype=torch.uint32, device=sorted_keys.device)
+    check(L.grs_shard_encode(sorter._h, _ptr(sorted_keys), int(n), _ptr(gathered_keys),
+                             _ptr(gathered_pos), int(nranks), int(rank), _ptr(send), cap,
+                             _ptr(sizes), _stream_ptr(stream)), "grs_shard_encode")
+    return send, sizes
+
+
+def shard_decode_merge(sorter: RadixSorter, recv: torch.Tensor, word_offsets, lens,
+                       out: torch.Tensor, stream: Optional[torch.cuda.Stream] = None) -> int:
+    """Decode the received runs (source p: lens[p] keys at recv[word_offsets[p]:]) and merge them
+    into out (grs_shard_decode_merge); returns the number of keys written."""
+    g = len(lens)
+    wo = (ctypes.c_uint64 * g)(*[int(x) for x in word_offsets])
+    ln = (ctypes.c_uint32 * g)(*[int(x) for x in lens])
+    check(lib().grs_shard_decode_merge(sorter._h, _ptr(recv), g, wo, ln, _ptr(out), out.numel(),
+                                       _stream_ptr(stream)), "grs_shard_decode_merge")
+    return int(sum(int(x) for x in lens))

@@ -158,16 +158,25 @@ grs_status grs_partition_ranges(grs_sorter* s, const void* d_keys, const uint32_
  * The reference has no multi-device path; this is BASELINE config C4's exchange.  Rank r's
  * input is the global range that follows ranks < r; on return rank r holds a contiguous,
  * sorted range of the global stable order, and the ranks' outputs concatenated in rank order
- * are the stable sort of the whole input.  Steps (one stream): regular samples of the shard ->
- * RCCL all-gather -> on-device splitter choice (ties broken by global index) -> grs partition
- * pass into G buckets -> all-gather of the G x G bucket counts -> ONE host synchronisation
- * (the counts) -> grouped ncclSend / ncclRecv of keys and payload -> local grs_sort of the
- * received run (received in source-rank order = global order for equal keys).
+ * are the stable sort of the whole input.  Two exchanges, one stream each call:
+ *  - presorted (u32 keys without payload, when out_capacity >= n_local; the default there
+ *    for G <= 4 ranks, GRS_SHARDED_EXCHANGE=presorted forces it for more):
+ *    local grs_sort of the shard into d_keys_out -> regular samples of the sorted shard ->
+ *    RCCL all-gather -> on-device splitters (ties broken by global index) -> bucket bounds in
+ *    the sorted shard -> each bucket encoded as 256-key blocks of bit-packed deltas (about one
+ *    byte per uniform key at 8 ranks) -> all-gather of the G x 2G (keys, words) matrix -> ONE
+ *    host synchronisation -> grouped ncclSend / ncclRecv of the encoded words -> decode ->
+ *    2-way merge rounds of the G received runs into d_keys_out (ties: source-rank order).
+ *  - partition-first (payload, u64 keys, or G > 4; GRS_SHARDED_EXCHANGE=partition forces it):
+ *    samples
+ *    -> splitters -> grs partition pass into G buckets -> all-gather of the G x G bucket
+ *    counts -> ONE host synchronisation -> grouped ncclSend / ncclRecv of keys and payload ->
+ *    local grs_sort of the received run (source-rank order = global order for equal keys).
  * nccl_comm: an initialised ncclComm_t (any RCCL communicator of G <= 16 ranks, one rank per
  * device); the sorter needs capacity >= max(n_local, *n_out) and out_capacity >= *n_out
- * (GRS_ECAPACITY otherwise, detected before any data moves).  Returns after enqueuing the local
- * sort (check it with grs_stream_check_error); look-back timeouts of the partition are reported
- * by the call itself. */
+ * (GRS_ECAPACITY otherwise, detected before any data moves).  Returns after enqueuing the last
+ * step (check it with grs_stream_check_error); look-back timeouts before the host
+ * synchronisation are reported by the call itself. */
 grs_status grs_sort_sharded(grs_sorter* s, const void* d_keys_in, const uint32_t* d_vals_in,
                             size_t n_local, void* d_keys_out, uint32_t* d_vals_out,
                             size_t out_capacity, size_t* n_out, void* nccl_comm, void* stream);
@@ -194,6 +203,29 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
                                uint64_t* send_off, uint64_t* recv_off, uint64_t* n_out);
 /* Samples per rank of the sharded sort for nranks ranks (min(1024, 8192 / nranks)). */
 int grs_shard_samples_per_rank(int nranks);
+
+/* The presorted exchange as transport-independent steps (u32 keys, no payload), for hosts
+ * that move the bytes themselves (MPI, gloo, a simulated exchange on one device).  Rank r:
+ *   1. sort its shard (grs_sort);
+ *   2. grs_shard_sample: S = grs_shard_samples_per_rank(G) samples of the SORTED shard;
+ *      all-gather them rank-major (keys and positions, G*S each);
+ *   3. grs_shard_encode: splitters, bucket bounds, encoding; d_send gets the G buckets back to
+ *      back (d_send_capacity_words >= grs_shard_encode_words_max(n, G)); d_sizes (device, 2G
+ *      u32) gets bucket b's key count [2b] and encoded words [2b+1];
+ *   4. all-gather the sizes; send bucket p's words to rank p, receive source p's words;
+ *   5. grs_shard_decode_merge: recv_word_offsets[p] / recv_keys[p] (host arrays) locate source
+ *      p's words in d_recv and its key count; writes the merged range to d_keys_out.
+ * The sorter needs capacity >= the received total (its ping-pong buffer is the merge scratch). */
+grs_status grs_shard_sample(const void* d_keys, size_t n, int key_bytes, int samples,
+                            void* d_sample_keys, uint32_t* d_sample_pos, void* stream);
+size_t grs_shard_encode_words_max(size_t n, int nranks);
+grs_status grs_shard_encode(grs_sorter* s, const uint32_t* d_sorted, size_t n,
+                            const uint32_t* d_gathered_keys, const uint32_t* d_gathered_pos,
+                            int nranks, int rank, uint32_t* d_send, size_t send_capacity_words,
+                            uint32_t* d_sizes, void* stream);
+grs_status grs_shard_decode_merge(grs_sorter* s, const uint32_t* d_recv, int nranks,
+                                  const uint64_t* recv_word_offsets, const uint32_t* recv_keys,
+                                  uint32_t* d_keys_out, size_t out_capacity, void* stream);
 
 /* ---- boundary helpers (reference K1/K5/verification, synthetic data) ---- */
 

@@ -13,6 +13,12 @@ with gloo collectives in place of RCCL and numpy restatements of the three devic
 
 The splitter and plan arithmetic are the product's own (libgrs host twins, the same inline
 functions the device code uses); nothing here is imported by gpuradixsort_amd.
+
+sim_presorted_sort follows the presorted exchange (run_sharded_presorted, grs_codec.hpp) for
+u32 keys without payload: local sort, samples of the SORTED shard, the same splitters, bucket
+bounds = clamp(threshold, lower_bound, upper_bound) of each splitter key (grs_shard_bounds),
+exchange of the bucket runs in source-rank order, merge.  The encoding of the runs is exercised
+on the GPU (tests/test_gpu_presorted.py); here the runs travel as plain keys.
 """
 from __future__ import annotations
 
@@ -99,3 +105,41 @@ def sim_sharded_sort(keys: np.ndarray, vals, group=None):
         out_v = rv.numpy().view(np.uint32)
     p2 = np.argsort(out_k, kind="stable")
     return out_k[p2], (out_v[p2] if out_v is not None else None), mat.reshape(G, G)
+
+
+def _splitters(sk, sp, G, me, S, kb, dtype, group=None):
+    L, check = _lib()
+    ak = _all_gather_np(sk, G, group)
+    ap = _all_gather_np(sp, G, group)
+    order = np.lexsort((np.arange(G * S), ak))
+    sorted_k = np.ascontiguousarray(ak[order])
+    sorted_j = np.ascontiguousarray(order.astype(np.uint32))
+    spl = np.zeros(max(G - 1, 1), dtype)
+    th = np.zeros(max(G - 1, 1), np.uint32)
+    check(L.grs_shard_splitters_host(sorted_k.ctypes.data, sorted_j.ctypes.data, ap.ctypes.data,
+                                     kb, G, S, me, spl.ctypes.data, th.ctypes.data),
+          "grs_shard_splitters_host")
+    return spl[:G - 1], th[:G - 1]
+
+
+def sim_presorted_sort(keys: np.ndarray, group=None):
+    """Returns (keys_out, bucket-size matrix) of this rank (u32 keys, presorted exchange)."""
+    L, _ = _lib()
+    G, me = dist.get_world_size(group), dist.get_rank(group)
+    S = int(L.grs_shard_samples_per_rank(G))
+    srt = np.sort(keys, kind="stable")
+    sk, sp = _samples(srt, S)
+    spl, th = _splitters(sk, sp, G, me, S, 4, keys.dtype, group)
+    lb = np.searchsorted(srt, spl, side="left")
+    ub = np.searchsorted(srt, spl, side="right")
+    bounds = np.concatenate([[0], np.clip(th.astype(np.int64), lb, ub), [srt.size]]).astype(np.int64)
+    assert np.all(np.diff(bounds) >= 0)
+    cnt = np.diff(bounds).astype(np.uint32)
+    mat = np.ascontiguousarray(_all_gather_np(cnt, G, group)).reshape(G, G)
+    rc = [int(x) for x in mat[:, me]]
+    rk = torch.empty(sum(rc), dtype=torch.int32)
+    dist.all_to_all_single(rk, torch.from_numpy(srt.view(np.int32).copy()), output_split_sizes=rc,
+                           input_split_sizes=[int(x) for x in cnt], group=group)
+    runs = np.split(rk.numpy().view(np.uint32), np.cumsum(rc)[:-1])
+    assert all(np.all(r[1:] >= r[:-1]) for r in runs)   # every received run is sorted
+    return np.sort(np.concatenate(runs), kind="stable"), mat

@@ -33,7 +33,7 @@ def world1(gpu):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("path", ["general", "general_contig", "one_rank"])
+@pytest.mark.parametrize("path", ["general", "general_contig", "general_partition", "one_rank"])
 @pytest.mark.parametrize("key_bits,pairs,dist_name", [(32, False, "uniform"), (32, True, "ties"),
                                                       (64, True, "uniform"), (64, False, "ties"),
                                                       (32, True, "all_equal")])
@@ -41,14 +41,18 @@ def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pair
     """path "general": GRS_SHARDED=general makes the one-rank call take the G-rank path
     (samples, all-gathers, device splitters, partition into per-bucket regions of the send
     buffer, bucket sizes from the look-back, count matrix, host sync, grouped send/recv with
-    the self copy, local sort); "general_contig": the same with the bucket histogram and
-    contiguous send buckets (GRS_SHARDED_SEND=contig); "one_rank": the copy + local sort."""
+    the self copy, local sort) -- u32 keys without payload take the presorted exchange there
+    (local sort, encode, exchange of encoded words, decode + merge) unless "general_partition"
+    forces the partition-first one; "general_contig": partition-first with the bucket histogram
+    and contiguous send buckets (GRS_SHARDED_SEND=contig); "one_rank": the copy + local sort."""
     from gpuradixsort_amd.sharded import ShardedSorter
 
     if path.startswith("general"):
         monkeypatch.setenv("GRS_SHARDED", "general")
     if path == "general_contig":
         monkeypatch.setenv("GRS_SHARDED_SEND", "contig")
+    if path in ("general_contig", "general_partition"):
+        monkeypatch.setenv("GRS_SHARDED_EXCHANGE", "partition")
 
     rng = np.random.default_rng(key_bits + pairs)
     dt = np.uint32 if key_bits == 32 else np.uint64

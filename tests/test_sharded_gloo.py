@@ -89,6 +89,41 @@ def test_sharded_sort_equals_global_stable_sort(tmp_path, world, n_local, key_bi
     assert mat.sum() == n_local * world
 
 
+def _worker_presorted(rank, world, port, n_local, dist_name, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sharded_sim
+
+    allk = _input(dist_name, n_local * world, 32)
+    ko, mat = sharded_sim.sim_presorted_sort(allk[rank * n_local:(rank + 1) * n_local].copy())
+    np.save(os.path.join(out_dir, f"k{rank}.npy"), ko)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "all.npy"), allk)
+        np.save(os.path.join(out_dir, "mat.npy"), mat)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_local,dist_name", [
+    (2, 5000, "uniform"), (3, 3001, "skewed"), (4, 2500, "all_equal"), (4, 20000, "few_unique"),
+    (2, 0, "uniform"),
+])
+def test_presorted_exchange_equals_sort(tmp_path, world, n_local, dist_name):
+    """The presorted exchange's orchestration (u32 keys): sorted-shard samples, the product's
+    splitters, clamp bounds, source-order runs; sorted and balanced."""
+    port = _free_port()
+    mp.spawn(_worker_presorted, args=(world, port, n_local, dist_name, str(tmp_path)),
+             nprocs=world, join=True)
+    allk = np.load(tmp_path / "all.npy")
+    outs = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
+    assert np.array_equal(np.concatenate(outs), np.sort(allk))
+    if n_local and dist_name in ("all_equal", "few_unique"):
+        sizes = np.array([o.size for o in outs], np.float64)
+        assert sizes.max() / sizes.mean() <= 1.1, sizes
+    assert np.load(tmp_path / "mat.npy").sum() == n_local * world
+
+
 def test_host_twins_validate_arguments():
     import ctypes
 

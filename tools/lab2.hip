@@ -253,6 +253,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
                        (const grs::RadixDigit<uint32_t>*)nullptr);                             \
   } break;
     V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
+    V(1024, 32, 1, 8)
 #undef V
     default:
       return -1;

@@ -164,7 +164,7 @@ def main():
         print(f"{':'.join(str(x) for x in v):28s} median {med:8.4f} ms  min {mn:8.4f}  "
               f"{alg / med / 1e6:8.1f} GB/s", flush=True)
     for v in variants:
-        stamped = (v[0] in ("v4", "r4") and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v6" and v[6] & 8)
+        stamped = (v[0] in ("v4", "r4", "r6") and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v6" and v[6] & 8)
         if not stamped:
             continue
         err.zero_()
@@ -175,7 +175,7 @@ def main():
         torch.cuda.synchronize()
         tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
-        if v[0] in ("v4", "v6", "r4"):
+        if v[0] in ("v4", "v6", "r4", "r6"):
             m = a_[:, :6].mean(0)
             d = np.diff(np.concatenate([[0.0], m]))
             names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
