@@ -9,8 +9,10 @@ buffer (generated before the timed region), so nothing is restored or skipped in
 
 Default workload: BASELINE config C4 itself, 2^30 uniform uint32 keys in total, 8-bit digits,
 STRONG scaling: at N = 1 one MI355X sorts all 2^30 keys in one call; at N > 1 rank r holds
-2^30 / N keys and the sort is grs_sort_sharded (range partition, one RCCL all-to-all over
-xGMI, local sort; gpuradixsort_amd/sharded.py).  `value` = 2^30 keys x steps / wall time.
+2^30 / N keys and the sort is grs_sort_sharded (gpuradixsort_amd/sharded.py): up to 4 ranks
+the presorted exchange (local sort, bit-packed delta encoding of the buckets, one RCCL send /
+recv per peer over xGMI, decode, merge), beyond that the partition-first one (range partition,
+one RCCL all-to-all, local sort).  `value` = 2^30 keys x steps / wall time.
 
 Rank 0 prints ONE JSON line with the driver contract plus:
   roofline      dominant kernel (the pass: grs_onesweep_v4, or v6 on small grids): algorithmic bytes per launch
@@ -41,7 +43,8 @@ CONFIGS = {
     # name: (config_id, total keys (c4: strong scaling) or keys per GPU, key_bits, pairs,
     #        radix_bits, description)
     "c4": (4, 1 << 30, 32, False, 8, "C4: 2^30 uint32 keys in total (strong scaling: 2^30 / N per "
-                                     "GPU), 8-bit LSD; N > 1: range partition + one RCCL all-to-all"),
+                                     "GPU), 8-bit LSD; N > 1: one RCCL all-to-all over xGMI "
+                                     "(config.exchange)"),
     "c2": (2, 1 << 24, 32, False, 4, "C2: 16M uint32 keys, 4-bit-digit LSD"),
     "c3": (3, 1 << 28, 32, True, 8, "C3: 256M uint32 key + uint32 payload, stable"),
     "c5": (5, 1 << 28, 64, False, 8, "C5: 256M uint64 keys, 8 x 8-bit passes"),
@@ -189,7 +192,14 @@ def main():
     mean_pass_ms = sum(pass_ms) / len(pass_ms)
     hist_ms = sum(t["hist_ms"] for t in tims) / len(tims)
     sort_ms = sum(t["total_ms"] for t in tims) / len(tims)
-    n_sorted_local = sorter.last_n_out if world > 1 else n_local
+    # the exchange grs_sort_sharded takes (include/grs.h): presorted = local sort of the shard
+    # first, then the encoded exchange and a merge; partition-first = local sort of the received run
+    exchange = None
+    if world > 1:
+        forced = os.environ.get("GRS_SHARDED_EXCHANGE", "")
+        presorted = kb == 32 and not pairs and (forced == "presorted" or (forced != "partition" and world <= 4))
+        exchange = "presorted" if presorted else "partition-first"
+    n_sorted_local = sorter.last_n_out if exchange == "partition-first" else n_local
     kernel_name = (sorter.sorter if world > 1 else sorter).pass_kernel_for(n_sorted_local)
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
@@ -234,6 +244,7 @@ def main():
         }
         if world > 1:
             out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
+            out["config"]["exchange"] = exchange
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

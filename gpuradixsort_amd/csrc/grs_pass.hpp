@@ -216,8 +216,9 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
 // and every thread passed a barrier since it was written and since the previous tile's last
 // LDS access.  Leaves sm.cnt dirty.
 // PF (persistent workgroups, grs_onesweep_v6): thread 0 draws the next ticket during the
-// ranking; after the reorder has moved this tile into LDS, the next tile's loads are issued
-// into key/val — their latency hides behind the look-back and the stores.  Returns the next
+// ranking; after the reorder has moved this tile into LDS (two-round tiles: once the last
+// round sits in LDS), the next tile's loads are issued into key/val — their latency hides
+// behind the look-back and the stores.  Returns the next
 // tile (>= tiles: none); without PF returns tiles.
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, bool PF = false,
           typename DigitF>
@@ -238,8 +239,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   constexpr int LITEMS = ITEMS / ROUNDS;   // store-loop items per round
   static_assert(LITEMS * ROUNDS == ITEMS, "ITEMS divisible by the rounds");
   static_assert(!C16 || TILE < 65536, "16-bit tile positions");
-  static_assert(ROUNDS == 1 || TILE < 65536, "two-round reorder keeps 16-bit positions");
-  static_assert(ROUNDS == 1 || !PF, "the prefetch reuses the registers round 2 still needs");
+  static_assert(ROUNDS == 1 || TILE <= 65536, "two-round reorder keeps 16-bit positions");
   uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
   constexpr bool IDX = DigitF::kIndexed;
   auto cnt_ld = [&](uint32_t i) -> uint32_t { if constexpr (C16) return c16[i]; else return sm.cnt[i]; };
@@ -417,7 +417,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t);
   }
   uint32_t next = tiles;
-  if constexpr (PF) {
+  if constexpr (PF && ROUNDS == 1) {   // two rounds: after round 2 sits in LDS (store phase)
     next = __builtin_amdgcn_readfirstlane(sm.next);
     if (next < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
@@ -461,6 +461,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         }
       }
       lds_barrier();
+      if constexpr (PF) {
+        // the last round's keys are in LDS: the registers take the next tile's loads, which
+        // fly behind this round's stores
+        if (rr == ROUNDS - 1) {
+          next = __builtin_amdgcn_readfirstlane(sm.next);
+          if (next < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
+        }
+      }
     }
     const uint32_t roff = static_cast<uint32_t>(rr * LTILE);
     if (valid == static_cast<uint32_t>(TILE)) {

@@ -229,6 +229,8 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
   } break;
     V(32, 0, 1024, 36, 1, 256) V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 288)
     V(64, 1, 1024, 11, 1, 256) V(32, 1, 1024, 17, 1, 256) V(64, 0, 1024, 17, 1, 256)
+    V(32, 0, 768, 64, 1, 1040) V(32, 0, 768, 64, 1, 1048) V(32, 0, 768, 64, 1, 1024)
+    V(32, 0, 768, 60, 1, 1040)
 #undef V
     default:
       return -1;
@@ -278,6 +280,8 @@ int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* ou
   } break;
     V(1024, 32, 1, 0) V(1024, 32, 1, 16) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(1024, 32, 1, 8)
     V(1024, 32, 1, 24) V(1024, 32, 1, 64) V(1024, 32, 1, 72)
+    V(1024, 64, 1, 1024) V(1024, 64, 1, 1040) V(1024, 64, 1, 1032) V(768, 84, 1, 1024)
+    V(512, 128, 1, 1024) V(512, 128, 1, 1040) V(512, 128, 1, 1032)
 #undef V
     default:
       return -1;
