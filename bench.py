@@ -192,13 +192,13 @@ def main():
     mean_pass_ms = sum(pass_ms) / len(pass_ms)
     hist_ms = sum(t["hist_ms"] for t in tims) / len(tims)
     sort_ms = sum(t["total_ms"] for t in tims) / len(tims)
-    # the exchange grs_sort_sharded takes (include/grs.h): presorted = local sort of the shard
-    # first, then the encoded exchange and a merge; partition-first = local sort of the received run
-    exchange = None
+    # the exchange grs_sort_sharded took (include/grs.h): presorted = local sort of the shard
+    # first, then the encoded exchange and a merge; partition-first = local sort of the received
+    # run.  Its phases of the last step, with the xGMI bytes and rate of this rank
+    exchange, xt = None, None
     if world > 1:
-        forced = os.environ.get("GRS_SHARDED_EXCHANGE", "")
-        presorted = kb == 32 and not pairs and (forced == "presorted" or (forced != "partition" and world <= 4))
-        exchange = "presorted" if presorted else "partition-first"
+        xt = sorter.exchange_timing()
+        exchange = xt["exchange"]
     n_sorted_local = sorter.last_n_out if exchange == "partition-first" else n_local
     kernel_name = (sorter.sorter if world > 1 else sorter).pass_kernel_for(n_sorted_local)
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
@@ -245,6 +245,12 @@ def main():
         if world > 1:
             out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
             out["config"]["exchange"] = exchange
+            xms = max(xt["exchange_ms"], 1e-6)
+            out["exchange_rank0"] = {
+                "before_ms": round(xt["before_ms"], 4), "exchange_ms": round(xt["exchange_ms"], 4),
+                "after_ms": round(xt["after_ms"], 4), "bytes_sent": xt["bytes_sent"],
+                "bytes_received": xt["bytes_received"],
+                "xgmi_GBps_sent": round(xt["bytes_sent"] / xms / 1e6, 1)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -38,6 +38,12 @@ class grs_timing(ctypes.Structure):
                 ("pass_ms", c_float * 16), ("copy_ms", c_float)]
 
 
+class grs_sharded_timing(ctypes.Structure):
+    _fields_ = [("total_ms", c_float), ("before_ms", c_float), ("exchange_ms", c_float),
+                ("after_ms", c_float), ("bytes_sent", c_uint64), ("bytes_received", c_uint64),
+                ("presorted", c_int)]
+
+
 class grs_key_extract(ctypes.Structure):
     _fields_ = [("kind", c_int), ("offset", c_uint32), ("transform", c_int),
                 ("lo", c_float * 3), ("hi", c_float * 3)]
@@ -69,6 +75,7 @@ SIGNATURES = [
                                      c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("grs_sort_sharded", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                  c_size_t, POINTER(c_size_t), c_void_p, c_void_p]),
+    ("grs_sharded_last_timing", c_int, [c_void_p, POINTER(grs_sharded_timing)]),
     ("grs_rccl_unique_id", c_int, [c_void_p]),
     ("grs_rccl_comm_init", c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int]),
     ("grs_rccl_comm_destroy", None, [c_void_p]),

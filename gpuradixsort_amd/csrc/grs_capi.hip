@@ -271,6 +271,12 @@ struct grs_sorter {
   void* codec_buf = nullptr;       // presorted exchange: plan, block sizes / offsets, scan, co-ranks
   size_t codec_bytes = 0;
   int sharded_exchange = 0;        // GRS_SHARDED_EXCHANGE: 0 auto, 1 partition-first, 2 presorted
+  // last grs_sort_sharded call, with profiling on: events at call start / exchange start /
+  // exchange end / call end, and the bytes that crossed the links (self part excluded)
+  hipEvent_t xev[4] = {};
+  bool xev_recorded = false;
+  uint64_t x_sent = 0, x_recv = 0;
+  int x_presorted = 0;
   // tuning knobs read from the environment at grs_create (A/B measurements on one box)
   int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the round-1 histogram grid
   int hist_variant = 2;            // GRS_HIST: 1 = grs_upfront_hist, 2 = grs_upfront_hist2
@@ -323,6 +329,8 @@ void grs_destroy(grs_sorter* s) {
   if (s->codec_buf) (void)hipFree(s->codec_buf);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
+  for (hipEvent_t e : s->xev)
+    if (e) (void)hipEventDestroy(e);
   delete[] s->ev;
   delete[] s->info;
   (void)hipSetDevice(prev);
@@ -482,7 +490,11 @@ grs_status grs_set_profiling(grs_sorter* s, int ring) {
     for (int i = 0; i < ring * grs_sorter::EV_PER_CALL && st == GRS_OK; ++i)
       if (hipEventCreate(&s->ev[i]) != hipSuccess)
         st = set_err(GRS_EHIP, "grs_set_profiling: hipEventCreate failed");
+    for (hipEvent_t& e : s->xev)
+      if (st == GRS_OK && !e && hipEventCreate(&e) != hipSuccess)
+        st = set_err(GRS_EHIP, "grs_set_profiling: hipEventCreate failed");
   }
+  s->xev_recorded = false;
   (void)hipSetDevice(prev);
   return st;
 }
@@ -1253,6 +1265,12 @@ void shard_plan(const uint32_t* mat, int g, int me, uint64_t* soff, uint64_t* ro
 template <typename K>
 constexpr ncclDataType_t nccl_type() { return sizeof(K) == 4 ? ncclUint32 : ncclUint64; }
 
+// Exchange timing of grs_sort_sharded (profiling on): event k of the call.
+grs_status xmark(grs_sorter* s, int k, hipStream_t st) {
+  if (s->ring > 0 && s->xev[k]) GRS_HIP(hipEventRecord(s->xev[k], st));
+  return GRS_OK;
+}
+
 template <typename K, bool PAIRS, int N>
 grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uint32_t n, K* out_k,
                          uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
@@ -1288,6 +1306,7 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   uint32_t* mat = reinterpret_cast<uint32_t*>(b);    b += al(static_cast<size_t>(g) * g * 4);
   Dig* dig = reinterpret_cast<Dig*>(b);
 
+  if (xmark(s, 0, st) != GRS_OK) return GRS_EHIP;
   // 1-2. samples, all-gathered (rank-major)
   hipLaunchKernelGGL((grs::grs_shard_samples<K>), dim3((S + 255) / 256), dim3(256), 0, st, keys, n,
                      S, sk, sp);
@@ -1345,6 +1364,7 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
     return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
                                       " items) exceeds out_capacity or the sorter capacity");
   // 7. exchange: keys and payload in one group; the self part is a device copy
+  if (xmark(s, 1, st) != GRS_OK) return GRS_EHIP;
   GRS_RCCL(ncclGroupStart());
   for (int p = 0; p < g; ++p) {
     if (p == me) continue;
@@ -1363,9 +1383,23 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
       GRS_HIP(hipMemcpyAsync(out_v + roff[me], send_v + soff[me], self * 4,
                              hipMemcpyDeviceToDevice, st));
   }
+  if (xmark(s, 2, st) != GRS_OK) return GRS_EHIP;
   *n_out = static_cast<size_t>(total);
   // 8. local stable sort of the received run (source-rank order = global order for ties)
-  return grs_sort(s, out_k, out_v, static_cast<size_t>(total), st);
+  const grs_status rs = grs_sort(s, out_k, out_v, static_cast<size_t>(total), st);
+  if (rs != GRS_OK || xmark(s, 3, st) != GRS_OK) return rs != GRS_OK ? rs : GRS_EHIP;
+  uint64_t sent = 0, recvd = 0;
+  for (int p = 0; p < g; ++p) {
+    if (p == me) continue;
+    sent += s->shard_host[me * g + p];
+    recvd += s->shard_host[p * g + me];
+  }
+  const uint64_t ib = sizeof(K) + (PAIRS ? 4 : 0);
+  s->xev_recorded = s->ring > 0;
+  s->x_sent = sent * ib;
+  s->x_recv = recvd * ib;
+  s->x_presorted = 0;
+  return GRS_OK;
 }
 
 // ---- presorted exchange (grs_codec.hpp): sort, encode the buckets, exchange, decode, merge --
@@ -1533,6 +1567,7 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
     return r;
   uint32_t* send = static_cast<uint32_t*>(s->xbuf);
 
+  if ((r = xmark(s, 0, st)) != GRS_OK) return r;
   // 1. local sort, out of place: the sorted shard lands in out_k
   if (n > 0 && (r = run_sort<uint32_t, false, 8>(s, out_k, nullptr, n, 0, 32, st, keys)) != GRS_OK)
     return r;
@@ -1576,6 +1611,7 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
     return r;
   uint32_t* recv = static_cast<uint32_t*>(s->xrbuf);
   // 6. exchange of encoded words; the self part is a device copy
+  if ((r = xmark(s, 1, st)) != GRS_OK) return r;
   GRS_RCCL(ncclGroupStart());
   for (int p = 0; p < g; ++p) {
     if (p == me) continue;
@@ -1587,8 +1623,14 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   const size_t self = h[me * 2 * g + 2 * me + 1];
   if (self)
     GRS_HIP(hipMemcpyAsync(recv + roff[me], send + soff[me], 4 * self, hipMemcpyDeviceToDevice, st));
+  if ((r = xmark(s, 2, st)) != GRS_OK) return r;
   // 7. decode + merge into out_k
   if ((r = codec_decode_merge(s, recv, g, roff, lens, out_k, total, cs, st)) != GRS_OK) return r;
+  if ((r = xmark(s, 3, st)) != GRS_OK) return r;
+  s->xev_recorded = s->ring > 0;
+  s->x_sent = 4 * (so - h[me * 2 * g + 2 * me + 1]);
+  s->x_recv = 4 * (ro - h[me * 2 * g + 2 * me + 1]);
+  s->x_presorted = 1;
   *n_out = static_cast<size_t>(total);
   return GRS_OK;
 }
@@ -1759,6 +1801,27 @@ grs_status grs_shard_decode_merge(grs_sorter* s, const uint32_t* d_recv, int nra
     r = codec_decode_merge(s, d_recv, nranks, recv_word_offsets, recv_keys, d_keys_out, total, cs, st);
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
+}
+
+grs_status grs_sharded_last_timing(grs_sorter* s, grs_sharded_timing* out) {
+  if (!s || !out) return set_err(GRS_EINVAL, "grs_sharded_last_timing: NULL argument");
+  std::memset(out, 0, sizeof(*out));
+  if (!s->xev_recorded)
+    return set_err(GRS_EINVAL, "grs_sharded_last_timing: no profiled multi-rank grs_sort_sharded call");
+  GRS_HIP(hipEventSynchronize(s->xev[3]));
+  float ms = 0;
+  GRS_HIP(hipEventElapsedTime(&ms, s->xev[0], s->xev[3]));
+  out->total_ms = ms;
+  GRS_HIP(hipEventElapsedTime(&ms, s->xev[0], s->xev[1]));
+  out->before_ms = ms;
+  GRS_HIP(hipEventElapsedTime(&ms, s->xev[1], s->xev[2]));
+  out->exchange_ms = ms;
+  GRS_HIP(hipEventElapsedTime(&ms, s->xev[2], s->xev[3]));
+  out->after_ms = ms;
+  out->bytes_sent = s->x_sent;
+  out->bytes_received = s->x_recv;
+  out->presorted = s->x_presorted;
+  return GRS_OK;
 }
 
 grs_status grs_rccl_unique_id(void* id_out) {

@@ -129,6 +129,18 @@ class ShardedSorter:
     def timing(self, k: int = 0) -> dict:
         return self.sorter.timing(k)
 
+    def exchange_timing(self) -> dict:
+        """Phases of the last multi-rank sort() (profiling on; grs_sharded_last_timing): ms
+        before / of / after the exchange and the bytes that crossed the links."""
+        from ._lib import grs_sharded_timing
+
+        t = grs_sharded_timing()
+        check(lib().grs_sharded_last_timing(self.sorter._h, ctypes.byref(t)), "grs_sharded_last_timing")
+        return {"total_ms": t.total_ms, "before_ms": t.before_ms, "exchange_ms": t.exchange_ms,
+                "after_ms": t.after_ms, "bytes_sent": int(t.bytes_sent),
+                "bytes_received": int(t.bytes_received),
+                "exchange": "presorted" if t.presorted else "partition-first"}
+
     def count_inversions(self) -> int:
         from .sorter import count_inversions
 

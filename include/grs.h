@@ -181,6 +181,19 @@ grs_status grs_sort_sharded(grs_sorter* s, const void* d_keys_in, const uint32_t
                             size_t n_local, void* d_keys_out, uint32_t* d_vals_out,
                             size_t out_capacity, size_t* n_out, void* nccl_comm, void* stream);
 
+/* Phases of the last multi-rank grs_sort_sharded call on this sorter (needs grs_set_profiling
+ * > 0; synchronises): before_ms = samples .. the host synchronisation (partition-first: the
+ * partition; presorted: local sort + encode), exchange_ms = the grouped send / recv and the self
+ * copy, after_ms = local sort (partition-first) or decode + merge (presorted).  bytes_* count
+ * what crossed the links (the self part excluded); bytes_sent / exchange_ms is the xGMI rate
+ * of this rank. */
+typedef struct grs_sharded_timing {
+  float total_ms, before_ms, exchange_ms, after_ms;
+  uint64_t bytes_sent, bytes_received;
+  int presorted;
+} grs_sharded_timing;
+grs_status grs_sharded_last_timing(grs_sorter* s, grs_sharded_timing* out);
+
 /* RCCL communicator helpers for callers without their own RCCL binding (ctypes, tests):
  * rank 0 creates the id (GRS_RCCL_ID_BYTES bytes), every rank passes it to comm_init. */
 #define GRS_RCCL_ID_BYTES 128

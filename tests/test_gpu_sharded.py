@@ -73,6 +73,14 @@ def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pair
         if pairs:
             assert np.array_equal(vo.cpu().numpy(), perm)
     assert s.count_inversions() == 0
+    if path.startswith("general"):     # exchange phases of the last call (profiling on)
+        s.set_profiling(2)
+        s.sort(k.clone(), v.clone() if pairs else None)
+        xt = s.exchange_timing()
+        assert xt["bytes_sent"] == 0 and xt["bytes_received"] == 0     # one rank: self copy only
+        assert xt["total_ms"] >= xt["exchange_ms"] >= 0.0
+        assert xt["exchange"] == ("presorted" if (key_bits == 32 and not pairs and path == "general")
+                                  else "partition-first")
     s.sorter.close()
 
 
