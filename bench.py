@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--traffic-json", default="", help="tools/bench_pmc.py output of this workload")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--sharded", action="store_true",
+                    help="N = 1 through grs_sort_sharded's multi-rank code path (GRS_SHARDED="
+                         "general, a one-rank RCCL communicator): a one-GPU rehearsal of N > 1")
     ap.add_argument("--pool-gib", type=float, default=96.0,
                     help="HBM budget for the distinct per-step input buffers")
     return ap.parse_args()
@@ -112,6 +115,15 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    sharded = world > 1 or a.sharded
+    if sharded and world == 1:
+        import socket
+
+        os.environ["GRS_SHARDED"] = "general"
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
 
     import gpuradixsort_amd as grs
 
@@ -137,7 +149,7 @@ def main():
             grs.iota_u32(v, rank * n_local)
             vals_pool.append(v)
 
-    if world == 1:
+    if not sharded:
         sorter = grs.RadixSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb)
         sorter.set_profiling(max(1, a.steps))
 
@@ -162,7 +174,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
+        if sharded:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -181,10 +193,10 @@ def main():
         elapsed = float(t.item())
 
     # look-back timeouts of the timed steps surface here (error word; raises GrsError)
-    (sorter.sorter if world > 1 else sorter).check_error()
+    (sorter.sorter if sharded else sorter).check_error()
     # correctness of the last timed step (cheap property: sortedness on device)
     last = (a.warmup + a.steps - 1) % pool
-    inversions = sorter.count_inversions() if world > 1 else grs.count_inversions(keys_pool[last])
+    inversions = sorter.count_inversions() if sharded else grs.count_inversions(keys_pool[last])
 
     # per-phase GPU times over the timed steps (hipEvents on the sort's stream)
     tims = [sorter.timing(k) for k in range(min(a.steps, pool))]
@@ -196,11 +208,11 @@ def main():
     # first, then the encoded exchange and a merge; partition-first = local sort of the received
     # run.  Its phases of the last step, with the xGMI bytes and rate of this rank
     exchange, xt = None, None
-    if world > 1:
+    if sharded:
         xt = sorter.exchange_timing()
         exchange = xt["exchange"]
     n_sorted_local = sorter.last_n_out if exchange == "partition-first" else n_local
-    kernel_name = (sorter.sorter if world > 1 else sorter).pass_kernel_for(n_sorted_local)
+    kernel_name = (sorter.sorter if sharded else sorter).pass_kernel_for(n_sorted_local)
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
 
@@ -242,7 +254,7 @@ def main():
                           "sort_total_gpu": round(sort_ms, 5)},
             "check": {"inversions_last_step": inversions},
         }
-        if world > 1:
+        if sharded:
             out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
             out["config"]["exchange"] = exchange
             xms = max(xt["exchange_ms"], 1e-6)
@@ -252,7 +264,7 @@ def main():
                 "bytes_received": xt["bytes_received"],
                 "xgmi_GBps_sent": round(xt["bytes_sent"] / xms / 1e6, 1)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 
