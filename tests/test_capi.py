@@ -85,3 +85,23 @@ def test_extension_entry_points_validate_without_a_device():
     assert L.grs_exclusive_scan_u32(fake, fake, 100, None, fake, 4, None) == _lib.GRS_EINVAL
     # segmented sort: a sorter is required
     assert L.grs_sort_segmented(None, None, None, 10, None, 1, None) == _lib.GRS_EINVAL
+
+
+def test_presorted_exchange_steps_validate_without_a_device():
+    """The presorted exchange's step entry points reject bad arguments before any HIP call."""
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    fake = ctypes.c_void_p(1 << 20)   # never dereferenced: validation fails first
+    # bound of the encoded words: n keys + a 3-word directory entry per 256-key block and bucket
+    assert L.grs_shard_encode_words_max(0, 8) == 3 * 8
+    assert L.grs_shard_encode_words_max(1 << 20, 8) == (1 << 20) + 3 * ((1 << 20) // 256 + 8)
+    assert L.grs_shard_sample(fake, 10, 2, 4, fake, fake, None) == _lib.GRS_EINVAL      # key bytes
+    assert L.grs_shard_sample(fake, 10, 4, 0, fake, fake, None) == _lib.GRS_EINVAL      # no samples
+    assert L.grs_shard_sample(None, 10, 4, 4, fake, fake, None) == _lib.GRS_EINVAL      # NULL keys
+    assert L.grs_shard_encode(None, fake, 10, fake, fake, 2, 0, fake, 1 << 20, fake, None) == _lib.GRS_EINVAL
+    wo = (ctypes.c_uint64 * 2)()
+    ln = (ctypes.c_uint32 * 2)()
+    assert L.grs_shard_decode_merge(None, fake, 2, wo, ln, fake, 10, None) == _lib.GRS_EINVAL
+    t = _lib.grs_sharded_timing()
+    assert L.grs_sharded_last_timing(None, ctypes.byref(t)) == _lib.GRS_EINVAL

@@ -117,3 +117,52 @@ def test_presorted_encoding_size(gpu):
     assert np.array_equal(np.concatenate(outs), np.sort(np.concatenate(shards)))
     bytes_per_key = 4 * words / (G * n_local)
     assert 1.8 < bytes_per_key < 2.1, bytes_per_key
+
+
+def test_presorted_steps_reject_short_buffers(gpu):
+    import ctypes
+
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd import _lib
+
+    L = _lib.lib()
+    s = grs.RadixSorter(1000, key_bits=32, device=gpu.index)
+    k = torch.zeros(1000, dtype=torch.uint32, device=gpu)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    # send buffer below grs_shard_encode_words_max
+    rc = L.grs_shard_encode(s._h, P(k), 1000, P(k), P(k), 2, 0, P(k), 100, P(k), None)
+    assert rc == _lib.GRS_ECAPACITY
+    # received keys above the sorter's capacity
+    wo = (ctypes.c_uint64 * 2)(0, 0)
+    ln = (ctypes.c_uint32 * 2)(800, 800)
+    assert L.grs_shard_decode_merge(s._h, P(k), 2, wo, ln, P(k), 1000, None) == _lib.GRS_ECAPACITY
+    s.close()
+
+
+def test_presorted_world1_empty_and_tiny(gpu, monkeypatch):
+    """grs_sort_sharded's presorted path on a one-rank RCCL communicator: empty, one-key and
+    one-block shards (the RCCL transport at G > 1 needs more GPUs than a box has)."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    from gpuradixsort_amd.sharded import RcclComm, ShardedSorter
+
+    monkeypatch.setenv("GRS_SHARDED", "general")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        comm = RcclComm(device=gpu.index)
+        s = ShardedSorter(5000, key_bits=32, device=gpu, comm=comm)
+        rng = np.random.default_rng(2)
+        for n in (0, 1, 255, 256, 257, 4999):
+            keys = rng.integers(0, 2**32, 5000, dtype=np.uint64).astype(np.uint32)
+            ko, _ = s.sort(torch.from_numpy(keys).to(gpu), n=n)
+            assert s.last_n_out == n
+            assert np.array_equal(ko.cpu().numpy(), np.sort(keys[:n]))
+        s.close()
+    finally:
+        dist.destroy_process_group()
