@@ -83,6 +83,8 @@ SIGNATURES = [
                                          c_void_p, c_void_p]),
     ("grs_shard_plan_host", c_int, [c_void_p, c_int, c_int, POINTER(c_uint64), POINTER(c_uint64),
                                     POINTER(c_uint64)]),
+    ("grs_shard_bounds_host", c_int, [c_void_p, c_size_t, c_int, c_void_p, c_void_p, c_int,
+                                      POINTER(c_uint64)]),
     ("grs_shard_samples_per_rank", c_int, [c_int]),
     ("grs_shard_sample", c_int, [c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("grs_shard_encode_words_max", c_size_t, [c_size_t, c_int]),

@@ -1877,6 +1877,24 @@ grs_status grs_shard_splitters_host(const void* sorted_keys, const uint32_t* sor
   return GRS_OK;
 }
 
+grs_status grs_shard_bounds_host(const void* sorted_keys, size_t n, int key_bytes,
+                                const void* splitters, const uint32_t* thresholds, int nranks,
+                                uint64_t* bounds_out) {
+  if ((key_bytes != 4 && key_bytes != 8) || nranks < 1 || nranks > grs::kMaxRanks || !bounds_out ||
+      (n > 0 && !sorted_keys) || (nranks > 1 && (!splitters || !thresholds)) || n > GRS_MAX_N)
+    return set_err(GRS_EINVAL, "grs_shard_bounds_host: bad argument");
+  const uint32_t n32 = static_cast<uint32_t>(n);
+  bounds_out[0] = 0;
+  bounds_out[nranks] = n;
+  for (int b = 0; b + 1 < nranks; ++b)
+    bounds_out[b + 1] = key_bytes == 4
+        ? grs::shard_bound(static_cast<const uint32_t*>(sorted_keys), n32,
+                           static_cast<const uint32_t*>(splitters)[b], thresholds[b])
+        : grs::shard_bound(static_cast<const uint64_t*>(sorted_keys), n32,
+                           static_cast<const uint64_t*>(splitters)[b], thresholds[b]);
+  return GRS_OK;
+}
+
 grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int rank,
                                uint64_t* send_off, uint64_t* recv_off, uint64_t* n_out) {
   if (!count_matrix || !send_off || !recv_off || !n_out || nranks < 1 || nranks > 16 || rank < 0 ||

@@ -38,6 +38,22 @@ constexpr int kMaxRanks = GRS_MAX_SPLITTERS + 1;
 // run of its key at clamp(th, lower_bound, upper_bound): th = 0 for a sample of an earlier
 // rank (every local copy of the key follows it), all-ones for a later rank (every copy
 // precedes it), the sample's own sorted position for this rank.  One 64-thread workgroup.
+template <typename K>
+__host__ __device__ __forceinline__ uint32_t shard_bound(const K* sorted, uint32_t n, K key, uint32_t th) {
+  uint32_t lo = 0, hi = n;   // lower bound
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (sorted[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  const uint32_t lb = lo;
+  hi = n;                    // upper bound
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (sorted[mid] <= key) lo = mid + 1; else hi = mid;
+  }
+  return th < lb ? lb : th > lo ? lo : th;
+}
+
 template <typename K, int N>
 __global__ __launch_bounds__(64) void grs_shard_bounds(const K* __restrict__ sorted, uint32_t n,
                                                        const SplitterIdxDigit<K, N>* __restrict__ dig,
@@ -48,22 +64,7 @@ __global__ __launch_bounds__(64) void grs_shard_bounds(const K* __restrict__ sor
     b[0] = 0;
     b[g] = n;
   }
-  if (t + 1 < g) {
-    const K key = dig->s[t];
-    uint32_t lo = 0, hi = n;   // lower bound
-    while (lo < hi) {
-      const uint32_t mid = lo + (hi - lo) / 2;
-      if (sorted[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    const uint32_t lb = lo;
-    hi = n;                    // upper bound
-    while (lo < hi) {
-      const uint32_t mid = lo + (hi - lo) / 2;
-      if (sorted[mid] <= key) lo = mid + 1; else hi = mid;
-    }
-    const uint32_t th = dig->th[t];
-    b[t + 1] = th < lb ? lb : th > lo ? lo : th;
-  }
+  if (t + 1 < g) b[t + 1] = shard_bound(sorted, n, dig->s[t], dig->th[t]);
   __syncthreads();
   if (t <= g) plan[t] = b[t];
   if (t == 0) {

@@ -214,6 +214,12 @@ grs_status grs_shard_splitters_host(const void* sorted_keys, const uint32_t* sor
                                     uint32_t* thresholds_out);
 grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int rank,
                                uint64_t* send_off, uint64_t* recv_off, uint64_t* n_out);
+/* The presorted exchange's bucket bounds in a SORTED shard (the device step grs_shard_bounds):
+ * bounds_out[0] = 0, bounds_out[G] = n, bounds_out[b+1] = clamp(thresholds[b], lower_bound,
+ * upper_bound of splitters[b]); bucket b = [bounds_out[b], bounds_out[b+1]). */
+grs_status grs_shard_bounds_host(const void* sorted_keys, size_t n, int key_bytes,
+                                 const void* splitters, const uint32_t* thresholds, int nranks,
+                                 uint64_t* bounds_out);
 /* Samples per rank of the sharded sort for nranks ranks (min(1024, 8192 / nranks)). */
 int grs_shard_samples_per_rank(int nranks);
 

@@ -16,7 +16,8 @@ functions the device code uses); nothing here is imported by gpuradixsort_amd.
 
 sim_presorted_sort follows the presorted exchange (run_sharded_presorted, grs_codec.hpp) for
 u32 keys without payload: local sort, samples of the SORTED shard, the same splitters, bucket
-bounds = clamp(threshold, lower_bound, upper_bound) of each splitter key (grs_shard_bounds),
+bounds = clamp(threshold, lower_bound, upper_bound) of each splitter key (libgrs's host twin
+grs_shard_bounds_host of the device step grs_shard_bounds, checked against numpy),
 exchange of the bucket runs in source-rank order, merge.  The encoding of the runs is exercised
 on the GPU (tests/test_gpu_presorted.py); here the runs travel as plain keys.
 """
@@ -130,9 +131,16 @@ def sim_presorted_sort(keys: np.ndarray, group=None):
     srt = np.sort(keys, kind="stable")
     sk, sp = _samples(srt, S)
     spl, th = _splitters(sk, sp, G, me, S, 4, keys.dtype, group)
-    lb = np.searchsorted(srt, spl, side="left")
+    L, check = _lib()
+    b = (ctypes.c_uint64 * (G + 1))()
+    spl = np.ascontiguousarray(spl)
+    th = np.ascontiguousarray(th)
+    check(L.grs_shard_bounds_host(srt.ctypes.data, srt.size, 4, spl.ctypes.data, th.ctypes.data,
+                                  G, b), "grs_shard_bounds_host")     # the product's arithmetic
+    bounds = np.array(list(b), np.int64)
+    lb = np.searchsorted(srt, spl, side="left")                        # ... and its restatement
     ub = np.searchsorted(srt, spl, side="right")
-    bounds = np.concatenate([[0], np.clip(th.astype(np.int64), lb, ub), [srt.size]]).astype(np.int64)
+    assert np.array_equal(bounds[1:G], np.clip(th.astype(np.int64), lb, ub))
     assert np.all(np.diff(bounds) >= 0)
     cnt = np.diff(bounds).astype(np.uint32)
     mat = np.ascontiguousarray(_all_gather_np(cnt, G, group)).reshape(G, G)

@@ -96,6 +96,46 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict_
   }
 }
 
+// Key + payload pass memory pattern (BASELINE C3) without compute: 256 equal digit runs per
+// tile, stored as two u32 arrays (AOS = 0, the library's SoA) or as one array of 8-byte
+// (key, value) records (AOS = 1): the same bytes, runs twice as long.
+template <int BLOCK, int ITEMS, int AOS>
+__global__ __launch_bounds__(BLOCK) void scatter_emu_pairs(const uint32_t* __restrict__ kin,
+                                                           const uint32_t* __restrict__ vin,
+                                                           uint32_t* __restrict__ kout,
+                                                           uint32_t* __restrict__ vout, uint32_t n) {
+  constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 256;
+  extern __shared__ uint32_t pad_lds[];
+  const uint32_t T = blockIdx.x;
+  if ((T + 1) * TILE > n) return;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t k[ITEMS], v[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t src = T * TILE + w * 64 * ITEMS + j * 64 + lane;
+    if constexpr (AOS) {
+      const uint2 x = reinterpret_cast<const uint2*>(kin)[src];
+      k[j] = x.x;
+      v[j] = x.y;
+    } else {
+      k[j] = kin[src];
+      v[j] = vin[src];
+    }
+  }
+  if (n == 0) pad_lds[threadIdx.x] = k[0] + v[0];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = j * BLOCK + threadIdx.x;
+    const uint32_t dst = (i / RUN) * (n / 256) + T * RUN + i % RUN;
+    if constexpr (AOS) {
+      reinterpret_cast<uint2*>(kout)[dst] = make_uint2(k[j], v[j]);
+    } else {
+      kout[dst] = k[j];
+      vout[dst] = v[j];
+    }
+  }
+}
+
 }  // namespace
 
 
@@ -165,6 +205,29 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
     default: return -1;
   }
   void* args[] = {&i, &o, &n};
+  if (hipLaunchKernel(k, dim3(tiles), dim3(block), args, lds, s) != hipSuccess) return -2;
+  return 0;
+}
+
+// pairs memory-pattern emulation: block, items, aos, dynamic LDS bytes; AoS buffers are 2n words
+int lab2_emu_pairs(int block, int items, int aos, int lds, const void* kin, const void* vin, void* kout,
+                   void* vout, uint32_t n, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t tiles = n / (block * items);
+  const void* k = nullptr;
+  const int code = block * 10000 + items * 10 + aos;
+  switch (code) {
+    case 10240320: k = (const void*)scatter_emu_pairs<1024, 32, 0>; break;
+    case 10240321: k = (const void*)scatter_emu_pairs<1024, 32, 1>; break;
+    case 7680400: k = (const void*)scatter_emu_pairs<768, 40, 0>; break;
+    case 7680401: k = (const void*)scatter_emu_pairs<768, 40, 1>; break;
+    default: return -1;
+  }
+  const uint32_t* a = static_cast<const uint32_t*>(kin);
+  const uint32_t* b = static_cast<const uint32_t*>(vin);
+  uint32_t* c = static_cast<uint32_t*>(kout);
+  uint32_t* d = static_cast<uint32_t*>(vout);
+  void* args[] = {&a, &b, &c, &d, &n};
   if (hipLaunchKernel(k, dim3(tiles), dim3(block), args, lds, s) != hipSuccess) return -2;
   return 0;
 }

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rot", type=int, default=0, help="OPT 2048 store-sweep rotation per tile (keys)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
+    ap.add_argument("--emu-pairs", default="", help="block:items:aos:lds,... pairs memory pattern (SoA vs AoS)")
     a = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, "liblab2.so"))
     vp = ctypes.c_void_p
@@ -140,6 +141,24 @@ def main():
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
             print(f"emu {e:20s} median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s", flush=True)
+    if a.emu_pairs:
+        # 2^28-pair C3 shape unless --n says otherwise: SoA (two arrays) vs AoS (one 8-B array)
+        npair = n
+        src = torch.empty(2 * npair, dtype=torch.uint32, device=dev)
+        grs.fill_splitmix(src, 77)
+        dst = torch.empty_like(src)
+        for e in a.emu_pairs.split(","):
+            b, it, aos, lds = (int(x) for x in e.split(":"))
+            ts = []
+            for _ in range(a.rounds):
+                e0.record()
+                assert L.lab2_emu_pairs(b, it, aos, lds, P(src), vp(src.data_ptr() + 4 * npair), P(dst),
+                                        vp(dst.data_ptr() + 4 * npair), ctypes.c_uint32(npair), sp) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            print(f"emu_pairs {e:20s} median {med:8.4f} ms  {npair * 16 / med / 1e6:8.1f} GB/s", flush=True)
     if a.check:
         for v in variants:
             kb, pairs = v[1], v[2]
