@@ -240,6 +240,8 @@ struct grs_sorter {
   size_t capacity = 0;
   void* alt_keys = nullptr;
   uint32_t* alt_vals = nullptr;
+  bool alt_joint = false;          // u32 pairs: alt_vals lies inside alt_keys' allocation (8n bytes)
+  int rec_mode = 1;                // GRS_RECORDS=0: no record passes (A/B)
   uint32_t* status = nullptr;      // 2 x status_words
   size_t status_words = 0;         // per buffer
   uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
@@ -314,7 +316,7 @@ void grs_destroy(grs_sorter* s) {
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(s->device);
   if (s->alt_keys) (void)hipFree(s->alt_keys);
-  if (s->alt_vals) (void)hipFree(s->alt_vals);
+  if (s->alt_vals && !s->alt_joint) (void)hipFree(s->alt_vals);
   if (s->status) (void)hipFree(s->status);
   if (s->ctrl) (void)hipFree(s->ctrl);
   if (s->h_err) (void)hipHostFree(s->h_err);
@@ -417,6 +419,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("GRS_HIST")) s->hist_variant = std::atoi(e) == 1 ? 1 : 2;
   if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("GRS_RECORDS")) s->rec_mode = std::atoi(e) != 0 ? 1 : 0;
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
   if (const char* e = std::getenv("GRS_XL")) s->xl_mode = std::atoi(e) != 0 ? 1 : 2;
@@ -445,8 +448,16 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
     }
     s->scratch_bytes += bytes;
   };
-  alloc(&s->alt_keys, cap * kb);
-  if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
+  if (s->pairs && key_type == GRS_KEY_U32) {
+    // one allocation: keys | payload, or the same bytes as 8-byte (key, value) records (the
+    // record passes of run_sort)
+    alloc(&s->alt_keys, cap * 8);
+    if (st == GRS_OK) s->alt_vals = static_cast<uint32_t*>(s->alt_keys) + cap;
+    s->alt_joint = true;
+  } else {
+    alloc(&s->alt_keys, cap * kb);
+    if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
+  }
   alloc(reinterpret_cast<void**>(&s->status), 2 * s->status_words * 4);
   alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
   if (st == GRS_OK && hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess)
@@ -609,6 +620,12 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
       vdst = vals;
     }
   }
+  // u32 pairs on XL tiles, even pass count, in place: the passes that write the scratch write
+  // it as 8-byte (key, value) records and the next pass reads them back (longer digit runs;
+  // the caller's buffers stay two arrays)
+  constexpr bool kRecType = sizeof(K) == 4 && PAIRS && RB == 8;
+  const bool rec = kRecType && xl && !src_in && (passes & 1) == 0 && s->alt_joint &&
+                   s->rec_mode != 0 && s->rank_mode == 0;
   using Dig = grs::RadixDigit<K>;
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
@@ -621,8 +638,14 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
       r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (xl) {
-      if constexpr (kXlType)
-        r = launch_pass<K, PAIRS, RB, XL, XL::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      if constexpr (kXlType) {
+        if (kRecType && rec && (p & 1) == 0)
+          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | (kRecType ? 8192u : 0u)>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        else if (kRecType && rec)
+          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | (kRecType ? 4096u : 0u)>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        else
+          r = launch_pass<K, PAIRS, RB, XL, XL::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      }
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
         r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);

@@ -174,6 +174,9 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //   1024 two-round reorder: the keys stay in registers and LDS holds half the tile at a
 //       time (positions [0, TILE/2) are reordered and stored, then [TILE/2, TILE)), so a
 //       tile can be twice what LDS holds: longer digit runs per tile, fewer partial lines
+//   4096 u32 pairs READ as 8-byte (key, value) records from keys_in (vals_in unused)
+//   8192 u32 pairs WRITTEN as 8-byte records to keys_out: one digit run of 8-byte records
+//       instead of two of 4-byte words, twice as long (fewer partial lines)
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
@@ -191,7 +194,20 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
     if constexpr ((OPT & 128) != 0) return __builtin_nontemporal_load(p + i);
     else return p[i];
   };
-  if (n - tile_base >= TILE) {
+  constexpr bool IN_REC = (OPT & 4096) != 0;
+  static_assert(!IN_REC || (PAIRS && sizeof(K) == 4), "records: u32 key + u32 value");
+  if constexpr (IN_REC) {
+    const uint2* rec = reinterpret_cast<const uint2*>(keys_in);
+    const uint32_t valid = n - tile_base;   // tile-local bounds (see below)
+    const uint32_t lbase = w * (GRS_WAVE * ITEMS) + lane;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const bool in = valid >= TILE || lbase + j * GRS_WAVE < valid;
+      const uint2 x = in ? rec[wbase + j * GRS_WAVE] : make_uint2(~0u, 0u);
+      key[j] = static_cast<K>(x.x);
+      val[j] = x.y;
+    }
+  } else if (n - tile_base >= TILE) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) key[j] = ld(keys_in, wbase + j * GRS_WAVE);
     if constexpr (PAIRS) {
@@ -471,6 +487,15 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       }
     }
     const uint32_t roff = static_cast<uint32_t>(rr * LTILE);
+    auto put = [&](uint32_t dst, K kk, uint32_t i) {
+      if constexpr ((OPT & 8192) != 0) {
+        static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
+        reinterpret_cast<uint2*>(keys_out)[dst] = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
+      } else {
+        keys_out[dst] = kk;
+        if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+      }
+    };
     if (valid == static_cast<uint32_t>(TILE)) {
 #pragma unroll
       for (int k = 0; k < LITEMS; ++k) {
@@ -479,8 +504,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         uint32_t dst = sm.base[dig_at(roff + i, kk)] + roff + i;
         if constexpr ((OPT & 64) != 0) dst = min(dst, n - 1);
         if constexpr ((OPT & 32) != 0) dst = tile_base + roff + i;
-        keys_out[dst] = kk;
-        if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+        put(dst, kk, i);
       }
     } else {
 #pragma unroll
@@ -489,8 +513,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         if (roff + i < valid) {
           const K kk = sm.keys[i];
           const uint32_t dst = sm.base[dig_at(roff + i, kk)] + roff + i;
-          keys_out[dst] = kk;
-          if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+          put(dst, kk, i);
         }
       }
     }

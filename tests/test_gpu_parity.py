@@ -168,16 +168,19 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     s4.close()
 
 
-@pytest.mark.parametrize("kb,pairs,t", [(32, False, 768 * 64), (32, True, 768 * 40),
-                                        (64, False, 768 * 44)])
-def test_xl_tiles(gpu, monkeypatch, kb, pairs, t):
+@pytest.mark.parametrize("kb,pairs,t,records", [(32, False, 768 * 64, "1"), (32, True, 768 * 40, "1"),
+                                                (32, True, 768 * 40, "0"), (64, False, 768 * 44, "1")])
+def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
     """GRS_XL=1 pins the two-round XL tiles (768 threads; LDS holds half the tile per round)
     at every big-tile size: bit-exact across tile, round and look-back group edges (the
-    library uses them from 32 tiles per CU)."""
+    library uses them from 32 tiles per CU).  u32 pairs: the even-numbered passes write the
+    scratch as 8-byte (key, value) records and the odd ones read them (GRS_RECORDS=0: two
+    arrays throughout); a 24-bit sort (3 passes) keeps two arrays and copies back."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_XL", "1")
     monkeypatch.setenv("GRS_TILE", "big")
+    monkeypatch.setenv("GRS_RECORDS", records)
     h = t // 2
     rng = np.random.default_rng(48 + kb + pairs)
     dt = np.uint32 if kb == 32 else np.uint64
@@ -196,6 +199,16 @@ def test_xl_tiles(gpu, monkeypatch, kb, pairs, t):
         assert np.array_equal(k.cpu().numpy(), keys[perm]), n
         if pairs:
             assert np.array_equal(v.cpu().numpy(), perm), n
+    if pairs:   # bits [0, 24): 3 passes, no record passes, result copied back
+        n = sizes[-1]
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        perm = oracle.stable_argsort(keys & np.uint32(0xFFFFFF))
+        k = to_dev(keys, gpu)
+        v = to_dev(np.arange(n, dtype=np.uint32), gpu)
+        s.sort(k, v, end_bit=24)
+        s.check_error()
+        assert np.array_equal(k.cpu().numpy(), keys[perm])
+        assert np.array_equal(v.cpu().numpy(), perm)
     s.close()
 
 
