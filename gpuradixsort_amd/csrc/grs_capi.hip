@@ -620,12 +620,13 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
       vdst = vals;
     }
   }
-  // u32 pairs on XL tiles, even pass count, in place: the passes that write the scratch write
-  // it as 8-byte (key, value) records and the next pass reads them back (longer digit runs;
-  // the caller's buffers stay two arrays)
+  // u32 pairs on big / XL tiles, 8-bit digits, even pass count, in place: the passes that write
+  // the scratch write it as 8-byte (key, value) records and the next pass reads them back
+  // (longer digit runs; the caller's buffers stay two arrays)
   constexpr bool kRecType = sizeof(K) == 4 && PAIRS && RB == 8;
-  const bool rec = kRecType && xl && !src_in && (passes & 1) == 0 && s->alt_joint &&
+  const bool rec = kRecType && big && !src_in && (passes & 1) == 0 && s->alt_joint &&
                    s->rec_mode != 0 && s->rank_mode == 0;
+  constexpr uint32_t kRecOut = kRecType ? 8192u : 0u, kRecIn = kRecType ? 4096u : 0u;
   using Dig = grs::RadixDigit<K>;
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
@@ -639,16 +640,26 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (xl) {
       if constexpr (kXlType) {
-        if (kRecType && rec && (p & 1) == 0)
-          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | (kRecType ? 8192u : 0u)>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-        else if (kRecType && rec)
-          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | (kRecType ? 4096u : 0u)>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        if (rec && (p & 1) == 0)
+          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | kRecOut>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        else if (rec)
+          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | kRecIn>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
         else
           r = launch_pass<K, PAIRS, RB, XL, XL::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
       }
     } else if (persist && big) {
-      if constexpr (!Big::TWO_ROUNDS)
-        r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      if constexpr (!Big::TWO_ROUNDS) {
+        if (rec && (p & 1) == 0)
+          r = launch_pass<K, PAIRS, RB, Big, kBig | kRecOut, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        else if (rec)
+          r = launch_pass<K, PAIRS, RB, Big, kBig | kRecIn, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        else
+          r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      }
+    } else if (big && rec) {
+      r = (p & 1) == 0
+          ? launch_pass<K, PAIRS, RB, Big, kBig | kRecOut>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
+          : launch_pass<K, PAIRS, RB, Big, kBig | kRecIn>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else {
       r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
