@@ -261,6 +261,17 @@ class ShardedParallelSort {
     return n_out;
   }
 
+  // Per-phase timing of the last Sort() (EnableProfiling first): before / of / after the
+  // exchange, and the bytes that crossed the links (grs_sharded_last_timing).
+  void EnableProfiling(int ring = 1) {
+    grs::check(grs_set_profiling(_sorter, ring), "ShardedParallelSort::EnableProfiling");
+  }
+  grs_sharded_timing LastExchangeTiming() {
+    grs_sharded_timing t{};
+    grs::check(grs_sharded_last_timing(_sorter, &t), "ShardedParallelSort::LastExchangeTiming");
+    return t;
+  }
+
  private:
   grs_sorter* _sorter = nullptr;
   void* _comm = nullptr;
