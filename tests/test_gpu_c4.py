@@ -185,3 +185,101 @@ def test_max_n_pairs_one_call(gpu, kb):
     assert torch.equal(gathered, k.view(iv))
     del k, gathered
     torch.cuda.empty_cache()
+
+
+def test_c4_presorted_eight_ranks_on_one_gpu(gpu):
+    """The presorted exchange of C4 at full size, eight ranks replayed on one GPU through the
+    C-ABI steps: each 2^27-key shard sorted, sampled, split by the tie-breaking splitters and
+    encoded; each receiver decodes and merges the eight encoded runs it gets.  The ranks'
+    outputs concatenated must hash to the committed digest; the encoding must be about a byte
+    per key; the receivers must be balanced."""
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd import _lib
+    from gpuradixsort_amd.sharded import shard_decode_merge, shard_encode, shard_sample
+
+    rec = _rec()
+    G, n = 8, rec["n"] // 8
+    S = int(_lib.lib().grs_shard_samples_per_rank(G))
+    s = grs.RadixSorter(n + n // 4, key_bits=32)
+    shards, sks, sps = [], [], []
+    for r in range(G):
+        k = torch.empty(n, dtype=torch.uint32, device=gpu)
+        grs.fill_splitmix(k, rec["seed"], first_index=r * n)
+        s.sort(k)
+        shards.append(k)
+        sk, sp = shard_sample(k, n, S)
+        sks.append(sk)
+        sps.append(sp)
+    gk, gp = torch.cat(sks), torch.cat(sps)
+    sends, mat = [], []
+    for r in range(G):
+        send, sz = shard_encode(s, shards[r], n, gk, gp, G, r)
+        sends.append(send)
+        mat.append(sz.cpu().numpy().astype(np.int64))
+    del shards
+    mat = np.stack(mat)
+    words = mat[:, 1::2]
+    assert 4 * words.sum() / (G * n) < 1.1
+    h = hashlib.sha256()
+    sizes = []
+    out = torch.empty(n + n // 4, dtype=torch.uint32, device=gpu)
+    for r in range(G):
+        parts, offs, lens, off = [], [], [], 0
+        for p in range(G):
+            start, w = int(words[p, :r].sum()), int(words[p, r])
+            parts.append(sends[p][start:start + w])
+            offs.append(off)
+            lens.append(int(mat[p, 2 * r]))
+            off += w
+        recv = torch.cat(parts)
+        m = shard_decode_merge(s, recv, offs, lens, out)
+        s.check_error()
+        sizes.append(m)
+        _host_sha_update(h, out[:m])
+        del recv
+    assert sum(sizes) == rec["n"]
+    assert max(sizes) / (sum(sizes) / G) <= 1.02, sizes
+    assert h.hexdigest() == rec["sha256_keys"]
+    s.close()
+
+
+@pytest.mark.parametrize("name", ["all_equal", "sorted", "reversed", "few_unique", "low_bits"])
+def test_c4_size_distributions(gpu, name):
+    """2^30 keys of structured distributions in one call: sorted, and the same multiset
+    (sum and sum of squares of the keys)."""
+    import gpuradixsort_amd as grs
+
+    n = 1 << 30
+    k = torch.empty(n, dtype=torch.uint32, device=gpu)
+    if name == "all_equal":
+        k.fill_(7)
+    else:
+        grs.fill_splitmix(k, 0xC4C4C4C4 + len(name))
+        if name == "sorted":
+            s0 = grs.RadixSorter(n, key_bits=32)
+            s0.sort(k)
+            s0.close()
+        elif name == "reversed":
+            s0 = grs.RadixSorter(n, key_bits=32)
+            s0.sort(k)
+            s0.close()
+            k = torch.flip(k.view(torch.int32), [0]).view(torch.uint32).contiguous()
+        elif name == "few_unique":
+            k = ((k.view(torch.int32) & 3) * 0x40000001).view(torch.uint32)   # 4 keys, top and low bits
+        elif name == "low_bits":   # every key below 2^12: the top passes see one digit
+            k = (k.view(torch.int32) & 0xFFF).view(torch.uint32).contiguous()
+
+    def checks(t):
+        s1 = s2 = 0
+        for i in range(0, n, 1 << 27):
+            c = t[i:i + (1 << 27)].view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+            s1 += int(c.sum().item())
+            s2 += int((c * c).remainder_(1 << 61).sum().item())   # int64 sums wrap: compare mod 2^64
+        return s1, s2 % (1 << 64)
+    before = checks(k)
+    s = grs.RadixSorter(n, key_bits=32)
+    s.sort(k)
+    s.check_error()
+    assert grs.count_inversions(k) == 0
+    assert checks(k) == before
+    s.close()
