@@ -65,6 +65,7 @@ def _worker(rank, world, port, n_local, key_bits, pairs, dist_name, out_dir):
     (4, 20000, 32, True, "few_unique"),
     (3, 7000, 64, False, "all_equal"),
     (2, 0, 32, True, "uniform"),
+    (8, 2000, 32, True, "skewed"),          # C4's rank count (G in {1, 2, 4, 8})
 ])
 def test_sharded_sort_equals_global_stable_sort(tmp_path, world, n_local, key_bits, pairs,
                                                  dist_name):
@@ -107,7 +108,7 @@ def _worker_presorted(rank, world, port, n_local, dist_name, out_dir):
 
 @pytest.mark.parametrize("world,n_local,dist_name", [
     (2, 5000, "uniform"), (3, 3001, "skewed"), (4, 2500, "all_equal"), (4, 20000, "few_unique"),
-    (2, 0, "uniform"),
+    (2, 0, "uniform"), (8, 3000, "few_unique"),
 ])
 def test_presorted_exchange_equals_sort(tmp_path, world, n_local, dist_name):
     """The presorted exchange's orchestration (u32 keys): sorted-shard samples, the product's
