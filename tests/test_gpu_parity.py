@@ -199,16 +199,18 @@ def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
         assert np.array_equal(k.cpu().numpy(), keys[perm]), n
         if pairs:
             assert np.array_equal(v.cpu().numpy(), perm), n
-    if pairs:   # bits [0, 24): 3 passes, no record passes, result copied back
+    if pairs:   # bits [0, 24): 3 passes, no record passes, result copied back;
+        #             bits [8, 24): 2 passes, record passes in between
         n = sizes[-1]
-        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
-        perm = oracle.stable_argsort(keys & np.uint32(0xFFFFFF))
-        k = to_dev(keys, gpu)
-        v = to_dev(np.arange(n, dtype=np.uint32), gpu)
-        s.sort(k, v, end_bit=24)
-        s.check_error()
-        assert np.array_equal(k.cpu().numpy(), keys[perm])
-        assert np.array_equal(v.cpu().numpy(), perm)
+        for lo, hi in ((0, 24), (8, 24)):
+            keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            perm = oracle.stable_argsort((keys >> np.uint32(lo)) & np.uint32((1 << (hi - lo)) - 1))
+            k = to_dev(keys, gpu)
+            v = to_dev(np.arange(n, dtype=np.uint32), gpu)
+            s.sort(k, v, begin_bit=lo, end_bit=hi)
+            s.check_error()
+            assert np.array_equal(k.cpu().numpy(), keys[perm]), (lo, hi)
+            assert np.array_equal(v.cpu().numpy(), perm), (lo, hi)
     s.close()
 
 
