@@ -241,7 +241,8 @@ struct grs_sorter {
   void* alt_keys = nullptr;
   uint32_t* alt_vals = nullptr;
   bool alt_joint = false;          // u32 pairs: alt_vals lies inside alt_keys' allocation (8n bytes)
-  int rec_mode = 1;                // GRS_RECORDS=0: no record passes (A/B)
+  int rec_mode = 2;                // GRS_RECORDS: 0 two arrays, 1 records in the scratch
+                                   // only, 2 also split over the caller's arrays (A/B)
   uint32_t* status = nullptr;      // 2 x status_words
   size_t status_words = 0;         // per buffer
   uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
@@ -419,7 +420,7 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("GRS_HIST")) s->hist_variant = std::atoi(e) == 1 ? 1 : 2;
   if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("GRS_RECORDS")) s->rec_mode = std::atoi(e) != 0 ? 1 : 0;
+  if (const char* e = std::getenv("GRS_RECORDS")) s->rec_mode = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("GRS_TILE"))
     s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
   if (const char* e = std::getenv("GRS_XL")) s->xl_mode = std::atoi(e) != 0 ? 1 : 2;
@@ -543,6 +544,25 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
   return GRS_OK;
 }
 
+// One pass with the record flags of kind (run_sort's rec_kind): 0 two arrays, 1 write
+// records, 2 read records, 3 read split records + write records, 4 read records + write split.
+template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERSIST>
+grs_status launch_rec(int kind, grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc,
+                      uint32_t* vdst, uint32_t n, const grs::RadixDigit<K>& dig,
+                      const uint32_t* hist, uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt,
+                      hipStream_t stream, uint32_t expect_tile) {
+  using Dig = grs::RadixDigit<K>;
+  constexpr bool R = sizeof(K) == 4 && PAIRS && RB == 8;
+  constexpr uint32_t W = R ? 8192u : 0u, Rd = R ? 4096u : 0u, RS = R ? 16384u : 0u, WS = R ? 32768u : 0u;
+  switch (R ? kind : 0) {
+    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+  }
+}
+
 // src_in (out-of-place, the presorted exchange): pass 0 reads src_in / vsrc_in instead of
 // keys / vals, and the passes alternate so that the last one writes keys / vals (no copy-back).
 template <typename K, bool PAIRS, int RB>
@@ -626,7 +646,17 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   constexpr bool kRecType = sizeof(K) == 4 && PAIRS && RB == 8;
   const bool rec = kRecType && big && !src_in && (passes & 1) == 0 && s->alt_joint &&
                    s->rec_mode != 0 && s->rank_mode == 0;
-  constexpr uint32_t kRecOut = kRecType ? 8192u : 0u, kRecIn = kRecType ? 4096u : 0u;
+  // even n, 4+ passes: the middle passes also write records, split over the caller's two
+  // arrays (records [0, n/2) in keys, [n/2, n) in vals), so every pass but the last writes
+  // records.  Pass p's record flags: 0 = none, 1 = write, 2 = read, 3 = read split + write,
+  // 4 = read + write split
+  // (not on the persistent pass: at 2^24 pairs it measured slower there)
+  const bool rec_split = rec && (n & 1u) == 0 && passes >= 4 && s->rec_mode == 2 && !persist;
+  auto rec_kind = [&](int p) -> int {
+    if (!rec) return 0;
+    if ((p & 1) == 0) return p > 0 && rec_split ? 3 : 1;
+    return p < passes - 1 && rec_split ? 4 : 2;
+  };
   using Dig = grs::RadixDigit<K>;
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
@@ -639,27 +669,13 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
       r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (xl) {
-      if constexpr (kXlType) {
-        if (rec && (p & 1) == 0)
-          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | kRecOut>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-        else if (rec)
-          r = launch_pass<K, PAIRS, RB, XL, XL::OPT | kRecIn>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-        else
-          r = launch_pass<K, PAIRS, RB, XL, XL::OPT>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-      }
+      if constexpr (kXlType)
+        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (persist && big) {
-      if constexpr (!Big::TWO_ROUNDS) {
-        if (rec && (p & 1) == 0)
-          r = launch_pass<K, PAIRS, RB, Big, kBig | kRecOut, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-        else if (rec)
-          r = launch_pass<K, PAIRS, RB, Big, kBig | kRecIn, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-        else
-          r = launch_pass<K, PAIRS, RB, Big, kBig, true>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
-      }
+      if constexpr (!Big::TWO_ROUNDS)
+        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else if (big && rec) {
-      r = (p & 1) == 0
-          ? launch_pass<K, PAIRS, RB, Big, kBig | kRecOut>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
-          : launch_pass<K, PAIRS, RB, Big, kBig | kRecIn>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tickets + p, st_cur, st_nxt, stream, tile);
     } else {
       r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
               : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);

@@ -177,6 +177,9 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //   4096 u32 pairs READ as 8-byte (key, value) records from keys_in (vals_in unused)
 //   8192 u32 pairs WRITTEN as 8-byte records to keys_out: one digit run of 8-byte records
 //       instead of two of 4-byte words, twice as long (fewer partial lines)
+//   16384 / 32768: the records read / written are SPLIT over two buffers: records [0, n/2)
+//       in keys_in / keys_out and [n/2, n) in vals_in / vals_out (n even; the caller's two
+//       4n-byte arrays hold n records that way)
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
@@ -198,12 +201,16 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
   static_assert(!IN_REC || (PAIRS && sizeof(K) == 4), "records: u32 key + u32 value");
   if constexpr (IN_REC) {
     const uint2* rec = reinterpret_cast<const uint2*>(keys_in);
+    const uint2* rec_hi = reinterpret_cast<const uint2*>(vals_in);   // split: records [n/2, n)
+    const uint32_t half = n / 2;
     const uint32_t valid = n - tile_base;   // tile-local bounds (see below)
     const uint32_t lbase = w * (GRS_WAVE * ITEMS) + lane;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
       const bool in = valid >= TILE || lbase + j * GRS_WAVE < valid;
-      const uint2 x = in ? rec[wbase + j * GRS_WAVE] : make_uint2(~0u, 0u);
+      const uint32_t idx = wbase + j * GRS_WAVE;
+      const bool hi = (OPT & 16384) != 0 && idx >= half;
+      const uint2 x = !in ? make_uint2(~0u, 0u) : hi ? rec_hi[idx - half] : rec[idx];
       key[j] = static_cast<K>(x.x);
       val[j] = x.y;
     }
@@ -490,7 +497,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     auto put = [&](uint32_t dst, K kk, uint32_t i) {
       if constexpr ((OPT & 8192) != 0) {
         static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
-        reinterpret_cast<uint2*>(keys_out)[dst] = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
+        const uint2 r = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
+        if constexpr ((OPT & 32768) != 0) {   // split records: [n/2, n) in vals_out
+          if (dst >= n / 2) reinterpret_cast<uint2*>(vals_out)[dst - n / 2] = r;
+          else reinterpret_cast<uint2*>(keys_out)[dst] = r;
+        } else {
+          reinterpret_cast<uint2*>(keys_out)[dst] = r;
+        }
       } else {
         keys_out[dst] = kk;
         if constexpr (PAIRS) vals_out[dst] = sm.vals[i];

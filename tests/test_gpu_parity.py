@@ -168,14 +168,16 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     s4.close()
 
 
-@pytest.mark.parametrize("kb,pairs,t,records", [(32, False, 768 * 64, "1"), (32, True, 768 * 40, "1"),
-                                                (32, True, 768 * 40, "0"), (64, False, 768 * 44, "1")])
+@pytest.mark.parametrize("kb,pairs,t,records", [(32, False, 768 * 64, "2"), (32, True, 768 * 40, "2"),
+                                                (32, True, 768 * 40, "1"), (32, True, 768 * 40, "0"),
+                                                (64, False, 768 * 44, "2")])
 def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
     """GRS_XL=1 pins the two-round XL tiles (768 threads; LDS holds half the tile per round)
     at every big-tile size: bit-exact across tile, round and look-back group edges (the
-    library uses them from 32 tiles per CU).  u32 pairs: the even-numbered passes write the
-    scratch as 8-byte (key, value) records and the odd ones read them (GRS_RECORDS=0: two
-    arrays throughout); a 24-bit sort (3 passes) keeps two arrays and copies back."""
+    library uses them from 32 tiles per CU).  u32 pairs: the passes write 8-byte (key, value)
+    records -- into the scratch, and (GRS_RECORDS=2, even n, 4 passes) split over the caller's
+    two arrays for the middle passes; GRS_RECORDS=1: the scratch only; 0: two arrays
+    throughout; a 24-bit sort (3 passes) keeps two arrays and copies back."""
     import gpuradixsort_amd as grs
 
     monkeypatch.setenv("GRS_XL", "1")
@@ -184,7 +186,9 @@ def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
     h = t // 2
     rng = np.random.default_rng(48 + kb + pairs)
     dt = np.uint32 if kb == 32 else np.uint64
-    sizes = (1, h - 1, h + 1, t - 1, t + 1, t + h + 3, 8 * t - 1, 8 * t + 1, 8 * t * 5 + h + 7)
+    # odd and even sizes: split records need an even n
+    sizes = (1, 2, h - 1, h, h + 1, t - 1, t, t + 1, t + h + 3, t + h + 4, 8 * t - 1, 8 * t,
+             8 * t + 1, 8 * t * 5 + h + 7, 8 * t * 5 + h + 8)
     s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs)
     assert s.pass_kernel_for(max(sizes)) == "grs_onesweep_v4"
     for n in sizes:
