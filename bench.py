@@ -1,6 +1,6 @@
 """bench.py — Gkeys/s of the MI355X LSD radix sort (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5|ns]
   (N > 1: torchrun --nproc-per-node N ... bench.py --gpus N ...; one rank per GPU, RCCL)
 
 A step = one complete sort of one batch of synthetic keys already resident in HBM
@@ -48,6 +48,9 @@ CONFIGS = {
     "c2": (2, 1 << 24, 32, False, 4, "C2: 16M uint32 keys, 4-bit-digit LSD"),
     "c3": (3, 1 << 28, 32, True, 8, "C3: 256M uint32 key + uint32 payload, stable"),
     "c5": (5, 1 << 28, 64, False, 8, "C5: 256M uint64 keys, 8 x 8-bit passes"),
+    # BASELINE.json north_star's own 1-GPU target: >= 60 % of the HBM roofline on 256 M
+    # uniform-random uint32 keys (keys only)
+    "ns": (6, 1 << 28, 32, False, 8, "north star: 256M uniform uint32 keys, keys only, 8-bit LSD"),
 }
 
 
@@ -69,6 +72,22 @@ def parse():
     return ap.parse_args()
 
 
+def usable_cores():
+    """(threads to use, what the host reports): the affinity mask's CPUs, capped by the
+    cgroup v2 CPU quota (cpu.max) when one is set."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    cores = max(1, min(aff, quota) if quota else aff)
+    return cores, {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+                   "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
@@ -88,9 +107,11 @@ def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
     out = {"value": round(n_sample / dt / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
            "sample": f"{n_sample} keys of the same splitmix64 uniform workload, {what}, "
                      f"1 thread, {dt:.2f} s (oracle/cpu_sort.cpp)"}
-    # __gnu_parallel::sort on this process's share of the host, beside it
-    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
-                       else (os.cpu_count() or 1)))
+    # __gnu_parallel::sort on ALL of the host cores this process may use: the
+    # CPUs of its affinity mask, capped by the cgroup's CPU quota where one is set (a GPU box
+    # shares a larger machine; os.cpu_count() counts the whole machine there)
+    cores, host = usable_cores()
+    host["hardware_concurrency"] = oracle.hardware_concurrency()
     keys = oracle.splitmix_keys(n_sample, key_bits, seed)
     t = time.perf_counter()
     if pairs:
@@ -99,7 +120,8 @@ def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
         oracle.cpu_sort(keys, cores)
     dt = time.perf_counter() - t
     out["parallel"] = {"value": round(n_sample / dt / 1e9, 5), "cores": cores,
-                       "what": f"__gnu_parallel::sort, {cores} threads, {dt:.2f} s"}
+                       "what": f"__gnu_parallel::sort, {cores} threads, {dt:.2f} s",
+                       "host": host}
     return out
 
 

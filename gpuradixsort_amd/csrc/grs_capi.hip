@@ -651,7 +651,13 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   // records.  Pass p's record flags: 0 = none, 1 = write, 2 = read, 3 = read split + write,
   // 4 = read + write split
   // (not on the persistent pass: at 2^24 pairs it measured slower there)
-  const bool rec_split = rec && (n & 1u) == 0 && passes >= 4 && s->rec_mode == 2 && !persist;
+  // The split records are 8-byte loads and stores on the caller's arrays: both must be 8-byte
+  // aligned (a torch view at an odd storage offset, or an offset C pointer, is only 4-byte
+  // aligned); otherwise the middle passes keep two arrays.
+  const bool caller_aligned =
+      ((reinterpret_cast<uintptr_t>(keys) | reinterpret_cast<uintptr_t>(vals)) & 7u) == 0;
+  const bool rec_split = rec && (n & 1u) == 0 && passes >= 4 && s->rec_mode == 2 && !persist &&
+                         caller_aligned;
   auto rec_kind = [&](int p) -> int {
     if (!rec) return 0;
     if ((p & 1) == 0) return p > 0 && rec_split ? 3 : 1;
@@ -861,6 +867,11 @@ grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n
   if (n == 0) return GRS_OK;  // the reference's N = 0 "won't crash" (PrefixSumSsbo.cpp:121-124)
   if (!d_keys) return set_err(GRS_EINVAL, "grs_sort: d_keys is NULL");
   if (s->pairs && !d_vals) return set_err(GRS_EINVAL, "grs_sort: payload sorter needs d_vals");
+  // natural alignment of the element types (u32 pairs at 4-byte alignment are fine: the record
+  // passes that move 8 bytes on the caller's arrays check for 8 and fall back, run_sort)
+  if ((reinterpret_cast<uintptr_t>(d_keys) & (static_cast<uintptr_t>(kbits / 8) - 1)) != 0 ||
+      (reinterpret_cast<uintptr_t>(d_vals) & 3u) != 0)
+    return set_err(GRS_EINVAL, "grs_sort: d_keys / d_vals not aligned to their element size");
   int prev = 0;
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));

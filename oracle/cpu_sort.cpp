@@ -11,9 +11,13 @@
 #include <cstddef>
 #include <cstdint>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 extern "C" {
+
+// std::thread::hardware_concurrency() of this host (recorded beside the parallel baseline)
+int cpu_hardware_concurrency(void) { return static_cast<int>(std::thread::hardware_concurrency()); }
 
 void cpu_sort_u32(uint32_t* keys, size_t n, int threads) {
   if (threads > 1) {

@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_fill_splitmix_u32.argtypes = [u32p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
         L.oracle_fill_splitmix_u64.restype = None
         L.oracle_fill_splitmix_u64.argtypes = [u64p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
+        L.cpu_hardware_concurrency.restype = ctypes.c_int
+        L.cpu_hardware_concurrency.argtypes = []
         L.cpu_sort_u32.restype = None
         L.cpu_sort_u32.argtypes = [u32p, ctypes.c_size_t, ctypes.c_int]
         L.cpu_sort_u64.restype = None
@@ -204,6 +206,11 @@ def splitmix_keys(n: int, key_bits: int, seed: int, first: int = 0) -> np.ndarra
 
 
 # ---- CPU baseline ---------------------------------------------------------------------------
+
+def hardware_concurrency() -> int:
+    """std::thread::hardware_concurrency() of this host."""
+    return int(lib().cpu_hardware_concurrency())
+
 
 def cpu_sort(keys: np.ndarray, threads: int = 1) -> None:
     """In-place std::sort (threads == 1) or __gnu_parallel::sort."""

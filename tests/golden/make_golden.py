@@ -12,7 +12,7 @@ committed oracle:
   digests.json            SHA-256 of the expected sorted keys (and stable permutation) of the
                           BASELINE.json configs at their seeds (SURVEY.md §8d generator).
 
-usage: python tests/golden/make_golden.py [--large]
+usage: python tests/golden/make_golden.py [--large] [--only NAME]
 """
 from __future__ import annotations
 
@@ -75,6 +75,9 @@ CONFIGS = {
     "c3_256m_u32_pairs": (3, 1 << 28, 32, True),
     "c4_1b_u32": (4, 1 << 30, 32, False),
     "c5_256m_u64": (5, 1 << 28, 64, False),
+    # the north star's own 1-GPU config (BASELINE.json north_star: 256 M uniform-random
+    # uint32 keys, keys only); config id 6 = its own seed
+    "ns_256m_u32": (6, 1 << 28, 32, False),
 }
 SMALL = ("c1_64k_u32", "c1_64k_u32_pairs", "c2_16m_u32")
 
@@ -99,6 +102,7 @@ def digest(name):
 
 def main():
     large = "--large" in sys.argv
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     rows = xlsx_rows(os.path.join(REF, "PrefixScan.xlsx"), [2, 3, 50, 102])
     assert rows[2] == list(range(32)), rows[2]
     scan = {"source": "PrefixScan.xlsx sheet1 rows 3 (input), 50 (after set-last-to-0), 102 (result)",
@@ -115,7 +119,7 @@ def main():
     path = os.path.join(HERE, "digests.json")
     digests = json.load(open(path)) if os.path.exists(path) else {}
     for name in CONFIGS:
-        if name in SMALL or large:
+        if (only is None and (name in SMALL or large)) or name == only:
             print("digest", name, flush=True)
             digests[name] = digest(name)
     json.dump(digests, open(path, "w"), indent=1, sort_keys=True)

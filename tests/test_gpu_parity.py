@@ -218,6 +218,93 @@ def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
     s.close()
 
 
+@pytest.mark.parametrize("records", ["1", "2"])
+def test_big_tile_record_passes(gpu, monkeypatch, records):
+    """The one-round big-tile v4 pass with record flags (launch_rec kinds 1-4: 8-byte (key,
+    value) records in the scratch, and for even n split over the caller's two arrays): the
+    library takes it between ~2^24 and ~2^28 u32 pairs.  GRS_XL=0 + GRS_TILE=big + GRS_PASS=v4
+    pin it at test sizes; odd and even n (split records need an even n); payload == the
+    stable permutation."""
+    import gpuradixsort_amd as grs
+
+    monkeypatch.setenv("GRS_XL", "0")
+    monkeypatch.setenv("GRS_TILE", "big")
+    monkeypatch.setenv("GRS_PASS", "v4")
+    monkeypatch.setenv("GRS_RECORDS", records)
+    t = 1024 * 17
+    h = t // 2
+    rng = np.random.default_rng(170 + int(records))
+    sizes = (2, 3, h, h + 1, t, t + 1, 8 * t, 8 * t + 1, 8 * t * 3 + h + 7, 8 * t * 3 + h + 8,
+             2_000_000, 2_000_001)
+    s = grs.RadixSorter(max(sizes), key_bits=32, pairs=True)
+    assert s.pass_kernel_for(max(sizes)) == "grs_onesweep_v4"
+    for n in sizes:
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        keys[::29] = keys[0]
+        keys[::101] = 0xFFFFFFFF
+        perm = oracle.stable_argsort(keys)
+        k = to_dev(keys, gpu)
+        v = to_dev(np.arange(n, dtype=np.uint32), gpu)
+        s.sort(k, v)
+        s.check_error()
+        assert np.array_equal(k.cpu().numpy(), keys[perm]), n
+        assert np.array_equal(v.cpu().numpy(), perm), n
+    s.close()
+
+
+@pytest.mark.parametrize("shape", ["xl", "big"])
+@pytest.mark.parametrize("offset", [1, 2])
+def test_pairs_offset_views(gpu, monkeypatch, shape, offset):
+    """u32 pairs sorted through views at a storage offset (keys[offset:], vals[offset:]):
+    offset 1 leaves the arrays only 4-byte aligned, so the record passes that move 8-byte
+    records on the caller's arrays must fall back to two arrays (run_sort's alignment gate);
+    offset 2 is 8-byte aligned and keeps the split records.  Even n past the record-pass
+    thresholds; payload == the stable permutation, and the elements before the view stay."""
+    import gpuradixsort_amd as grs
+
+    if shape == "xl":
+        monkeypatch.setenv("GRS_XL", "1")
+    else:
+        monkeypatch.setenv("GRS_XL", "0")
+        monkeypatch.setenv("GRS_PASS", "v4")
+    monkeypatch.setenv("GRS_TILE", "big")
+    monkeypatch.setenv("GRS_RECORDS", "2")
+    rng = np.random.default_rng(90 + offset)
+    n = 1_000_002
+    s = grs.RadixSorter(n, key_bits=32, pairs=True)
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    keys[::31] = 12345
+    perm = oracle.stable_argsort(keys)
+    kb = torch.full((n + offset,), 0xABCDEF, dtype=torch.int32, device=gpu)
+    vb = torch.full((n + offset,), 0x13579B, dtype=torch.int32, device=gpu)
+    k, v = kb[offset:], vb[offset:]
+    assert (k.data_ptr() % 8 == 0) == (offset % 2 == 0)
+    k.copy_(torch.from_numpy(keys.view(np.int32)).to(gpu))
+    v.copy_(torch.arange(n, dtype=torch.int32, device=gpu))
+    s.sort(k, v)
+    s.check_error()
+    assert np.array_equal(k.cpu().numpy().view(np.uint32), keys[perm])
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), perm)
+    assert kb[:offset].eq(0xABCDEF).all() and vb[:offset].eq(0x13579B).all()
+    s.close()
+
+
+def test_misaligned_u64_keys_rejected(gpu):
+    """u64 keys must be 8-byte aligned: a 4-byte-offset pointer returns GRS_EINVAL instead of
+    issuing misaligned 8-byte accesses."""
+    import ctypes
+
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd._lib import lib
+
+    s = grs.RadixSorter(1024, key_bits=64, pairs=False)
+    buf = torch.zeros(2048 + 2, dtype=torch.int32, device=gpu)
+    rc = lib().grs_sort(s._h, ctypes.c_void_p(buf.data_ptr() + 4), ctypes.c_void_p(0), 1024,
+                        ctypes.c_void_p(0))
+    assert rc != 0 and "aligned" in lib().grs_last_error().decode()
+    s.close()
+
+
 def test_ballot_match_fallback(gpu, monkeypatch):
     """GRS_RANK=match forces ballot-match ranking (the path taken if the LDS order probe
     ever fails): same bit-exact results, both tile shapes."""
@@ -332,7 +419,8 @@ def test_config_digests_small(gpu, name, radix_bits):
         assert _digest(v.cpu().numpy()) == rec["sha256_perm"]
 
 
-@pytest.mark.parametrize("name,radix_bits", [("c3_256m_u32_pairs", 8), ("c5_256m_u64", 8)])
+@pytest.mark.parametrize("name,radix_bits", [("ns_256m_u32", 8), ("c3_256m_u32_pairs", 8),
+                                             ("c5_256m_u64", 8)])
 def test_config_digests_full_size(gpu, name, radix_bits):
     """Full BASELINE sizes: exact SHA-256 of the expected output, plus the properties
     (sortedness via the device inversion counter)."""
