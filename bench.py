@@ -65,8 +65,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--sharded", action="store_true",
-                    help="N = 1 through grs_sort_sharded's multi-rank code path (GRS_SHARDED="
-                         "general, a one-rank RCCL communicator): a one-GPU rehearsal of N > 1")
+                    help="N = 1 through grs_sort_sharded's multi-rank code path (option "
+                         "sharded_path=general, a one-rank RCCL communicator): a one-GPU "
+                         "rehearsal of N > 1")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="sorter option (grs_set_option, gpuradixsort_amd._lib.OPTIONS) for A/B "
+                         "runs; repeatable")
     ap.add_argument("--pool-gib", type=float, default=96.0,
                     help="HBM budget for the distinct per-step input buffers")
     return ap.parse_args()
@@ -141,7 +145,6 @@ def main():
     if sharded and world == 1:
         import socket
 
-        os.environ["GRS_SHARDED"] = "general"
         with socket.socket() as so:
             so.bind(("127.0.0.1", 0))
             port = so.getsockname()[1]
@@ -150,6 +153,10 @@ def main():
     import gpuradixsort_amd as grs
 
     cid, n_cfg, kb, pairs, rb, desc = CONFIGS[a.config]
+    options = dict(o.split("=", 1) for o in a.opt)
+    options = {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in options.items()}
+    if sharded and world == 1:
+        options.setdefault("sharded_path", "general")
     if a.n:
         n_cfg = a.n
     strong = a.config == "c4"
@@ -172,7 +179,7 @@ def main():
             vals_pool.append(v)
 
     if not sharded:
-        sorter = grs.RadixSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb)
+        sorter = grs.RadixSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb, options=options)
         sorter.set_profiling(max(1, a.steps))
 
         def step(i):
@@ -183,7 +190,8 @@ def main():
     else:
         from gpuradixsort_amd.sharded import ShardedSorter
 
-        sorter = ShardedSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb, device=dev)
+        sorter = ShardedSorter(n_local, key_bits=kb, pairs=pairs, radix_bits=rb, device=dev,
+                               options=options)
         sorter.set_profiling(max(1, a.steps))
 
         def step(i):
@@ -276,6 +284,8 @@ def main():
                           "sort_total_gpu": round(sort_ms, 5)},
             "check": {"inversions_last_step": inversions},
         }
+        if options:
+            out["config"]["options"] = options
         if sharded:
             out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
             out["config"]["exchange"] = exchange

@@ -8,7 +8,9 @@ ParallelSort controller surface (amdreallyfast/GpuRadixSort).
   key_transform        order-preserving signed / float key bits (sort them as unsigned)
   exclusive_scan_u32   stand-alone device-wide scan (the reference's K3a + K3b)
   RadixSorter.sort_segmented   batched sort of independent segments
-  sharded_sort         multi-GPU key-range sort: one RCCL all-to-all-v over xGMI
+  sharded.ShardedSorter        multi-GPU key-range sort (grs_sort_sharded): device splitters,
+                       one exchange of grouped RCCL ncclSend / ncclRecv over xGMI, local sort
+                       (or presorted runs bit-packed, exchanged and merged)
 
 All compute runs in libgrs.so's HIP kernels; there is no CPU fallback.
 """

@@ -51,6 +51,19 @@ class grs_key_extract(ctypes.Structure):
 
 GRS_EXTRACT_FIELD, GRS_EXTRACT_MORTON3 = 0, 1
 
+# grs_option (include/grs.h) by the names RadixSorter(options=...) takes, with the value names
+# each accepts besides plain ints
+OPTIONS = {
+    "tile": (1, {"size": -1, "small": 0, "big": 1}),
+    "xl": (2, {"size": -1, "never": 0, "always": 1}),
+    "pass": (3, {"auto": 0, "v4": 4, "v6": 6}),
+    "records": (4, {"arrays": 0, "scratch": 1, "split": 2}),
+    "rank": (5, {"probe": 0, "match": 1}),
+    "sharded_path": (6, {"auto": 0, "general": 1}),
+    "sharded_send": (7, {"regions": 0, "contig": 1}),
+    "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
+}
+
 # (name, restype, argtypes) of every symbol include/grs.h declares
 SIGNATURES = [
     ("grs_version", c_int, []),
@@ -61,6 +74,8 @@ SIGNATURES = [
     ("grs_scratch_bytes", c_size_t, [c_void_p]),
     ("grs_rank_mode", c_int, [c_void_p]),
     ("grs_lds_order_check", c_int, [c_int, c_int, c_int, POINTER(c_ulonglong)]),
+    ("grs_set_option", c_int, [c_void_p, c_int, c_int]),
+    ("grs_get_option", c_int, [c_void_p, c_int, POINTER(c_int)]),
     ("grs_pass_kernel", c_char_p, [c_void_p, c_size_t]),
     ("grs_sort", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     ("grs_sort_bits", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),

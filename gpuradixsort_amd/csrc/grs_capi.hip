@@ -3,7 +3,7 @@
 // The pass driver replaces ParallelSort::Sort (Source/ComputeControllers/ParallelSort.cpp:168-298):
 // where the reference issues 1 + 32 x 4 GLSL dispatches with a glMemoryBarrier after each,
 // one grs_sort call issues
-//     hipMemsetAsync(control block)  -> grs_upfront_hist  -> P x grs_onesweep_pass
+//     hipMemsetAsync(control block)  -> grs_upfront_hist2  -> P x grs_onesweep_v4 / v6
 // on one stream (P = ceil((end_bit - begin_bit) / radix_bits); 4 launches for u32 at 8-bit
 // digits), plus one D2D copy when P is odd so the result lands back in the caller's buffer
 // (the reference's glCopyBufferSubData, ParallelSort.cpp:312-318).
@@ -200,13 +200,11 @@ __global__ __launch_bounds__(512) void grs_lds_order_scale(uint32_t pattern, uin
 }
 
 // Rank mode per device: 0 = atomic ranking (probe passed), 1 = ballot-match fallback.
-// GRS_RANK=match in the environment forces the fallback (tests cover both paths).
+// grs_set_option(GRS_OPT_RANK, 1) forces the fallback on one sorter (tests cover both paths).
 int device_rank_mode(int device) {
   static std::mutex mu;
   static int mode[64];
   static bool known[64];
-  const char* env = std::getenv("GRS_RANK");
-  if (env && std::strcmp(env, "match") == 0) return 1;
   std::lock_guard<std::mutex> lock(mu);
   if (device >= 0 && device < 64 && known[device]) return mode[device];
   int m = 1;
@@ -241,8 +239,8 @@ struct grs_sorter {
   void* alt_keys = nullptr;
   uint32_t* alt_vals = nullptr;
   bool alt_joint = false;          // u32 pairs: alt_vals lies inside alt_keys' allocation (8n bytes)
-  int rec_mode = 2;                // GRS_RECORDS: 0 two arrays, 1 records in the scratch
-                                   // only, 2 also split over the caller's arrays (A/B)
+  int rec_mode = 2;                // GRS_OPT_RECORDS: 0 two arrays, 1 records in the scratch
+                                   // only, 2 also split over the caller's arrays
   uint32_t* status = nullptr;      // 2 x status_words
   size_t status_words = 0;         // per buffer
   uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
@@ -273,22 +271,20 @@ struct grs_sorter {
   size_t xrbuf_bytes = 0;
   void* codec_buf = nullptr;       // presorted exchange: plan, block sizes / offsets, scan, co-ranks
   size_t codec_bytes = 0;
-  int sharded_exchange = 0;        // GRS_SHARDED_EXCHANGE: 0 auto, 1 partition-first, 2 presorted
+  // options (grs_set_option; defaults pick by size; nothing is read from the environment)
+  int sharded_exchange = 0;        // GRS_OPT_EXCHANGE: 0 auto, 1 partition-first, 2 presorted
   // last grs_sort_sharded call, with profiling on: events at call start / exchange start /
   // exchange end / call end, and the bytes that crossed the links (self part excluded)
   hipEvent_t xev[4] = {};
   bool xev_recorded = false;
   uint64_t x_sent = 0, x_recv = 0;
   int x_presorted = 0;
-  // tuning knobs read from the environment at grs_create (A/B measurements on one box)
-  int hist_grid_cap = 2048;        // GRS_HIST_GRID: cap of the round-1 histogram grid
-  int hist_variant = 2;            // GRS_HIST: 1 = grs_upfront_hist, 2 = grs_upfront_hist2
-  int hist2_grid = 0;              // GRS_HIST2_GRID: grs_upfront_hist2 grid (0 = auto)
-  int tile_mode = -1;              // GRS_TILE=big|small: force a tile shape (-1 = by size)
-  int pass_mode = 0;               // GRS_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
-  bool sharded_general = false;    // GRS_SHARDED=general: one rank takes the G-rank path too (tests)
-  bool sharded_contig = false;     // GRS_SHARDED_SEND=contig: histogram + contiguous send buckets (A/B, tests)
-  int xl_mode = 0;                 // GRS_XL: unset = by size, 1 = 48K two-round u32 tiles wherever big tiles run, 0 = never
+  int tile_mode = -1;              // GRS_OPT_TILE: -1 by size, 0 small, 1 big
+  int pass_mode = 0;               // GRS_OPT_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
+  bool sharded_general = false;    // GRS_OPT_SHARDED_PATH: one rank takes the G-rank path too
+  bool sharded_contig = false;     // GRS_OPT_SHARDED_SEND: histogram + contiguous send buckets
+  int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
+  int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
 };
 
 extern "C" {
@@ -386,9 +382,97 @@ size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
   return std::max(w, status_words_for((cap + part - 1) / part, 16));
 }
 
+// Status words per look-back buffer for the sorter's capacity and current options.
+size_t needed_status_words(const grs_sorter* s) {
+  const size_t cap = std::max<size_t>(s->capacity, 1);
+  const size_t radix = std::max<size_t>(size_t(1) << s->radix_bits, 16);
+  if (s->key_type == GRS_KEY_U32)
+    return s->pairs ? max_status_words<uint32_t, true>(s, cap, radix)
+                    : max_status_words<uint32_t, false>(s, cap, radix);
+  return s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
+                  : max_status_words<uint64_t, false>(s, cap, radix);
+}
+
 }  // namespace
 
 extern "C" {
+
+grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
+  if (!s) return set_err(GRS_EINVAL, "grs_set_option: NULL sorter");
+  auto bad = [&]() { return set_err(GRS_EINVAL, "grs_set_option: value out of range for option " +
+                                                    std::to_string(static_cast<int>(opt))); };
+  switch (opt) {
+    case GRS_OPT_TILE:
+      if (value < -1 || value > 1) return bad();
+      s->tile_mode = value;
+      break;
+    case GRS_OPT_XL:
+      if (value < -1 || value > 1) return bad();
+      s->xl_mode = value == -1 ? 0 : value == 1 ? 1 : 2;
+      break;
+    case GRS_OPT_PASS:
+      if (value != 0 && value != 4 && value != 6) return bad();
+      s->pass_mode = value;
+      break;
+    case GRS_OPT_RECORDS:
+      if (value < 0 || value > 2) return bad();
+      s->rec_mode = value;
+      break;
+    case GRS_OPT_RANK:
+      if (value < 0 || value > 1) return bad();
+      s->rank_mode = value == 1 ? 1 : s->probe_rank_mode;
+      break;
+    case GRS_OPT_SHARDED_PATH:
+      if (value < 0 || value > 1) return bad();
+      s->sharded_general = value == 1;
+      break;
+    case GRS_OPT_SHARDED_SEND:
+      if (value < 0 || value > 1) return bad();
+      s->sharded_contig = value == 1;
+      break;
+    case GRS_OPT_EXCHANGE:
+      if (value < 0 || value > 2) return bad();
+      s->sharded_exchange = value;
+      break;
+    default:
+      return set_err(GRS_EINVAL, "grs_set_option: unknown option");
+  }
+  // a pinned tile shape can need more look-back status words than the defaults sized
+  const size_t words = needed_status_words(s);
+  if (words > s->status_words) {
+    int prev = 0;
+    GRS_HIP(hipGetDevice(&prev));
+    GRS_HIP(hipSetDevice(s->device));
+    uint32_t* st = nullptr;
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&st), 2 * words * 4);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return set_err(GRS_ENOMEM, "grs_set_option: status buffer allocation failed");
+    }
+    if (s->status) (void)hipFree(s->status);
+    s->scratch_bytes += 2 * (words - s->status_words) * 4;
+    s->status = st;
+    s->status_words = words;
+  }
+  return GRS_OK;
+}
+
+grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
+  if (!s || !value) return set_err(GRS_EINVAL, "grs_get_option: NULL argument");
+  switch (opt) {
+    case GRS_OPT_TILE: *value = s->tile_mode; break;
+    case GRS_OPT_XL: *value = s->xl_mode == 0 ? -1 : s->xl_mode == 1 ? 1 : 0; break;
+    case GRS_OPT_PASS: *value = s->pass_mode; break;
+    case GRS_OPT_RECORDS: *value = s->rec_mode; break;
+    case GRS_OPT_RANK: *value = s->rank_mode; break;
+    case GRS_OPT_SHARDED_PATH: *value = s->sharded_general ? 1 : 0; break;
+    case GRS_OPT_SHARDED_SEND: *value = s->sharded_contig ? 1 : 0; break;
+    case GRS_OPT_EXCHANGE: *value = s->sharded_exchange; break;
+    default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
+  }
+  return GRS_OK;
+}
 
 grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
                       int with_u32_payload, int radix_bits, int device) {
@@ -415,30 +499,11 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   s->pairs = with_u32_payload ? 1 : 0;
   s->radix_bits = radix_bits;
   s->capacity = capacity;
-  s->rank_mode = device_rank_mode(device);
+  s->rank_mode = s->probe_rank_mode = device_rank_mode(device);
   (void)hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device);
-  if (const char* e = std::getenv("GRS_HIST_GRID")) s->hist_grid_cap = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("GRS_HIST")) s->hist_variant = std::atoi(e) == 1 ? 1 : 2;
-  if (const char* e = std::getenv("GRS_HIST2_GRID")) s->hist2_grid = std::max(0, std::atoi(e));
-  if (const char* e = std::getenv("GRS_RECORDS")) s->rec_mode = std::max(0, std::min(2, std::atoi(e)));
-  if (const char* e = std::getenv("GRS_TILE"))
-    s->tile_mode = std::strcmp(e, "big") == 0 ? 1 : std::strcmp(e, "small") == 0 ? 0 : -1;
-  if (const char* e = std::getenv("GRS_XL")) s->xl_mode = std::atoi(e) != 0 ? 1 : 2;
-  if (const char* e = std::getenv("GRS_SHARDED")) s->sharded_general = std::strcmp(e, "general") == 0;
-  if (const char* e = std::getenv("GRS_SHARDED_SEND")) s->sharded_contig = std::strcmp(e, "contig") == 0;
-  if (const char* e = std::getenv("GRS_SHARDED_EXCHANGE"))
-    s->sharded_exchange = std::strcmp(e, "partition") == 0 ? 1 : std::strcmp(e, "presorted") == 0 ? 2 : 0;
-  if (const char* e = std::getenv("GRS_PASS"))
-    s->pass_mode = std::strcmp(e, "v6") == 0 ? 6 : std::strcmp(e, "v4") == 0 ? 4 : 0;
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(capacity, 1);
-  const size_t radix = std::max<size_t>(size_t(1) << radix_bits, 16);
-  if (key_type == GRS_KEY_U32)
-    s->status_words = s->pairs ? max_status_words<uint32_t, true>(s, cap, radix)
-                               : max_status_words<uint32_t, false>(s, cap, radix);
-  else
-    s->status_words = s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
-                               : max_status_words<uint64_t, false>(s, cap, radix);
+  s->status_words = needed_status_words(s);
   grs_status st = GRS_OK;
   auto alloc = [&](void** p, size_t bytes) {
     if (st != GRS_OK) return;
@@ -603,21 +668,12 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   if ((r = mark()) != GRS_OK) return r;
   // zero histograms + tickets (the error word is sticky: only the checks clear it)
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
-  if (s->hist_variant == 1) {
-    // > n / 2^18 blocks keeps every 16-bit bank-private counter below 2^16 (HistLayout);
-    // grid ~ n / 2^17 between 512 and 2048 blocks (round-1 layout, kept for A/B)
-    const int want = std::min<int>(s->hist_grid_cap, std::max<int>(512, static_cast<int>(n >> 17)));
-    const int grid = std::max<int>((n >> 18) + 1, std::min<int>(want, (n + 4095) / 4096));
-    hipLaunchKernelGGL((grs::grs_upfront_hist<K, RB>), dim3(grid), dim3(GRS_HIST_BLOCK), 0,
-                       stream, src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
-                       static_cast<uint32_t>(words));
-    GRS_HIP(hipGetLastError());
-  } else {
+  {
     // grs_upfront_hist2: 2 blocks of 512 per CU; a multiple of the resident slots so the
     // grid-stride loop ends evenly, and > n >> kHist2GridShift blocks (16-bit counters)
     const int slots = 2 * s->cus;
     const int need = static_cast<int>(n >> grs::kHist2GridShift<K>) + 1;
-    int grid = s->hist2_grid > 0 ? s->hist2_grid : (n <= (1u << 25) ? s->cus : slots);
+    int grid = n <= (1u << 25) ? s->cus : slots;
     if (grid < need) grid = (need + slots - 1) / slots * slots;
     const bool full = begin_bit == 0 && end_bit == static_cast<int>(8 * sizeof(K));
     auto kern = full ? grs::grs_upfront_hist2<K, RB, true> : grs::grs_upfront_hist2<K, RB, false>;
@@ -1701,8 +1757,8 @@ grs_status run_sharded(grs_sorter* s, const K* keys, const uint32_t* vals, uint3
                        uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
                        int me, hipStream_t st) {
   if constexpr (sizeof(K) == 4 && !PAIRS) {
-    // presorted exchange: u32 keys without payload, up to 4 ranks (GRS_SHARDED_EXCHANGE=
-    // presorted | partition forces one).  It moves ~1 byte a key instead of 4 but adds the
+    // presorted exchange: u32 keys without payload, up to 4 ranks (GRS_OPT_EXCHANGE forces
+    // either).  It moves ~1 byte a key instead of 4 but adds the
     // encode and ceil(log2 G) merge rounds; measured on one MI355X at C4 it is
     // ahead at 2 and 4 ranks and level at 8.  The sorted shard is staged in the output, and
     // encoded words count in u32.

@@ -6,7 +6,7 @@
 // That is 130 dispatches and ~40 B of HBM traffic per key per bit.  libgrs re-derives the
 // same stable LSD sort for MI355X as:
 //
-//   grs_upfront_hist   (here) one read of the keys; LDS-privatised digit histograms of EVERY
+//   grs_upfront_hist2  (here) one read of the keys; LDS-privatised digit histograms of EVERY
 //                      pass (replaces K2 + K3a + K3b's role of counting digits)
 //   grs_onesweep_v4    (grs_pass.hpp) one launch per digit: rank, publish, look-back, reorder,
 //                      scatter (replaces K4's stable split and the scans feeding it)
@@ -167,130 +167,13 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 // clear/cw:   status buffer of pass 0, zeroed here (grid-stride) so no separate memset
 //             launch is needed.
 //
-// Bank-private counters: lane l adds into copy (l % COPIES) of the histogram, laid out so
-// that copy c lives entirely in LDS bank c.  The 32 lanes of one half-wave LDS access then
-// never collide (no bank conflicts, no same-address serialisation, whatever the key
-// distribution — with 4-bit digits 64 lanes share 16 counters).  Two digits share one
-// 32-bit word as 16-bit halves; a copy counts at most ceil(n / grid / COPIES) keys, which the
-// launch keeps below 2^16 (grid > n / 2^18, COPIES >= 8).  32 KB of LDS per block.
 // Counting always happens on 8-bit "super digits"; 4-bit passes (BASELINE C2) read their
 // counts off them: pass 2q's digit is the low nibble of super digit q, pass 2q+1's the high
-// nibble, so hist4[2q][d] = sum_h cnt8[q][16h + d] and hist4[2q+1][d] = sum_l cnt8[q][16d + l].
-// That is half the LDS atomics of counting 4-bit digits directly (4 instead of 8 per u32 key).
-template <typename K>
-struct HistLayout {
-  static constexpr int MAXQ = static_cast<int>(sizeof(K));  // super digits per key
-  static constexpr int PER_COPY = MAXQ * 128;                // words of one copy
-  static constexpr int COPIES = (8192 / PER_COPY) >= 32 ? 32 : (8192 / PER_COPY);
-  static constexpr int WORDS = PER_COPY * COPIES;
-  static_assert(COPIES >= 8, "16-bit counters need >= 8 copies");
-};
-
-template <typename K, int RB>
-__global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_upfront_hist(
-    const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
-    uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words) {
-  static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
-  using HL = HistLayout<K>;
-  constexpr int MAXQ = HL::MAXQ;
-  constexpr int COPIES = HL::COPIES;
-  __shared__ uint32_t s_hist[HL::WORDS];
-  __shared__ uint32_t s_red[RB == 4 ? MAXQ * 256 : 1];
-
-  const uint32_t t = threadIdx.x;
-  for (uint32_t i = t; i < HL::WORDS; i += GRS_HIST_BLOCK) s_hist[i] = 0;
-  // zero the first pass's look-back status words
-  for (uint32_t i = blockIdx.x * GRS_HIST_BLOCK + t; i < clear_words; i += gridDim.x * GRS_HIST_BLOCK)
-    clear[i] = 0;
-  __syncthreads();
-
-  const uint32_t copy = t & (COPIES - 1);
-  const int supers = (end_bit - begin_bit + 7) / 8;   // super digits covering the bit range
-  int shifts[MAXQ];
-  uint32_t masks[MAXQ];
-#pragma unroll
-  for (int q = 0; q < MAXQ; ++q) {
-    const int s = begin_bit + q * 8;
-    shifts[q] = s;
-    const int bits = (end_bit - s) < 8 ? (end_bit - s) : 8;
-    masks[q] = (q < supers && bits > 0) ? ((1u << bits) - 1u) : 0u;
-  }
-  auto count = [&](K k) {
-#pragma unroll
-    for (int q = 0; q < MAXQ; ++q) {
-      if (q < supers) {
-        const uint32_t d = digit_of(k, shifts[q], masks[q]);
-        atomicAdd(&s_hist[(q * 128 + (d >> 1)) * COPIES + copy], 1u << ((d & 1u) << 4));
-      }
-    }
-  };
-
-  constexpr int VEC = 16 / sizeof(K);  // keys per 16-byte load
-  using V = uint4;
-  // 16-B vector loads need a 16-B aligned base; otherwise everything takes the scalar tail
-  const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : n / VEC;
-  const V* kv = reinterpret_cast<const V*>(keys);
-  const uint32_t stride = gridDim.x * GRS_HIST_BLOCK;
-  uint32_t v = blockIdx.x * GRS_HIST_BLOCK + t;
-  for (; v + 3 * stride < nvec; v += 4 * stride) {   // 4 loads in flight per thread
-    V x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = kv[v + u * stride];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const K* kk = reinterpret_cast<const K*>(&x[u]);
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) count(kk[e]);
-    }
-  }
-  for (; v < nvec; v += stride) {
-    const V x = kv[v];
-    const K* kk = reinterpret_cast<const K*>(&x);
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) count(kk[e]);
-  }
-  // ragged tail (fewer than VEC keys)
-  // 64-bit index: i + stride can pass 2^32 when n is near GRS_MAX_N
-  for (uint64_t i = static_cast<uint64_t>(nvec) * VEC + blockIdx.x * GRS_HIST_BLOCK + t; i < n;
-       i += gridDim.x * GRS_HIST_BLOCK)
-    count(keys[i]);
-  __syncthreads();
-  // reduce the copies: count of super digit value d at position q
-  auto total8 = [&](uint32_t q, uint32_t d) {
-    const uint32_t* row = &s_hist[(q * 128 + (d >> 1)) * COPIES];
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < COPIES; ++k) c += (row[(k + t) & (COPIES - 1)] >> ((d & 1u) << 4)) & 0xFFFFu;
-    return c;
-  };
-  if constexpr (RB == 8) {
-    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 256); i += GRS_HIST_BLOCK) {
-      const uint32_t c = total8(i / 256, i % 256);
-      if (c) atomicAdd(&g_hist[i], c);
-    }
-  } else {
-    for (uint32_t i = t; i < static_cast<uint32_t>(supers * 256); i += GRS_HIST_BLOCK)
-      s_red[i] = total8(i / 256, i % 256);
-    __syncthreads();
-    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 16); i += GRS_HIST_BLOCK) {
-      const uint32_t p = i / 16, d = i % 16, q = p / 2;
-      const uint32_t* r8 = &s_red[q * 256];
-      uint32_t c = 0;
-#pragma unroll
-      for (int h = 0; h < 16; ++h) c += (p & 1u) ? r8[d * 16 + h] : r8[h * 16 + d];
-      if (c) atomicAdd(&g_hist[i], c);
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------------------
-// upfront histogram, issue-lean layout (grs_upfront_hist2)
-// ----------------------------------------------------------------------------------------
-//
-// grs_upfront_hist spends 6 VALU per key digit (shift, mask, two shifts for the 16-bit half
-// chosen by the digit's low bit, and-or, variable shift of the add value) and a scalar branch
-// per digit position; at 2^30 keys that issue, not HBM, sets its 0.91 ms.  Here the 16-bit
-// half is chosen by the POSITION's parity instead: super digits 2p and 2p+1 share the word
+// nibble, so hist4[2q][d] = sum_h cnt8[q][16h + d] and hist4[2q+1][d] = sum_l cnt8[q][16d + l]
+// (half the LDS atomics of counting 4-bit digits directly).
+// Round 1's layout chose the 16-bit half of a counter word by the digit's low bit: 6 VALU per
+// key digit and a scalar branch per digit position, and at 2^30 keys that issue, not HBM, set
+// its 0.91 ms.  Here the 16-bit half is chosen by the POSITION's parity instead: super digits 2p and 2p+1 share the word
 // of (pair p, digit value d), so the add value is a compile-time 1 or 0x10000 and a digit
 // costs v_bfe_u32 + v_lshl_add_u32 (+ the ds_add_u32, whose pair offset is an immediate).
 // Copy c of each counter sits in bank c (COPIES = 32 for u32 keys: every 32-lane LDS group
@@ -415,7 +298,7 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
       if (c) atomicAdd(&g_hist[i], c);
     }
   } else {
-    // 4-bit passes read their counts off the 8-bit super digits (see grs_upfront_hist)
+    // 4-bit passes read their counts off the 8-bit super digits (see above)
     constexpr int R = (MAXQ * 256 + HB - 1) / HB;
     uint32_t tot[R];
 #pragma unroll

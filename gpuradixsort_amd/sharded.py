@@ -81,7 +81,8 @@ class ShardedSorter:
 
     def __init__(self, capacity_local: int, key_bits: int = 32, pairs: bool = False,
                  radix_bits: int = 8, group=None, device: Optional[torch.device] = None,
-                 recv_slack: float = 1.25, comm: Optional[RcclComm] = None):
+                 recv_slack: float = 1.25, comm: Optional[RcclComm] = None,
+                 options: Optional[dict] = None):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = device
@@ -95,7 +96,7 @@ class ShardedSorter:
         self.cap = int(capacity_local)
         self.out_cap = max(int(self.cap * recv_slack), self.cap, 1)
         self.sorter = RadixSorter(self.out_cap, key_bits=key_bits, pairs=pairs,
-                                  radix_bits=radix_bits, device=device.index)
+                                  radix_bits=radix_bits, device=device.index, options=options)
         kdt = torch.uint32 if key_bits == 32 else torch.uint64
         self.out_k = torch.empty(self.out_cap, dtype=kdt, device=device)
         self.out_v = torch.empty(self.out_cap, dtype=torch.uint32, device=device) if pairs else None

@@ -10,7 +10,7 @@ from typing import Optional
 
 import torch
 
-from ._lib import GRS_KEY_U32, GRS_KEY_U64, check, grs_timing, lib
+from ._lib import GRS_KEY_U32, GRS_KEY_U64, OPTIONS, check, grs_timing, lib
 
 _KEY_TYPES = {torch.int32: GRS_KEY_U32, torch.uint32: GRS_KEY_U32,
               torch.int64: GRS_KEY_U64, torch.uint64: GRS_KEY_U64}
@@ -34,7 +34,8 @@ class RadixSorter:
     them (torch.int32 / torch.uint32 / torch.int64 / torch.uint64)."""
 
     def __init__(self, capacity: int, key_bits: int = 32, pairs: bool = False,
-                 radix_bits: int = 8, device: Optional[int] = None):
+                 radix_bits: int = 8, device: Optional[int] = None,
+                 options: Optional[dict] = None):
         L = lib()
         if device is None:
             device = torch.cuda.current_device()
@@ -50,6 +51,21 @@ class RadixSorter:
         check(L.grs_create(ctypes.byref(h), self.capacity, kt, int(self.pairs), self.radix_bits,
                            self.device), "grs_create")
         self._h = h
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
+
+    def set_option(self, name: str, value) -> None:
+        """Pin a kernel choice the defaults make by size (grs_set_option): name is one of
+        _lib.OPTIONS ("tile", "xl", "pass", "records", "rank", "sharded_path", "sharded_send",
+        "exchange"), value an int or one of that option's value names."""
+        opt, names = OPTIONS[name]
+        v = names[value] if isinstance(value, str) else int(value)
+        check(lib().grs_set_option(self._h, opt, v), f"grs_set_option({name}={value})")
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int()
+        check(lib().grs_get_option(self._h, OPTIONS[name][0], ctypes.byref(v)), "grs_get_option")
+        return v.value
 
     def close(self) -> None:
         if getattr(self, "_h", None):

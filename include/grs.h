@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GRS_VERSION 200 /* 2.0.0: v4 pass, 32-bit prefixes, sharded C-ABI */
+#define GRS_VERSION 300 /* 3.0.0: options API (no environment knobs) */
 
 typedef enum grs_status {
   GRS_OK = 0,
@@ -90,8 +90,8 @@ void grs_destroy(grs_sorter* s);
 size_t grs_scratch_bytes(const grs_sorter* s);
 
 /* Ranking used by this sorter's passes: 0 = lane-ordered LDS atomics (the default; probed on
- * the device at grs_create), 1 = wave64 ballot-match fallback (probe failed, or the
- * environment variable GRS_RANK=match was set at grs_create).  -1 for a NULL sorter. */
+ * the device at grs_create), 1 = wave64 ballot-match fallback (probe failed, or
+ * grs_set_option(GRS_OPT_RANK, 1)).  -1 for a NULL sorter. */
 int grs_rank_mode(const grs_sorter* s);
 
 /* At-scale check of the property the atomic ranking relies on (the lanes of one returning
@@ -103,6 +103,30 @@ int grs_rank_mode(const grs_sorter* s);
  * rank a ballot match computes independently.  *mismatches = the number that differ (0 on
  * MI355X).  Synchronises.  New with respect to the reference. */
 grs_status grs_lds_order_check(int device, int blocks, int items, unsigned long long* mismatches);
+
+/* Per-sorter options: they pin what the defaults choose by size (tile shape, pass kernel,
+ * record layout, ranking, the sharded exchange).  Tests pin every kernel variant through them
+ * and A/B measurements compare variants with them; the defaults are the measured best, and no
+ * option is ever read from the environment.  Set before the sorts they should affect (a pinned
+ * small tile shape may grow the look-back status buffer: GRS_ENOMEM if that fails). */
+typedef enum grs_option {
+  GRS_OPT_TILE = 1,          /* -1 by size (default), 0 small (256-thread) tiles, 1 big tiles */
+  GRS_OPT_XL = 2,            /* -1 by size (default), 0 never, 1 XL two-round tiles wherever big
+                                tiles run (8-bit digits) */
+  GRS_OPT_PASS = 3,          /* 0 by size (default), 4 one tile per workgroup (grs_onesweep_v4),
+                                6 persistent workgroups with next-tile prefetch (grs_onesweep_v6) */
+  GRS_OPT_RECORDS = 4,       /* u32 pairs at 8-bit digits: 0 two arrays every pass, 1 8-byte
+                                (key, value) records in the sorter's scratch, 2 (default) also
+                                split over the caller's arrays (even n, 8-byte aligned) */
+  GRS_OPT_RANK = 5,          /* 0 (default) the device probe's choice, 1 ballot-match ranking */
+  GRS_OPT_SHARDED_PATH = 6,  /* grs_sort_sharded on ONE rank: 0 (default) copy + local sort,
+                                1 the G-rank path (a one-GPU rehearsal of the exchange) */
+  GRS_OPT_SHARDED_SEND = 7,  /* partition-first exchange: 0 (default) G regions of n_local items
+                                where they fit, 1 bucket histogram + contiguous buckets */
+  GRS_OPT_EXCHANGE = 8       /* 0 by rank count (default), 1 partition-first, 2 presorted */
+} grs_option;
+grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
+grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);
 
 /* Name of the pass kernel a sort of n items launches ("grs_onesweep_v4" or, on small grids,
  * "grs_onesweep_v6"): what profiling and roofline reports attribute the pass time to. */
@@ -160,14 +184,14 @@ grs_status grs_partition_ranges(grs_sorter* s, const void* d_keys, const uint32_
  * sorted range of the global stable order, and the ranks' outputs concatenated in rank order
  * are the stable sort of the whole input.  Two exchanges, one stream each call:
  *  - presorted (u32 keys without payload, when out_capacity >= n_local; the default there
- *    for G <= 4 ranks, GRS_SHARDED_EXCHANGE=presorted forces it for more):
+ *    for G <= 4 ranks, GRS_OPT_EXCHANGE = 2 forces it for more):
  *    local grs_sort of the shard into d_keys_out -> regular samples of the sorted shard ->
  *    RCCL all-gather -> on-device splitters (ties broken by global index) -> bucket bounds in
  *    the sorted shard -> each bucket encoded as 256-key blocks of bit-packed deltas (about one
  *    byte per uniform key at 8 ranks) -> all-gather of the G x 2G (keys, words) matrix -> ONE
  *    host synchronisation -> grouped ncclSend / ncclRecv of the encoded words -> decode ->
  *    2-way merge rounds of the G received runs into d_keys_out (ties: source-rank order).
- *  - partition-first (payload, u64 keys, or G > 4; GRS_SHARDED_EXCHANGE=partition forces it):
+ *  - partition-first (payload, u64 keys, or G > 4; GRS_OPT_EXCHANGE = 1 forces it):
  *    samples
  *    -> splitters -> grs partition pass into G buckets -> all-gather of the G x G bucket
  *    counts -> ONE host synchronisation -> grouped ncclSend / ncclRecv of keys and payload ->

@@ -36,7 +36,7 @@ def test_version_and_status_strings():
     from gpuradixsort_amd import _lib
 
     L = _lib.lib()
-    assert L.grs_version() == 200
+    assert L.grs_version() == 300
     assert L.grs_status_string(0) == b"GRS_OK"
     assert L.grs_status_string(4) == b"GRS_ECAPACITY"
 
@@ -105,3 +105,17 @@ def test_presorted_exchange_steps_validate_without_a_device():
     assert L.grs_shard_decode_merge(None, fake, 2, wo, ln, fake, 10, None) == _lib.GRS_EINVAL
     t = _lib.grs_sharded_timing()
     assert L.grs_sharded_last_timing(None, ctypes.byref(t)) == _lib.GRS_EINVAL
+
+
+def test_options_api_without_device():
+    """grs_set_option / grs_get_option validate their arguments before touching a device: a
+    NULL sorter is GRS_EINVAL (the options replace round 2's environment knobs)."""
+    import ctypes
+
+    from gpuradixsort_amd._lib import OPTIONS, lib
+
+    L = lib()
+    v = ctypes.c_int()
+    for name, (opt, _) in OPTIONS.items():
+        assert L.grs_set_option(None, opt, 0) == 1, name
+        assert L.grs_get_option(None, opt, ctypes.byref(v)) == 1, name

@@ -135,12 +135,11 @@ def test_rank_mode_is_atomic_on_gfx950(gpu):
 @pytest.mark.parametrize("tile", ["big", "small"])
 @pytest.mark.parametrize("kb,pairs", [(32, False), (32, True), (64, False), (64, True)])
 def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
-    """GRS_TILE pins the big (1024-thread) or small (256-thread) tile shape whatever the size:
+    """Option tile pins the big (1024-thread) or small (256-thread) tile shape whatever the size:
     bit-exact across each shape's tile edges and look-back group edges (8 tiles), ragged
     last groups, both digit widths."""
     import gpuradixsort_amd as grs
 
-    monkeypatch.setenv("GRS_TILE", tile)
     # u64 pairs: 22K-pair tiles reordered in two rounds of 11K (t // 2 is the round edge)
     big = {(32, False): 36864, (32, True): 17408, (64, False): 17408, (64, True): 22528}
     small = {(32, False): 4096, (32, True): 2048, (64, False): 2048, (64, True): 1536}
@@ -149,8 +148,8 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
     dt = np.uint32 if kb == 32 else np.uint64
     sizes = (1, t // 2 - 1, t // 2 + 1, t - 1, t + 1, 8 * t - 1, 8 * t + 1, 8 * t * 9 + 3,
              17 * t + 5)
-    s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=8)
-    s4 = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=4)
+    s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=8, options={"tile": tile})
+    s4 = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs, radix_bits=4, options={"tile": tile})
     for n in sizes:
         keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
         keys[::31] = keys[0]   # ties across tiles
@@ -172,24 +171,22 @@ def test_tile_shapes(gpu, monkeypatch, tile, kb, pairs):
                                                 (32, True, 768 * 40, "1"), (32, True, 768 * 40, "0"),
                                                 (64, False, 768 * 44, "2")])
 def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
-    """GRS_XL=1 pins the two-round XL tiles (768 threads; LDS holds half the tile per round)
+    """Option xl=always pins the two-round XL tiles (768 threads; LDS holds half the tile per round)
     at every big-tile size: bit-exact across tile, round and look-back group edges (the
     library uses them from 32 tiles per CU).  u32 pairs: the passes write 8-byte (key, value)
-    records -- into the scratch, and (GRS_RECORDS=2, even n, 4 passes) split over the caller's
-    two arrays for the middle passes; GRS_RECORDS=1: the scratch only; 0: two arrays
+    records -- into the scratch, and (records=2, even n, 4 passes) split over the caller's
+    two arrays for the middle passes; records=1: the scratch only; 0: two arrays
     throughout; a 24-bit sort (3 passes) keeps two arrays and copies back."""
     import gpuradixsort_amd as grs
 
-    monkeypatch.setenv("GRS_XL", "1")
-    monkeypatch.setenv("GRS_TILE", "big")
-    monkeypatch.setenv("GRS_RECORDS", records)
     h = t // 2
     rng = np.random.default_rng(48 + kb + pairs)
     dt = np.uint32 if kb == 32 else np.uint64
     # odd and even sizes: split records need an even n
     sizes = (1, 2, h - 1, h, h + 1, t - 1, t, t + 1, t + h + 3, t + h + 4, 8 * t - 1, 8 * t,
              8 * t + 1, 8 * t * 5 + h + 7, 8 * t * 5 + h + 8)
-    s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs)
+    s = grs.RadixSorter(max(sizes), key_bits=kb, pairs=pairs,
+                        options={"xl": "always", "tile": "big", "records": int(records)})
     assert s.pass_kernel_for(max(sizes)) == "grs_onesweep_v4"
     for n in sizes:
         keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
@@ -222,21 +219,19 @@ def test_xl_tiles(gpu, monkeypatch, kb, pairs, t, records):
 def test_big_tile_record_passes(gpu, monkeypatch, records):
     """The one-round big-tile v4 pass with record flags (launch_rec kinds 1-4: 8-byte (key,
     value) records in the scratch, and for even n split over the caller's two arrays): the
-    library takes it between ~2^24 and ~2^28 u32 pairs.  GRS_XL=0 + GRS_TILE=big + GRS_PASS=v4
+    library takes it between ~2^24 and ~2^28 u32 pairs.  Options xl=never, tile=big, pass=v4
     pin it at test sizes; odd and even n (split records need an even n); payload == the
     stable permutation."""
     import gpuradixsort_amd as grs
 
-    monkeypatch.setenv("GRS_XL", "0")
-    monkeypatch.setenv("GRS_TILE", "big")
-    monkeypatch.setenv("GRS_PASS", "v4")
-    monkeypatch.setenv("GRS_RECORDS", records)
     t = 1024 * 17
     h = t // 2
     rng = np.random.default_rng(170 + int(records))
     sizes = (2, 3, h, h + 1, t, t + 1, 8 * t, 8 * t + 1, 8 * t * 3 + h + 7, 8 * t * 3 + h + 8,
              2_000_000, 2_000_001)
-    s = grs.RadixSorter(max(sizes), key_bits=32, pairs=True)
+    s = grs.RadixSorter(max(sizes), key_bits=32, pairs=True,
+                        options={"xl": "never", "tile": "big", "pass": "v4",
+                                 "records": int(records)})
     assert s.pass_kernel_for(max(sizes)) == "grs_onesweep_v4"
     for n in sizes:
         keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
@@ -262,16 +257,11 @@ def test_pairs_offset_views(gpu, monkeypatch, shape, offset):
     thresholds; payload == the stable permutation, and the elements before the view stay."""
     import gpuradixsort_amd as grs
 
-    if shape == "xl":
-        monkeypatch.setenv("GRS_XL", "1")
-    else:
-        monkeypatch.setenv("GRS_XL", "0")
-        monkeypatch.setenv("GRS_PASS", "v4")
-    monkeypatch.setenv("GRS_TILE", "big")
-    monkeypatch.setenv("GRS_RECORDS", "2")
+    opts = {"tile": "big", "records": "split"}
+    opts.update({"xl": "always"} if shape == "xl" else {"xl": "never", "pass": "v4"})
     rng = np.random.default_rng(90 + offset)
     n = 1_000_002
-    s = grs.RadixSorter(n, key_bits=32, pairs=True)
+    s = grs.RadixSorter(n, key_bits=32, pairs=True, options=opts)
     keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     keys[::31] = 12345
     perm = oracle.stable_argsort(keys)
@@ -306,20 +296,19 @@ def test_misaligned_u64_keys_rejected(gpu):
 
 
 def test_ballot_match_fallback(gpu, monkeypatch):
-    """GRS_RANK=match forces ballot-match ranking (the path taken if the LDS order probe
+    """Option rank=match forces ballot-match ranking (the path taken if the LDS order probe
     ever fails): same bit-exact results, both tile shapes."""
     import gpuradixsort_amd as grs
 
-    monkeypatch.setenv("GRS_RANK", "match")
     rng = np.random.default_rng(5)
     for tile in ("big", "small"):
-        monkeypatch.setenv("GRS_TILE", tile)
         for kb, pairs, rb in ((32, False, 8), (32, True, 4), (64, True, 8), (64, False, 4)):
             dt = np.uint32 if kb == 32 else np.uint64
             keys = rng.integers(0, np.iinfo(dt).max, 300_007, dtype=dt, endpoint=True)
             keys[::5] = 77
             perm = oracle.stable_argsort(keys)
-            s = grs.RadixSorter(keys.size, key_bits=kb, pairs=pairs, radix_bits=rb)
+            s = grs.RadixSorter(keys.size, key_bits=kb, pairs=pairs, radix_bits=rb,
+                                options={"rank": "match", "tile": tile})
             assert s.rank_mode == "match"
             k = to_dev(keys, gpu)
             v = to_dev(np.arange(keys.size, dtype=np.uint32), gpu) if pairs else None
@@ -334,15 +323,13 @@ def test_ballot_match_fallback(gpu, monkeypatch):
 @pytest.mark.parametrize("kb,pairs,rb", [(32, False, 8), (32, True, 8), (64, False, 8),
                                           (64, True, 8), (32, False, 4), (64, True, 4)])
 def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb):
-    """GRS_PASS=v6: the persistent big-tile pass (grs_onesweep_v6: resident workgroups loop
+    """Option pass=v6: the persistent big-tile pass (grs_onesweep_v6: resident workgroups loop
     over tickets, the next tile's loads issued behind the reorder) gives the same bit-exact
     results across tile edges, for every key/payload type and both digit widths (u64 pairs at
     8-bit digits keep the two-round v4 pass, whose second round needs the registers the
     prefetch would take)."""
     import gpuradixsort_amd as grs
 
-    monkeypatch.setenv("GRS_PASS", "v6")
-    monkeypatch.setenv("GRS_TILE", "big")
     rng = np.random.default_rng(11 + kb + pairs + rb)
     dt = np.uint32 if kb == 32 else np.uint64
     for n in (1, 16383, 32769, 36865, 8 * 36864 + 1, 1_000_003, 3 * 1024 * 1024 + 7):
@@ -350,7 +337,8 @@ def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb):
         keys[::7] = np.iinfo(dt).max
         keys[1::13] = 3
         perm = oracle.stable_argsort(keys)
-        s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb)
+        s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb,
+                            options={"pass": "v6", "tile": "big"})
         k = to_dev(keys, gpu)
         v = to_dev(np.arange(n, dtype=np.uint32), gpu) if pairs else None
         s.sort(k, v)

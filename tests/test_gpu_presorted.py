@@ -149,14 +149,14 @@ def test_presorted_world1_empty_and_tiny(gpu, monkeypatch):
 
     from gpuradixsort_amd.sharded import RcclComm, ShardedSorter
 
-    monkeypatch.setenv("GRS_SHARDED", "general")
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
         comm = RcclComm(device=gpu.index)
-        s = ShardedSorter(5000, key_bits=32, device=gpu, comm=comm)
+        s = ShardedSorter(5000, key_bits=32, device=gpu, comm=comm,
+                          options={"sharded_path": "general"})
         rng = np.random.default_rng(2)
         for n in (0, 1, 255, 256, 257, 4999):
             keys = rng.integers(0, 2**32, 5000, dtype=np.uint64).astype(np.uint32)

@@ -38,21 +38,22 @@ def world1(gpu):
                                                       (64, True, "uniform"), (64, False, "ties"),
                                                       (32, True, "all_equal")])
 def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pairs, dist_name):
-    """path "general": GRS_SHARDED=general makes the one-rank call take the G-rank path
+    """path "general": option sharded_path=general makes the one-rank call take the G-rank path
     (samples, all-gathers, device splitters, partition into per-bucket regions of the send
     buffer, bucket sizes from the look-back, count matrix, host sync, grouped send/recv with
     the self copy, local sort) -- u32 keys without payload take the presorted exchange there
     (local sort, encode, exchange of encoded words, decode + merge) unless "general_partition"
     forces the partition-first one; "general_contig": partition-first with the bucket histogram
-    and contiguous send buckets (GRS_SHARDED_SEND=contig); "one_rank": the copy + local sort."""
+    and contiguous send buckets (sharded_send=contig); "one_rank": the copy + local sort."""
     from gpuradixsort_amd.sharded import ShardedSorter
 
+    opts = {}
     if path.startswith("general"):
-        monkeypatch.setenv("GRS_SHARDED", "general")
+        opts["sharded_path"] = "general"
     if path == "general_contig":
-        monkeypatch.setenv("GRS_SHARDED_SEND", "contig")
+        opts["sharded_send"] = "contig"
     if path in ("general_contig", "general_partition"):
-        monkeypatch.setenv("GRS_SHARDED_EXCHANGE", "partition")
+        opts["exchange"] = "partition"
 
     rng = np.random.default_rng(key_bits + pairs)
     dt = np.uint32 if key_bits == 32 else np.uint64
@@ -63,7 +64,7 @@ def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pair
     elif dist_name == "all_equal":
         keys[:] = 9
     perm = oracle.stable_argsort(keys)
-    s = ShardedSorter(n, key_bits=key_bits, pairs=pairs, device=gpu, comm=world1)
+    s = ShardedSorter(n, key_bits=key_bits, pairs=pairs, device=gpu, comm=world1, options=opts)
     k = torch.from_numpy(keys).to(gpu)
     v = torch.arange(n, dtype=torch.int64, device=gpu).to(torch.uint32) if pairs else None
     for _ in range(2):   # repeated calls reuse the sorter's scratch
@@ -90,12 +91,11 @@ def test_sharded_prefix_n(gpu, world1, monkeypatch, path):
     sort), and the tail of the input tensor is left alone."""
     from gpuradixsort_amd.sharded import ShardedSorter
 
-    if path == "general":
-        monkeypatch.setenv("GRS_SHARDED", "general")
+    opts = {"sharded_path": "general"} if path == "general" else {}
     rng = np.random.default_rng(9)
     total, n = 300_000, 123_457
     keys = rng.integers(0, 2**32, total, dtype=np.uint64).astype(np.uint32)
-    s = ShardedSorter(total, key_bits=32, pairs=True, device=gpu, comm=world1)
+    s = ShardedSorter(total, key_bits=32, pairs=True, device=gpu, comm=world1, options=opts)
     k = torch.from_numpy(keys).to(gpu)
     v = torch.arange(total, dtype=torch.int64, device=gpu).to(torch.uint32)
     ko, vo = s.sort(k, v, n=n)
@@ -113,9 +113,9 @@ def test_records_then_sharded_scratch(gpu, world1, monkeypatch):
     import gpuradixsort_amd as grs
     from gpuradixsort_amd.sharded import ShardedSorter
 
-    monkeypatch.setenv("GRS_SHARDED", "general")
     n = 200_003
-    s = ShardedSorter(n, key_bits=32, pairs=True, device=gpu, comm=world1)
+    s = ShardedSorter(n, key_bits=32, pairs=True, device=gpu, comm=world1,
+                      options={"sharded_path": "general"})
     rs = grs.RecordSort(n, key_bits=32)
     rs._sorter.close()
     rs._sorter = s.sorter                      # one libgrs sorter for both entry points

@@ -6,7 +6,6 @@
 #include <type_traits>
 
 #include "../gpuradixsort_amd/csrc/grs_pass.hpp"
-#include "r1_kernels.hpp"
 
 namespace {
 
@@ -346,30 +345,6 @@ int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* ou
     V(1024, 64, 1, 1024) V(1024, 64, 1, 1040) V(1024, 64, 1, 1032) V(768, 84, 1, 1024)
     V(512, 128, 1, 1024) V(512, 128, 1, 1040) V(512, 128, 1, 1032)
 #undef V
-    default:
-      return -1;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// round-1 library pass (grs_onesweep_ar) for reference: kb, pairs, block, items, dbg
-int lab2_ar(int kb, int pairs, int block, int items, int dbg, const void* in, void* out,
-            const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
-            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = ((((long)kb * 2 + pairs) * 10000 + block) * 100 + items) * 100 + dbg;
-  switch (code) {
-#define A(KB, P, B, I, D)                                                                     \
-  case ((((long)KB * 2 + P) * 10000 + B) * 100 + I) * 100 + D: {                                \
-    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                              \
-    const uint32_t tiles = (n + B * I - 1) / (B * I);                                         \
-    hipLaunchKernelGGL((grs::grs_onesweep_ar<KT, P != 0, 8, B, I, D>), dim3(tiles), dim3(B),   \
-                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                           \
-                       grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err);         \
-  } break;
-    A(32, 0, 512, 72, 0) A(32, 0, 512, 72, 8) A(32, 1, 512, 36, 0) A(64, 0, 512, 36, 0)
-    A(64, 1, 512, 24, 0)
-#undef A
     default:
       return -1;
   }

@@ -1,9 +1,9 @@
 """Round-2 kernel laboratory driver (tools/lab2.hip): interleaved timing of pass variants.
 
 python tools/lab2.py [--n N] [--rounds R] [--check] [--copy]
-       [--variants v4:kb:pairs:block:items:minw:opt,ar:kb:pairs:block:items:dbg,...]
+       [--variants v4:kb:pairs:block:items:minw:opt,v6:kb:pairs:block:items:minw:opt:grid,...]
 Prints median / min ms and algorithmic GB/s (2 x (key + payload) bytes per key) per variant;
-variants with the stamp bit (v4 opt & 8, ar dbg & 8) also print mean cycles per phase.
+variants with the stamp bit (opt & 8) also print mean cycles per phase.
 """
 import argparse
 import ctypes
@@ -77,7 +77,7 @@ def main():
         elif kind == "v6":   # v6:kb:pairs:block:items:minw:opt:grid
             rc = L.lab2_v6(kb, pairs, block, items, v[5], v[6], v[7], *args)
         else:
-            rc = L.lab2_ar(kb, pairs, block, items, v[5], *args)
+            raise SystemExit(f"unknown variant kind {kind}")
         assert rc == 0, (v, rc)
 
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -183,7 +183,7 @@ def main():
         print(f"{':'.join(str(x) for x in v):28s} median {med:8.4f} ms  min {mn:8.4f}  "
               f"{alg / med / 1e6:8.1f} GB/s", flush=True)
     for v in variants:
-        stamped = (v[0] in ("v4", "r4", "r6") and v[6] & 8) or (v[0] == "ar" and v[5] & 8) or (v[0] == "v6" and v[6] & 8)
+        stamped = v[0] in ("v4", "v6", "r4", "r6") and v[6] & 8
         if not stamped:
             continue
         err.zero_()
@@ -194,19 +194,13 @@ def main():
         torch.cuda.synchronize()
         tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
-        if v[0] in ("v4", "v6", "r4", "r6"):
-            m = a_[:, :6].mean(0)
-            d = np.diff(np.concatenate([[0.0], m]))
-            names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
-                     "reorder+lookback+B4", "store+drain"]
-            print(f"stamps {v}: " + ", ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d))
-                  + f"  total={m[5]:.0f}  (p90 reorder+lb {np.percentile(a_[:, 4] - a_[:, 3], 90):.0f})",
-                  flush=True)
-        else:
-            m = a_[:, :7].mean(0)
-            print(f"stamps {v}: ticket+load={m[6]:.0f} rank+B1={m[1]-m[0]:.0f} scan+B2={m[2]-m[1]:.0f} "
-                  f"lookback+B3={m[3]-m[2]:.0f} reorder+B4={m[4]-m[3]:.0f} store+drain={m[5]-m[4]:.0f} "
-                  f"total={m[5]:.0f}", flush=True)
+        m = a_[:, :6].mean(0)
+        d = np.diff(np.concatenate([[0.0], m]))
+        names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
+                 "reorder+lookback+B4", "store+drain"]
+        print(f"stamps {v}: " + ", ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d))
+              + f"  total={m[5]:.0f}  (p90 reorder+lb {np.percentile(a_[:, 4] - a_[:, 3], 90):.0f})",
+              flush=True)
         starts = a_[:, 7] * 256.0
         span = (starts.max() - starts.min())
         print(f"   tiles={tiles} start spread {span:.0f} cycles", flush=True)

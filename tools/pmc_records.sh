@@ -1,10 +1,10 @@
 #!/bin/bash
-# PMC write / fetch bytes of the C3 pass kernels with and without record passes (GRS_RECORDS).
+# PMC write / fetch bytes of the C3 pass kernels with and without record passes (--opt records).
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for r in 0 2; do
   for c in WRITE_SIZE FETCH_SIZE; do
-    GRS_RECORDS=$r timeout -s KILL 120 rocprofv3 --pmc $c -d gpurun_out/pmcrec_${r}_${c} -o p --output-format csv -- python3 bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcrec_${r}_${c}.log 2>&1 || exit $?
+    timeout -s KILL 120 rocprofv3 --pmc $c -d gpurun_out/pmcrec_${r}_${c} -o p --output-format csv -- python3 bench.py --opt records=$r --config c3 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcrec_${r}_${c}.log 2>&1 || exit $?
   done
 done
 python3 - <<'PY'
