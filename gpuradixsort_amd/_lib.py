@@ -116,6 +116,10 @@ SIGNATURES = [
     ("grs_key_transform", c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p]),
     ("grs_sort_records", c_int, [c_void_p, c_void_p, c_size_t, c_size_t, POINTER(grs_key_extract),
                                  c_void_p]),
+    ("grs_records_key_buffers", c_int, [c_void_p, c_size_t, c_size_t, POINTER(c_void_p),
+                                        POINTER(c_void_p)]),
+    ("grs_sort_records_by_keys", c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p,
+                                         c_void_p]),
     ("grs_scan_scratch_bytes", c_size_t, [c_size_t]),
     ("grs_exclusive_scan_u32", c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_size_t,
                                        c_void_p]),

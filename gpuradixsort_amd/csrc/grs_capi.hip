@@ -2021,6 +2021,71 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
   return GRS_OK;
 }
 
+// The record sort's scratch (first use, grown on demand): n keys | n indices | n records.
+static grs_status records_scratch(grs_sorter* s, size_t n, size_t record_bytes, void** keys,
+                                  uint32_t** idx, void** copy) {
+  const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t need = al(n * kb) + al(n * 4) + al(n * record_bytes);
+  if (s->rec_bytes < need) {
+    if (s->rec_buf) (void)hipFree(s->rec_buf);
+    s->rec_buf = nullptr;
+    s->rec_bytes = 0;
+    if (hipMalloc(&s->rec_buf, need) != hipSuccess) {
+      (void)hipGetLastError();
+      return set_err(GRS_ENOMEM, "grs_sort_records: scratch allocation failed");
+    }
+    s->rec_bytes = need;
+  }
+  char* b = static_cast<char*>(s->rec_buf);
+  *keys = b;
+  *idx = reinterpret_cast<uint32_t*>(b + al(n * kb));
+  *copy = b + al(n * kb) + al(n * 4);
+  return GRS_OK;
+}
+
+grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes, void** d_keys,
+                                   uint32_t** d_idx) {
+  if (!s || !d_keys || !d_idx) return set_err(GRS_EINVAL, "grs_records_key_buffers: NULL argument");
+  if (!s->pairs) return set_err(GRS_EINVAL, "grs_records_key_buffers: needs a sorter created with a payload");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_records_key_buffers: n exceeds capacity");
+  if (record_bytes == 0 || record_bytes > 0xFFFFFFFFull)
+    return set_err(GRS_EINVAL, "grs_records_key_buffers: bad record size");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  void* copy = nullptr;
+  const grs_status r = records_scratch(s, std::max<size_t>(n, 1), record_bytes, d_keys, d_idx, &copy);
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_sort_records_by_keys(grs_sorter* s, void* d_records, size_t n, size_t record_bytes,
+                                    void* d_keys, uint32_t* d_idx, void* stream) {
+  if (!s) return set_err(GRS_EINVAL, "grs_sort_records_by_keys: NULL sorter");
+  if (!s->pairs) return set_err(GRS_EINVAL, "grs_sort_records_by_keys: needs a sorter created with a payload");
+  if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_records_by_keys: n exceeds capacity");
+  if (record_bytes == 0 || record_bytes > 0xFFFFFFFFull)
+    return set_err(GRS_EINVAL, "grs_sort_records_by_keys: bad record size");
+  if (n == 0) return GRS_OK;
+  if (!d_records || !d_keys || !d_idx) return set_err(GRS_EINVAL, "grs_sort_records_by_keys: NULL buffer");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  void* keys = nullptr;
+  uint32_t* idx = nullptr;
+  void* copy = nullptr;
+  grs_status r = records_scratch(s, n, record_bytes, &keys, &idx, &copy);
+  // the caller's keys / indices may live in the scratch (grs_records_key_buffers) or anywhere
+  if (r == GRS_OK) r = grs_sort(s, d_keys, d_idx, n, stream);                     // stable pairs
+  if (r == GRS_OK) r = grs_gather_records(d_records, copy, d_idx, n, record_bytes, stream);  // K5
+  if (r == GRS_OK && hipMemcpyAsync(d_records, copy, n * record_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_records_by_keys: copy back");
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
 grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t record_bytes,
                             const grs_key_extract* key, void* stream) {
   if (!s || !key) return set_err(GRS_EINVAL, "grs_sort_records: NULL argument");
@@ -2039,24 +2104,10 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
-  const size_t need = al(n * kb) + al(n * 4) + al(n * record_bytes);
-  grs_status r = GRS_OK;
-  if (s->rec_bytes < need) {
-    if (s->rec_buf) (void)hipFree(s->rec_buf);
-    s->rec_buf = nullptr;
-    s->rec_bytes = 0;
-    if (hipMalloc(&s->rec_buf, need) != hipSuccess) {
-      (void)hipGetLastError();
-      r = set_err(GRS_ENOMEM, "grs_sort_records: scratch allocation failed");
-    } else {
-      s->rec_bytes = need;
-    }
-  }
-  char* b = static_cast<char*>(s->rec_buf);
-  void* keys = b;
-  uint32_t* idx = reinterpret_cast<uint32_t*>(b + al(n * kb));
-  void* copy = b + al(n * kb) + al(n * 4);
+  void* keys = nullptr;
+  uint32_t* idx = nullptr;
+  void* copy = nullptr;
+  grs_status r = records_scratch(s, n, record_bytes, &keys, &idx, &copy);
   const grs::KeyExtract kx{key->kind, key->offset, key->transform,
                            {key->lo[0], key->lo[1], key->lo[2]}, {key->hi[0], key->hi[1], key->hi[2]}};
   if (r == GRS_OK) {   // K1: one fused pre-pass, key + index

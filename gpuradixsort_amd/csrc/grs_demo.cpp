@@ -6,6 +6,9 @@
 //        the reference's stated purpose (ParallelSort.h:13-31): N Particle structs sorted by the
 //        Morton code of their position through ParallelSort(RecordSsbo<Particle>, MortonKey);
 //        verified against a host std::stable_sort by the same code
+//        grs_demo distance [N] [seed]
+//        a user-defined key functor (ParallelSortBy<Particle, DistanceKey>): particles by their
+//        float distance from a point, through grs::OrderedBits, verified the same way
 // The reference's std::random_shuffle (main.cpp:125) is replaced by a seeded Fisher-Yates
 // over splitmix64 so the run is reproducible; verification strengthens the reference's
 // adjacent-order check (ParallelSort.cpp:336-352) to "output == 0..N-1".
@@ -83,7 +86,59 @@ static int particles(unsigned n, uint64_t seed) {
   return bad ? 1 : 0;
 }
 
+// A user key functor: squared distance of the particle from a point, as order-preserving bits
+// (ties are common: positions are quantised to 1/64, so stability is exercised).
+struct DistanceKey {
+  float c[3];
+  __host__ __device__ uint32_t operator()(const Particle& p) const {
+    float d = 0.0f;
+    for (int a = 0; a < 3; ++a) {
+      const float x = p.pos[a] - c[a];
+      d = __builtin_fmaf(x, x, d);
+    }
+    return grs::OrderedBits(d);
+  }
+};
+
+static int distance(unsigned n, uint64_t seed) {
+  std::vector<Particle> host(n);
+  for (unsigned i = 0; i < n; ++i) {
+    for (int a = 0; a < 3; ++a) {
+      host[i].pos[a] = static_cast<float>(static_cast<int>(splitmix64(seed) % 129) - 64) / 64.0f;
+      host[i].vel[a] = -static_cast<float>(a);
+    }
+    host[i].id = i;
+  }
+  auto buf = std::make_shared<RecordSsbo<Particle>>(n);
+  buf->Upload(host);
+  const DistanceKey key{{0.25f, -0.5f, 0.125f}};
+  ParallelSortBy<Particle, DistanceKey> ps(buf, key);
+  ps.Sort();
+  ps.Sort();   // sorting sorted records again must not move them (stability)
+  const std::vector<Particle> out = buf->Download();
+  std::vector<uint32_t> code(n);
+  for (unsigned i = 0; i < n; ++i) code[i] = key(host[i]);   // the same functor on the host
+  std::vector<unsigned> perm(n);
+  std::iota(perm.begin(), perm.end(), 0u);
+  std::stable_sort(perm.begin(), perm.end(), [&](unsigned a, unsigned b) { return code[a] < code[b]; });
+  unsigned bad = 0;
+  for (unsigned i = 0; i < n; ++i)
+    bad += std::memcmp(&out[i], &host[perm[i]], sizeof(Particle)) != 0;
+  std::printf("grs_demo distance n=%u sorted=%s mismatches=%u\n", n, bad ? "NO" : "yes", bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "distance") == 0) {
+    const unsigned n = argc > 2 ? static_cast<unsigned>(std::strtoul(argv[2], nullptr, 10)) : 100000u;
+    const uint64_t seed = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 1;
+    try {
+      return distance(n, seed);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "grs_demo: %s\n", e.what());
+      return 2;
+    }
+  }
   if (argc > 1 && std::strcmp(argv[1], "particles") == 0) {
     const unsigned n = argc > 2 ? static_cast<unsigned>(std::strtoul(argv[2], nullptr, 10)) : 100000u;
     const uint64_t seed = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 1;

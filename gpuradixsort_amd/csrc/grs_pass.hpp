@@ -141,7 +141,7 @@ struct Lb3 {
 };
 
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
-          bool IDX = false, int ROUNDS = 1>
+          bool IDX = false, int ROUNDS = 1, bool ALIGN = false>
 struct V4Smem {
   static constexpr int RADIX = 1 << RB;
   static constexpr int WAVES = BLOCK / GRS_WAVE;
@@ -150,7 +150,7 @@ struct V4Smem {
   // per-wave digit counters -> tile position of (wave, digit); CNT16: 16-bit, two per word
   uint32_t cnt[WAVES * RADIX / (CNT16 ? 2 : 1)];
   uint32_t base[RADIX];         // global destination of tile position 0 of digit d
-  uint32_t wsum[2 * WAVES];     // wave totals of the two digit scans
+  uint32_t wsum[3 * WAVES];     // wave totals of the digit scans
   uint32_t ticket;
   uint32_t next;                // persistent kernel: the next tile's ticket
   alignas(16) K keys[LTILE];
@@ -158,10 +158,16 @@ struct V4Smem {
   // indexed digits (partition): tile-local start of every digit, from which the store phase
   // reads off the digit of a reordered position (the key alone does not determine it)
   uint32_t lstart[IDX ? RADIX + 1 : 1];
+  // destination-aligned stores (OPT 65536): per digit the first store chunk, tile-local run
+  // start and run length; jsplit: the first chunk of the second round (two-round tiles)
+  uint32_t cstart[ALIGN ? RADIX + 1 : 1];
+  uint32_t lst[ALIGN ? RADIX : 1];
+  uint32_t rlen[ALIGN ? RADIX : 1];
+  uint32_t jsplit;
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
-                         (OPT & 1024) != 0 ? 2 : 1>;
+                         (OPT & 1024) != 0 ? 2 : 1, (OPT & 65536) != 0 && !DigitF::kIndexed>;
 
 // OPT bits (lab ablations; the library uses OPT = 0):
 //   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
@@ -180,6 +186,13 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //   16384 / 32768: the records read / written are SPLIT over two buffers: records [0, n/2)
 //       in keys_in / keys_out and [n/2, n) in vals_in / vals_out (n even; the caller's two
 //       4n-byte arrays hold n records that way)
+//   65536 destination-aligned stores: each wave-instruction writes one 64-item chunk of ONE
+//       digit run, aligned in the destination (item dst of a run goes to lane dst % 64), so a
+//       run of L items costs ceil(((D % 64) + L) / 64) instructions that touch only its own
+//       lines, instead of 64-item slices of the tile that start anywhere in a line and cut
+//       across runs (every slice then half-writes a line at each end)
+//   131072 speculative tile load (grs_onesweep_v4): tile blockIdx.x is loaded while the ticket
+//       is in flight; a ticket that differs reloads
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
@@ -366,7 +379,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   lds_barrier();  // B1
   V4_STAMP(1);
 
-  uint32_t tile_cnt = 0, publish = 0, gold = 0, lstart = 0, gstart = 0;
+  constexpr bool ALIGN = (OPT & 65536) != 0 && !IDX;
+  uint32_t tile_cnt = 0, publish = 0, gold = 0, lstart = 0, gstart = 0, cstart = 0, cbound = 0;
   if (t < static_cast<uint32_t>(RADIX)) {
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) {
@@ -382,12 +396,21 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   if (w < static_cast<uint32_t>(DW)) {
     const uint32_t li = wave_scan_dpp(tile_cnt);
     const uint32_t gi = wave_scan_dpp(gh);
+    uint32_t ci = 0;
+    if constexpr (ALIGN) {
+      // store chunks of this digit's run, bounded before its destination alignment is known
+      // (the look-back): ceil((63 + L) / 64) >= ceil((D % 64 + L) / 64) for any D
+      cbound = publish ? (publish + 126u) >> 6 : 0u;
+      ci = wave_scan_dpp(cbound);
+    }
     if (lane == GRS_WAVE - 1) {
       sm.wsum[w] = li;
       sm.wsum[WAVES + w] = gi;
+      if constexpr (ALIGN) sm.wsum[2 * WAVES + w] = ci;
     }
     lstart = li - tile_cnt;
     gstart = gi - gh;
+    cstart = ci - cbound;
   }
   lds_barrier();  // B2
   V4_STAMP(2);
@@ -397,6 +420,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     for (uint32_t ww = 0; ww < w; ++ww) {
       lstart += sm.wsum[ww];
       gstart += sm.wsum[WAVES + ww];
+      if constexpr (ALIGN) cstart += sm.wsum[2 * WAVES + ww];
+    }
+    if constexpr (ALIGN) {
+      sm.cstart[t] = cstart;
+      if (t == static_cast<uint32_t>(RADIX - 1)) sm.cstart[RADIX] = cstart + cbound;
+      sm.lst[t] = lstart;
+      sm.rlen[t] = publish;
     }
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
@@ -452,6 +482,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
     }
     sm.base[t] = gstart + prefix - lstart;
+    if constexpr (ALIGN && ROUNDS > 1) {
+      // the run holding tile position LTILE (the round boundary) names the first chunk of
+      // round 2: the chunk of that position (it is stored partly in each round)
+      if (t == 0) sm.jsplit = 0xFFFFFFFFu;
+      const uint32_t D = gstart + prefix;
+      if (lstart <= static_cast<uint32_t>(LTILE) && static_cast<uint32_t>(LTILE) < lstart + publish)
+        sm.jsplit = cstart + ((D + (LTILE - lstart)) - (D & ~63u)) / 64u;
+    }
   }
   lds_barrier();  // B4
   V4_STAMP(4);
@@ -461,12 +499,66 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // its digit only moves forward through the tile-local digit starts (at most RADIX - 1 steps
   // per tile, over empty digits too).
   uint32_t dcur = 0;
+  auto put = [&](uint32_t dst, K kk, uint32_t i) {
+    if constexpr ((OPT & 8192) != 0) {
+      static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
+      const uint2 r = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
+      if constexpr ((OPT & 32768) != 0) {   // split records: [n/2, n) in vals_out
+        if (dst >= n / 2) reinterpret_cast<uint2*>(vals_out)[dst - n / 2] = r;
+        else reinterpret_cast<uint2*>(keys_out)[dst] = r;
+      } else {
+        reinterpret_cast<uint2*>(keys_out)[dst] = r;
+      }
+    } else {
+      keys_out[dst] = kk;
+      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+    }
+  };
   auto dig_at = [&](uint32_t i, K kk) -> uint32_t {
     if constexpr (IDX) {
       while (i >= sm.lstart[dcur + 1]) ++dcur;
       return dcur;
     } else {
       return dig(kk);
+    }
+  };
+  // destination-aligned chunks: wave w takes a contiguous range of chunk indices of this round
+  // and walks the digits forward through cstart (wave-uniform values)
+  auto store_chunks = [&](uint32_t jbeg, uint32_t jend, uint32_t r0, uint32_t r1) {
+    const uint32_t per = (jend - jbeg + WAVES - 1) / WAVES;
+    uint32_t j = jbeg + w * per;
+    const uint32_t je = min(jend, j + per);
+    if (j >= je) return;
+    // largest d with cstart[d] <= j (empty digits share the next digit's start)
+    uint32_t lo = 0, hi = RADIX;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sm.cstart[mid] <= j) lo = mid; else hi = mid;
+    }
+    uint32_t d = __builtin_amdgcn_readfirstlane(lo);
+    uint32_t cs = __builtin_amdgcn_readfirstlane(sm.cstart[d]);
+    uint32_t cn = __builtin_amdgcn_readfirstlane(sm.cstart[d + 1]);
+    uint32_t ls = __builtin_amdgcn_readfirstlane(sm.lst[d]);
+    uint32_t ln = __builtin_amdgcn_readfirstlane(sm.rlen[d]);
+    uint32_t D = __builtin_amdgcn_readfirstlane(sm.base[d]) + ls;
+    for (; j < je; ++j) {
+      while (j >= cn) {
+        ++d;
+        cs = cn;
+        cn = __builtin_amdgcn_readfirstlane(sm.cstart[d + 1]);
+        ls = __builtin_amdgcn_readfirstlane(sm.lst[d]);
+        ln = __builtin_amdgcn_readfirstlane(sm.rlen[d]);
+        D = __builtin_amdgcn_readfirstlane(sm.base[d]) + ls;
+      }
+      const uint32_t A = (D & ~63u) + 64u * (j - cs);
+      if (A >= D + ln) continue;   // past the run (the chunk bound over-counts by up to one)
+      const uint32_t dst = A + lane;
+      const uint32_t off = dst - D;   // wraps below D: out of the run
+      const uint32_t pos = ls + off;
+      if (off < ln && pos >= r0 && pos < r1) {
+        const uint32_t i = pos - r0;
+        put(dst, sm.keys[i], i);
+      }
     }
   };
 #pragma unroll
@@ -494,21 +586,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       }
     }
     const uint32_t roff = static_cast<uint32_t>(rr * LTILE);
-    auto put = [&](uint32_t dst, K kk, uint32_t i) {
-      if constexpr ((OPT & 8192) != 0) {
-        static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
-        const uint2 r = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
-        if constexpr ((OPT & 32768) != 0) {   // split records: [n/2, n) in vals_out
-          if (dst >= n / 2) reinterpret_cast<uint2*>(vals_out)[dst - n / 2] = r;
-          else reinterpret_cast<uint2*>(keys_out)[dst] = r;
-        } else {
-          reinterpret_cast<uint2*>(keys_out)[dst] = r;
-        }
-      } else {
-        keys_out[dst] = kk;
-        if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
-      }
-    };
+    if constexpr (ALIGN) {
+      const uint32_t total = sm.cstart[RADIX];
+      const uint32_t js = ROUNDS > 1 ? min(sm.jsplit, total) : total;
+      if (rr == 0) store_chunks(0, ROUNDS > 1 ? min(js + 1, total) : total, 0, LTILE);
+      else store_chunks(js, total, roff, roff + LTILE);
+      continue;
+    }
     if (valid == static_cast<uint32_t>(TILE)) {
 #pragma unroll
       for (int k = 0; k < LITEMS; ++k) {
@@ -554,18 +638,40 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   __shared__ SM sm;
   const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
   const uint32_t t = threadIdx.x;
-  if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
-  for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
-  const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
-  __syncthreads();
-  // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
-  const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   uint32_t tt = t;
   asm volatile("" : "+v"(tt));
-  const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
   K key[ITEMS];
   uint32_t val[ITEMS];
-  tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
+  uint32_t tile;
+  if constexpr ((OPT & 131072) != 0) {
+    // speculative load: with in-order dispatch the ticket mostly equals blockIdx.x, so the
+    // tile's loads go out before the ticket's round trip; a different ticket reloads (the
+    // ticket alone decides which tile this workgroup sorts)
+    const uint32_t guess = blockIdx.x;
+    uint32_t tk = 0;
+    if (t == 0) tk = atomicAdd(ticket, 1u);
+    tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, guess, tt);
+    // the ticket goes to LDS after the loads are issued (its wait is then vmcnt(loads))
+    if (t == 0) sm.ticket = tk;
+    for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    lds_barrier();
+    tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+    if (tile != guess) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
+  } else {
+    if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+    for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    __syncthreads();
+    tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+    tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
+  }
+  if constexpr ((OPT & 8) != 0) {
+    if (t == 0)
+      error_word[64 + static_cast<size_t>(tile) * 8 + 6] =
+          static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);
+  }
+  const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
+  // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
+  const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, key, val, keys_in, keys_out, vals_in,
                                                  vals_out, n, dg, gh, ticket, status, status_next,
                                                  error_word, t_begin);

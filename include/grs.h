@@ -339,6 +339,19 @@ typedef struct grs_key_extract {
 grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t record_bytes,
                             const grs_key_extract* key, void* stream);
 
+/* The same record sort with a caller-defined key (the reference's K1 is "adapted to whatever
+ * needs to be sorted", OriginalDataToIntermediateData.comp:12-19): the caller's own kernel has
+ * written d_keys[i] = key of record i (the sorter's key width) and d_idx[i] = i, stream-ordered
+ * before this call; the (key, index) pairs are sorted stably (both buffers are overwritten),
+ * the records gathered by index and copied back, so d_records[0..n) ends up sorted in place.
+ * grs_records_key_buffers hands out sorter-owned device buffers for the keys and indices
+ * (valid until the next record-sort call on this sorter grows them).  The C++ template
+ * grs::ParallelSortBy (grs_parallel_sort.hpp) wraps both around a __device__ key functor. */
+grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes, void** d_keys,
+                                   uint32_t** d_idx);
+grs_status grs_sort_records_by_keys(grs_sorter* s, void* d_records, size_t n, size_t record_bytes,
+                                    void* d_keys, uint32_t* d_idx, void* stream);
+
 /* Stand-alone device-wide exclusive prefix sum of uint32 (sums wrap mod 2^32), the
  * reference's K3a + K3b (ParallelPrefixScan.comp:41-196, ParallelSort.cpp:253-274) as one
  * reduce-then-scan (three launches).  d_out may equal d_in; both 16-byte aligned.  d_total (nullable) receives the sum of all

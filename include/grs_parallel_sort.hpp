@@ -18,10 +18,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "grs.h"
@@ -229,6 +232,99 @@ class ParallelSort {
   bool _records = false;
   size_t _recordBytes = 4;
   grs_key_extract _key{};
+};
+
+// ---- user-defined key functors (the reference's K1 hook) ----------------------------------
+// The reference's K1 is written to "adapt to whatever needs to be sorted": structs with
+// integers, floats and vec4s (Shaders/ParallelSort/OriginalDataToIntermediateData.comp:12-19,
+// 42; ParallelSort.h:15-18,27-31).  ParallelSortBy<Record, KeyFn> takes any device-callable
+// key function of a record; the caller's hipcc instantiates its extraction kernel here, and
+// libgrs sorts the (key, index) pairs and gathers the records (grs_sort_records_by_keys).
+namespace grs {
+
+// Order-preserving bit maps for functors whose key is signed or floating point: a < b (as
+// int / float, IEEE-754 total order: -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN) iff
+// OrderedBits(a) < OrderedBits(b) as unsigned (the maps of grs_key_transform).
+__host__ __device__ inline uint32_t OrderedBits(int32_t v) { return static_cast<uint32_t>(v) ^ 0x80000000u; }
+__host__ __device__ inline uint64_t OrderedBits(int64_t v) {
+  return static_cast<uint64_t>(v) ^ 0x8000000000000000ull;
+}
+__host__ __device__ inline uint32_t OrderedBits(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline uint64_t OrderedBits(double f) {
+  uint64_t u;
+  __builtin_memcpy(&u, &f, 8);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+// K1 with the caller's functor: keys[i] = fn(rec[i]), idx[i] = i (grid-stride).
+template <typename Key, typename Record, typename KeyFn>
+__global__ void ExtractKeysWith(const Record* __restrict__ rec, uint32_t n, KeyFn fn,
+                                Key* __restrict__ keys, uint32_t* __restrict__ idx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    keys[i] = static_cast<Key>(fn(rec[i]));
+    idx[i] = i;
+  }
+}
+
+}  // namespace grs
+
+// Controller bound to a RecordSsbo<Record> that sorts it in place, stably, by key_fn(record):
+// KeyFn is a functor with a __device__ (or __host__ __device__) const operator() taking a
+// const Record& and returning uint32_t or uint64_t (use grs::OrderedBits for int / float keys).
+template <typename Record, typename KeyFn>
+class ParallelSortBy {
+ public:
+  using Key = std::decay_t<decltype(std::declval<const KeyFn&>()(std::declval<const Record&>()))>;
+  static_assert(std::is_same<Key, uint32_t>::value || std::is_same<Key, uint64_t>::value,
+                "the key functor must return uint32_t or uint64_t (grs::OrderedBits maps signed "
+                "and floating-point keys)");
+
+  ParallelSortBy(const std::shared_ptr<RecordSsbo<Record>>& dataToSort, KeyFn keyFn,
+                 void* stream = nullptr)
+      : _keep(dataToSort), _fn(keyFn), _stream(stream) {
+    if (!dataToSort) throw std::invalid_argument("ParallelSortBy: null RecordSsbo");
+    _data = dataToSort->DevicePtr();
+    _numItems = dataToSort->NumItems();
+    int dev = 0;
+    grs::check_hip(hipGetDevice(&dev), "ParallelSortBy");
+    grs::check(grs_create(&_sorter, _numItems, sizeof(Key) == 8 ? GRS_KEY_U64 : GRS_KEY_U32, 1, 8, dev),
+               "ParallelSortBy: grs_create");
+  }
+  ~ParallelSortBy() { grs_destroy(_sorter); }
+  ParallelSortBy(const ParallelSortBy&) = delete;
+  ParallelSortBy& operator=(const ParallelSortBy&) = delete;
+
+  // Blocking, like ParallelSort::Sort(); SortAsync() only enqueues.
+  void Sort() {
+    SortAsync();
+    grs::check(grs_stream_check_error(_sorter, _stream), "ParallelSortBy::CheckError");
+  }
+  void SortAsync() {
+    if (_numItems == 0) return;
+    void* keys = nullptr;
+    uint32_t* idx = nullptr;
+    grs::check(grs_records_key_buffers(_sorter, _numItems, sizeof(Record), &keys, &idx),
+               "ParallelSortBy: key buffers");
+    const unsigned grid = std::min<unsigned>((_numItems + 255) / 256, 8192u);
+    hipLaunchKernelGGL((grs::ExtractKeysWith<Key, Record, KeyFn>), dim3(grid), dim3(256), 0,
+                       static_cast<hipStream_t>(_stream), _data, _numItems, _fn,
+                       static_cast<Key*>(keys), idx);
+    grs::check_hip(hipGetLastError(), "ParallelSortBy: extract launch");
+    grs::check(grs_sort_records_by_keys(_sorter, _data, _numItems, sizeof(Record), keys, idx, _stream),
+               "ParallelSortBy::Sort");
+  }
+
+ private:
+  std::shared_ptr<void> _keep;
+  Record* _data = nullptr;
+  unsigned int _numItems = 0;
+  KeyFn _fn;
+  grs_sorter* _sorter = nullptr;
+  void* _stream = nullptr;
 };
 
 // Multi-GPU controller (one process per GPU): sorts this rank's shard as part

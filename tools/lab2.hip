@@ -236,10 +236,10 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
             const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
             uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000 + opt;
+  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 1000000 + opt;
   switch (code) {
 #define V(KB, P, B, I, M, O)                                                                   \
-  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000 + O: {                  \
+  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 1000000 + O: {                \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                               \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
     hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
@@ -266,6 +266,11 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 768, 66, 1, 1040) V(32, 0, 768, 62, 1, 1040) V(32, 0, 768, 64, 1, 1048)
     V(32, 0, 1024, 36, 1, 280)
     V(64, 0, 768, 40, 1, 1040) V(64, 0, 768, 44, 1, 1040) V(64, 1, 768, 28, 1, 1040)
+    V(32, 0, 1024, 36, 1, 65808) V(32, 0, 1024, 36, 1, 65816) V(32, 0, 768, 64, 1, 66576)
+    V(32, 0, 768, 64, 1, 66584) V(32, 1, 1024, 17, 1, 65808) V(32, 1, 768, 40, 1, 66576)
+    V(64, 0, 1024, 17, 1, 65808) V(64, 0, 768, 44, 1, 66576)
+    V(32, 0, 1024, 36, 1, 131344) V(32, 0, 1024, 36, 1, 131352) V(32, 0, 768, 64, 1, 132112)
+    V(32, 0, 768, 64, 1, 132120) V(32, 1, 1024, 17, 1, 131344) V(64, 0, 1024, 17, 1, 131344)
 #undef V
     default:
       return -1;
@@ -278,10 +283,10 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
             void* out, const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
             uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000 + opt;
+  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 1000000 + opt;
   switch (code) {
 #define V(KB, P, B, I, M, O)                                                                    \
-  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000 + O: {                   \
+  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 1000000 + O: {                 \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                           \
     const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
@@ -292,7 +297,7 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     V(32, 0, 1024, 36, 1, 256) V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 288)
     V(64, 1, 1024, 11, 1, 256) V(32, 1, 1024, 17, 1, 256) V(64, 0, 1024, 17, 1, 256)
     V(32, 0, 768, 64, 1, 1040) V(32, 0, 768, 64, 1, 1048) V(32, 0, 768, 64, 1, 1024)
-    V(32, 0, 768, 60, 1, 1040)
+    V(32, 0, 768, 60, 1, 1040) V(32, 0, 1024, 36, 1, 65792)
 #undef V
     default:
       return -1;

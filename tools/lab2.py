@@ -195,6 +195,7 @@ def main():
         tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
         a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
         m = a_[:, :6].mean(0)
+        print(f"   ticket known at {a_[:, 6].mean():.0f} cycles (p90 {np.percentile(a_[:, 6], 90):.0f})", flush=True)
         d = np.diff(np.concatenate([[0.0], m]))
         names = ["ticket+load+rank", "zero+B1", "colscan+publish+scan+B2", "fold+issue+B3",
                  "reorder+lookback+B4", "store+drain"]
