@@ -118,6 +118,9 @@ struct PartTile {
 constexpr uint32_t kBig4Opt = 0;
 constexpr uint32_t kSmallOpt = 16;
 constexpr uint32_t kMatchOpt = 512 | 16;               // ballot-match ranking (fallback)
+// (XCD ranges, grs_pass.hpp draw_ticket_xr, stay a lab option: they need the digit counts of
+// every range for every pass, and a range of pass p > 0 holds the keys pass p - 1 scattered
+// there, which no upfront histogram of the input positions gives)
 
 // Status words of one look-back buffer for `tiles` tiles of radix `radix`.
 size_t status_words_for(size_t tiles, size_t radix) { return grs::lb3_status_words(tiles, radix); }
@@ -434,6 +437,7 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value < 0 || value > 2) return bad();
       s->sharded_exchange = value;
       break;
+
     default:
       return set_err(GRS_EINVAL, "grs_set_option: unknown option");
   }
@@ -587,7 +591,7 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
                        uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
                        uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream,
-                       uint32_t expect_tile = 0) {
+                       uint32_t expect_tile = 0, uint32_t range_tiles = 0) {
   const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
   if (status_words_for(tiles, 1u << RB) > s->status_words)
     return set_err(GRS_ECAPACITY, "status buffer too small");
@@ -598,12 +602,14 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
     hipLaunchKernelGGL((grs::grs_onesweep_v6<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(grid), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev,
+                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE), range_tiles);
   } else {
     hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev,
+                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE), range_tiles);
   }
   GRS_HIP(hipGetLastError());
   return GRS_OK;
@@ -615,16 +621,16 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_rec(int kind, grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc,
                       uint32_t* vdst, uint32_t n, const grs::RadixDigit<K>& dig,
                       const uint32_t* hist, uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt,
-                      hipStream_t stream, uint32_t expect_tile) {
+                      hipStream_t stream, uint32_t expect_tile, uint32_t range_tiles) {
   using Dig = grs::RadixDigit<K>;
   constexpr bool R = sizeof(K) == 4 && PAIRS && RB == 8;
   constexpr uint32_t W = R ? 8192u : 0u, Rd = R ? 4096u : 0u, RS = R ? 16384u : 0u, WS = R ? 32768u : 0u;
   switch (R ? kind : 0) {
-    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
-    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
-    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
-    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
-    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
+    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
+    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
+    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
+    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
   }
 }
 
@@ -657,6 +663,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   uint32_t* st1 = s->status + s->status_words;
   uint32_t* hist = s->ctrl;
   uint32_t* tickets = s->ctrl + GRS_CTRL_TICKETS;
+  // one look-back chain over all tiles (no XCD ranges: see kMatchOpt's note)
+  const uint32_t range_tiles = std::max<uint32_t>(tiles, 1);
   int ev = 0;
   hipEvent_t* evs = s->ring ? s->ev + (s->calls % s->ring) * grs_sorter::EV_PER_CALL : nullptr;
   auto mark = [&]() -> grs_status {
@@ -679,7 +687,8 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     auto kern = full ? grs::grs_upfront_hist2<K, RB, true> : grs::grs_upfront_hist2<K, RB, false>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream,
                        src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
-                       static_cast<uint32_t>(words));
+                       static_cast<uint32_t>(words), 0u,
+                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE));
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
@@ -727,20 +736,22 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     uint32_t* st_nxt = (p & 1) ? st0 : st1;
     const Dig dig{shift, (1u << bits) - 1u};
     const uint32_t* ph = hist + p * RADIX;
+    uint32_t* tk = tickets + p * GRS_XCDS;
+    const uint32_t rt = range_tiles;
     if (s->rank_mode != 0) {
-      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
-              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt)
+              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt);
     } else if (xl) {
       if constexpr (kXlType)
-        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, rt);
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
-        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tickets + p, st_cur, st_nxt, stream, tile);
+        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, rt);
     } else if (big && rec) {
-      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, rt);
     } else {
-      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile)
-              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tickets + p, st_cur, st_nxt, stream, tile);
+      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt)
+              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt);
     }
     if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;

@@ -197,10 +197,15 @@ struct Hist2Layout {
 template <typename K>
 constexpr int kHist2GridShift = sizeof(K) == 4 ? 20 : 19;
 
+// range_keys > 0 (the pass's XCD ranges, grs_pass.hpp): block b counts range b % GRS_XCDS
+// (keys [c * range_keys, (c + 1) * range_keys)) with the other blocks of its range and
+// flushes into g_hist + c * hist_stride: per-range histograms (the grid is a multiple of
+// GRS_XCDS, range_keys a multiple of the 16-byte vector).
 template <typename K, int RB, bool FULL>
 __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
-    uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words) {
+    uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words,
+    uint32_t range_keys = 0, uint32_t hist_stride = 0) {
   static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
   using HL = Hist2Layout<K>;
   constexpr int MAXQ = HL::MAXQ;
@@ -243,10 +248,21 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
 
   constexpr int VEC = 16 / sizeof(K);
   using V = uint4;
-  const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : n / VEC;
+  // this block's share: all keys (grid-stride), or its range's keys (range-stride)
+  uint32_t lo = 0, cnt_n = n, first = blockIdx.x, nblk = gridDim.x;
+  if (range_keys != 0) {
+    const uint32_t c = blockIdx.x % GRS_XCDS;
+    lo = min(n, c * range_keys);
+    cnt_n = min(n - lo, range_keys);
+    first = blockIdx.x / GRS_XCDS;
+    nblk = gridDim.x / GRS_XCDS;
+    g_hist += c * hist_stride;
+    keys += lo;
+  }
+  const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : cnt_n / VEC;
   const V* kv = reinterpret_cast<const V*>(keys);
-  const uint32_t stride = gridDim.x * HB;
-  uint32_t v = blockIdx.x * HB + t;
+  const uint32_t stride = nblk * HB;
+  uint32_t v = first * HB + t;
   constexpr int U = 4;   // 16-B loads in flight per thread, plus the next group's while counting
   if (v + (U - 1) * stride < nvec) {
     V cur[U];
@@ -278,7 +294,7 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
 #pragma unroll
     for (int e = 0; e < VEC; ++e) count(kk[e]);
   }
-  for (uint64_t i = static_cast<uint64_t>(nvec) * VEC + blockIdx.x * HB + t; i < n; i += stride)
+  for (uint64_t i = static_cast<uint64_t>(nvec) * VEC + first * HB + t; i < cnt_n; i += stride)
     count(keys[i]);   // 64-bit index: i + stride can pass 2^32 near GRS_MAX_N
   __syncthreads();
 

@@ -62,18 +62,21 @@ struct Lb3 {
   uint32_t tw[G - 1];
   uint32_t gi[GW], ga[GW];
   int32_t ph;
+  int32_t g0;   // first group of this tile's chain (XCD ranges: the range's first group)
 
   __device__ __forceinline__ void load_groups(const uint32_t* gacc, const uint32_t* ginc,
                                               uint32_t d) {
 #pragma unroll
     for (int k = 0; k < GW; ++k) {
       const int32_t h = ph - k;
-      gi[k] = h >= 0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
-      ga[k] = h >= 0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      gi[k] = h >= g0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      ga[k] = h >= g0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
     }
   }
   __device__ __forceinline__ void issue(const uint32_t* status, const uint32_t* gacc,
-                                        const uint32_t* ginc, uint32_t tile, uint32_t d) {
+                                        const uint32_t* ginc, uint32_t tile, uint32_t d,
+                                        int32_t first_group = 0) {
+    g0 = first_group;
     const uint32_t first = (tile / G) * G;
 #pragma unroll
     for (int k = 0; k < G - 1; ++k)
@@ -104,12 +107,12 @@ struct Lb3 {
       own += v - 1u;
     }
     uint32_t gp = 0;
-    while (ph >= 0) {
+    while (ph >= g0) {
       int consumed = 0;
       bool done = false, blocked = false;
 #pragma unroll
       for (int k = 0; k < GW; ++k) {
-        if (!done && !blocked && ph - k >= 0) {
+        if (!done && !blocked && ph - k >= g0) {
           if (gi[k] != 0u) {
             gp += gi[k] - 1u;
             done = true;
@@ -123,7 +126,7 @@ struct Lb3 {
       }
       if (done) break;
       ph -= consumed;
-      if (ph < 0) break;
+      if (ph < g0) break;
       if (consumed == 0) {
         if (++spins > GRS_SPIN_LIMIT) {
           atomicOr(error_word, 1u);
@@ -191,8 +194,41 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //       run of L items costs ceil(((D % 64) + L) / 64) instructions that touch only its own
 //       lines, instead of 64-item slices of the tile that start anywhere in a line and cut
 //       across runs (every slice then half-writes a line at each end)
+//   262144 persistent pass: the next tile's loads are issued after this tile's stores (not
+//       after its reorder)
+//   524288 persistent pass: the digit-thread waves issue their part of the next tile's loads
+//       after their look-back (see PF_SPLIT)
+//   1048576 XCD ranges (see draw_ticket_xr): tickets, look-back chains and digit offsets per
+//       range of neighbouring tiles on one XCD
 //   131072 speculative tile load (grs_onesweep_v4): tile blockIdx.x is loaded while the ticket
 //       is in flight; a ticket that differs reloads
+
+// XCD ranges (OPT 1048576): the tiles form GRS_XCDS contiguous ranges of range_tiles tiles
+// (a multiple of the look-back group), one per XCD, each with its own ticket counter and its
+// own look-back chain; a tile's digit offsets add the digit counts of the ranges before it
+// (per-range histograms of the upfront histogram kernel).  Neighbouring tiles then run on
+// one XCD, so the 128-B lines their digit runs share are completed in that XCD's L2 instead
+// of reaching HBM as two partial writes.  A workgroup draws from its own XCD's counter and,
+// once that range is used up, from the next ones: every range's tiles start in order (the
+// look-back's forward progress) whatever the workgroup placement, and the grid's workgroups
+// take exactly the grid's tiles.
+__device__ __forceinline__ uint32_t xcc_id() {
+  // HW_REG_XCC_ID (hwreg 20 on gfx940+), bits [3:0]
+  return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (GRS_XCDS - 1);
+}
+__device__ __forceinline__ uint32_t draw_ticket_xr(uint32_t* ticket, uint32_t tiles,
+                                                   uint32_t range_tiles) {
+  const uint32_t x = xcc_id();
+  for (uint32_t k = 0; k < GRS_XCDS; ++k) {
+    const uint32_t c = (x + k) & (GRS_XCDS - 1);
+    const uint32_t lo = c * range_tiles;
+    if (lo >= tiles) continue;
+    const uint32_t rc = min(range_tiles, tiles - lo);
+    const uint32_t v = atomicAdd(ticket + c, 1u);
+    if (v < rc) return lo + v;
+  }
+  return 0xFFFFFFFFu;   // unreachable: as many workgroups as tiles
+}
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
@@ -264,7 +300,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
-    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, uint64_t t_begin) {
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, uint64_t t_begin,
+    const uint32_t* __restrict__ pass_hist = nullptr, uint32_t hist_stride = 0,
+    uint32_t range_tiles = 0) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr int RADIX = SM::RADIX;
@@ -298,6 +336,25 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   const uint32_t dmask = dig.max_digit();
   uint32_t* gacc = status + static_cast<size_t>(tiles) * RADIX;
   uint32_t* ginc = gacc + static_cast<size_t>(groups) * RADIX;
+  constexpr bool XR = (OPT & 1048576) != 0;
+  // XCD ranges: the pass totals and the counts of the ranges before this tile's (issued here,
+  // used at B2 / B4, after the tile's own loads)
+  uint32_t roff = 0;
+  int32_t g0 = 0;
+  if constexpr (XR) {
+    const uint32_t x = tile / range_tiles;
+    g0 = static_cast<int32_t>((x * range_tiles) / G);
+    if (t < static_cast<uint32_t>(RADIX)) {
+      uint32_t tot = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < GRS_XCDS; ++c) {
+        const uint32_t v = pass_hist[c * hist_stride + t];
+        tot += v;
+        roff += c < x ? v : 0u;
+      }
+      gh = tot;
+    }
+  }
 
 #define V4_STAMP(k)                                                                        \
   do {                                                                                     \
@@ -366,7 +423,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   }
   V4_STAMP(0);
   if constexpr (PF) {
-    if (t == 0) sm.next = atomicAdd(ticket, 1u);   // read after B2
+    if (t == 0) sm.next = XR ? draw_ticket_xr(ticket, tiles, range_tiles) : atomicAdd(ticket, 1u);  // read after B2
   }
   // this tile's (and its group's) words of the next pass's status buffer
   if (t < static_cast<uint32_t>(RADIX)) {
@@ -434,7 +491,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       sm.lstart[t] = lstart;
       if (t == static_cast<uint32_t>(RADIX - 1)) sm.lstart[RADIX] = TILE;
     }
-    if constexpr ((OPT & (16 | 64)) == 0 && !PF) lb.issue(status, gacc, ginc, tile, t);
+    if constexpr ((OPT & (16 | 64)) == 0 && !PF) lb.issue(status, gacc, ginc, tile, t, g0);
   }
   lds_barrier();  // B3
   V4_STAMP(3);
@@ -467,29 +524,39 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     }
   }
   if constexpr ((OPT & 16) != 0 || PF) {
-    if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t);
+    if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t, g0);
   }
   uint32_t next = tiles;
-  if constexpr (PF && ROUNDS == 1) {   // two rounds: after round 2 sits in LDS (store phase)
+  constexpr bool PF_LATE = (OPT & 262144) != 0;
+  // PF_SPLIT: the waves holding digit threads issue their share of the next tile's loads only
+  // after their look-back has finished: vmcnt retires loads in issue order, so a look-back poll
+  // issued behind the prefetch would wait for all of it
+  constexpr bool PF_SPLIT = (OPT & 524288) != 0;
+  if constexpr (PF && ROUNDS == 1 && !PF_LATE) {   // two rounds: after round 2 sits in LDS
     next = __builtin_amdgcn_readfirstlane(sm.next);
-    if (next < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
+    if (next < tiles && (!PF_SPLIT || w >= static_cast<uint32_t>(DW)))
+      tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
   if (t < static_cast<uint32_t>(RADIX)) {
     uint32_t prefix;
     if constexpr ((OPT & 64) != 0) {
-      prefix = static_cast<uint32_t>((static_cast<uint64_t>(gh) * tile) / tiles);
+      prefix = static_cast<uint32_t>((static_cast<uint64_t>(gh) * tile) / tiles) - roff;
     } else {
       prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
     }
-    sm.base[t] = gstart + prefix - lstart;
+    sm.base[t] = gstart + roff + prefix - lstart;
     if constexpr (ALIGN && ROUNDS > 1) {
       // the run holding tile position LTILE (the round boundary) names the first chunk of
       // round 2: the chunk of that position (it is stored partly in each round)
       if (t == 0) sm.jsplit = 0xFFFFFFFFu;
-      const uint32_t D = gstart + prefix;
+      const uint32_t D = gstart + roff + prefix;
       if (lstart <= static_cast<uint32_t>(LTILE) && static_cast<uint32_t>(LTILE) < lstart + publish)
         sm.jsplit = cstart + ((D + (LTILE - lstart)) - (D & ~63u)) / 64u;
     }
+  }
+  if constexpr (PF && ROUNDS == 1 && !PF_LATE && PF_SPLIT) {
+    if (next < tiles && w < static_cast<uint32_t>(DW))
+      tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
   lds_barrier();  // B4
   V4_STAMP(4);
@@ -615,6 +682,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       }
     }
   }
+  if constexpr (PF && ROUNDS == 1 && PF_LATE) {   // the next tile's loads behind the stores
+    next = __builtin_amdgcn_readfirstlane(sm.next);
+    if (next < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
+  }
   if constexpr ((OPT & 8) != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     V4_STAMP(5);
@@ -633,9 +704,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev,
+    uint32_t hist_stride = 0, uint32_t range_tiles = 0) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
+  constexpr bool XR = (OPT & 1048576) != 0;
   const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
   const uint32_t t = threadIdx.x;
   uint32_t tt = t;
@@ -658,10 +731,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
     tile = __builtin_amdgcn_readfirstlane(sm.ticket);
     if (tile != guess) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
   } else {
-    if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+    if (t == 0)
+      sm.ticket = XR ? draw_ticket_xr(ticket, (n + SM::TILE - 1) / SM::TILE, range_tiles)
+                     : atomicAdd(ticket, 1u);
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
     __syncthreads();
     tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+    if (XR && tile >= (n + SM::TILE - 1) / SM::TILE) {   // unreachable (see draw_ticket_xr)
+      if (t == 0) atomicOr(error_word, 1u);
+      return;
+    }
     tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
   }
   if constexpr ((OPT & 8) != 0) {
@@ -674,7 +753,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, key, val, keys_in, keys_out, vals_in,
                                                  vals_out, n, dg, gh, ticket, status, status_next,
-                                                 error_word, t_begin);
+                                                 error_word, t_begin, pass_hist, hist_stride,
+                                                 range_tiles);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -695,11 +775,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev,
+    uint32_t hist_stride = 0, uint32_t range_tiles = 0) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
+  constexpr bool XR = (OPT & 1048576) != 0;
   const uint32_t t = threadIdx.x;
-  if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+  if (t == 0)
+    sm.ticket = XR ? draw_ticket_xr(ticket, (n + SM::TILE - 1) / SM::TILE, range_tiles)
+                   : atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   __syncthreads();
@@ -713,7 +797,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     const uint64_t t_begin = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
     tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true>(
         sm, tile, key, val, keys_in, keys_out, vals_in, vals_out, n, dg, gh, ticket, status,
-        status_next, error_word, t_begin);
+        status_next, error_word, t_begin, pass_hist, hist_stride, range_tiles);
     // every LDS read of the finished tile is done before the counters are reset
     lds_barrier();
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;

@@ -160,7 +160,17 @@ __global__ __launch_bounds__(1024) void lds_atomic_rate(uint32_t* out, int iters
   if (acc == 0xFFFFFFFFu) out[1023] = acc;
 }
 
+// XCC id of every block (placement check of draw_ticket_xr's counter choice)
+__global__ void xcc_probe(uint32_t* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = grs::xcc_id();
+}
+
 extern "C" {
+
+int lab2_xcc(uint32_t* out, int blocks, void* stream) {
+  hipLaunchKernelGGL(xcc_probe, dim3(blocks), dim3(64), 0, static_cast<hipStream_t>(stream), out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // pass memory-pattern emulation: block, items, mode, dynamic LDS bytes (occupancy control)
 int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out, uint32_t n,
@@ -190,6 +200,11 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
     case 102403607: k = (const void*)scatter_emu<1024, 36, 7>; break;
     case 102403601: k = (const void*)scatter_emu<1024, 36, 1>; break;
     case 102403621: k = (const void*)scatter_emu<1024, 36, 1, 2>; break;
+    case 102403611: k = (const void*)scatter_emu<1024, 36, 1, 1>; break;
+    case 102403613: k = (const void*)scatter_emu<1024, 36, 3, 1>; break;
+    case 102403623: k = (const void*)scatter_emu<1024, 36, 3, 2>; break;
+    case 102404800: k = (const void*)scatter_emu<1024, 48, 0>; break;
+    case 102407200: k = (const void*)scatter_emu<1024, 72, 0>; break;
     case 102403631: k = (const void*)scatter_emu<1024, 36, 1, 3>; break;
     case 102403603: k = (const void*)scatter_emu<1024, 36, 3>; break;
     case 102403605: k = (const void*)scatter_emu<1024, 36, 5>; break;
@@ -234,7 +249,8 @@ int lab2_emu_pairs(int block, int items, int aos, int lds, const void* kin, cons
 // v4 pass: kb, pairs, block, items, minw, opt
 int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const void* in, void* out,
             const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
-            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
+            uint32_t hist_stride, uint32_t range_tiles) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 1000000 + opt;
   switch (code) {
@@ -245,7 +261,7 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
                        0, s, (const KT*)in, (KT*)out, vin, vout, n,                            \
                        grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
-                       (const grs::RadixDigit<KT>*)nullptr);                                  \
+                       (const grs::RadixDigit<KT>*)nullptr, hist_stride, range_tiles);        \
   } break;
     V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 32, 1, 528) V(32, 0, 1024, 36, 1, 304)
     V(32, 0, 1024, 36, 1, 336) V(32, 0, 1024, 36, 1, 368) V(32, 0, 1024, 40, 1, 1296)
@@ -271,6 +287,12 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(64, 0, 1024, 17, 1, 65808) V(64, 0, 768, 44, 1, 66576)
     V(32, 0, 1024, 36, 1, 131344) V(32, 0, 1024, 36, 1, 131352) V(32, 0, 768, 64, 1, 132112)
     V(32, 0, 768, 64, 1, 132120) V(32, 1, 1024, 17, 1, 131344) V(64, 0, 1024, 17, 1, 131344)
+    V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1048856) V(32, 0, 768, 64, 1, 1049616)
+    V(32, 0, 768, 64, 1, 1049624) V(32, 1, 1024, 17, 1, 1048848) V(64, 0, 1024, 17, 1, 1048848)
+    V(32, 1, 768, 40, 1, 1049616)
+    V(32, 0, 1024, 48, 1, 1049872) V(32, 0, 1024, 40, 1, 1049872) V(32, 0, 768, 56, 1, 1049616)
+    V(32, 0, 768, 60, 1, 1049616) V(32, 0, 768, 48, 1, 1049616) V(32, 0, 768, 48, 1, 1040)
+    V(64, 0, 768, 44, 1, 1049616) V(64, 1, 768, 28, 1, 1049616)
 #undef V
     default:
       return -1;
@@ -281,7 +303,8 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
 // v6 (persistent, next-tile prefetch): kb, pairs, block, items, minw, opt, grid
 int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid, const void* in,
             void* out, const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
-            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream) {
+            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
+            uint32_t hist_stride, uint32_t range_tiles) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 1000000 + opt;
   switch (code) {
@@ -292,12 +315,18 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
     hipLaunchKernelGGL((grs::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O>), dim3(g), dim3(B), 0,   \
                        s, (const KT*)in, (KT*)out, vin, vout, n, grs::RadixDigit<KT>{shift, 255u}, \
-                       hist, ticket, st, st2, err, (const grs::RadixDigit<KT>*)nullptr);        \
+                       hist, ticket, st, st2, err, (const grs::RadixDigit<KT>*)nullptr,         \
+                       hist_stride, range_tiles);                                               \
   } break;
     V(32, 0, 1024, 36, 1, 256) V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 288)
     V(64, 1, 1024, 11, 1, 256) V(32, 1, 1024, 17, 1, 256) V(64, 0, 1024, 17, 1, 256)
     V(32, 0, 768, 64, 1, 1040) V(32, 0, 768, 64, 1, 1048) V(32, 0, 768, 64, 1, 1024)
     V(32, 0, 768, 60, 1, 1040) V(32, 0, 1024, 36, 1, 65792)
+    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 36, 1, 280) V(32, 0, 1024, 36, 1, 262416)
+    V(32, 0, 1024, 36, 1, 262424) V(32, 0, 1024, 36, 1, 524560) V(32, 0, 1024, 36, 1, 524568)
+    V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1573136)
+    V(32, 0, 768, 64, 1, 525328) V(32, 1, 1024, 17, 1, 524560) V(64, 0, 1024, 17, 1, 524560)
+    V(32, 0, 1024, 36, 1, 524544) V(32, 0, 1024, 36, 1, 524552)
 #undef V
     default:
       return -1;

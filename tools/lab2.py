@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--lds-atomic", action="store_true", help="returning ds_add rate by address multiplicity")
     ap.add_argument("--rot", type=int, default=0, help="OPT 2048 store-sweep rotation per tile (keys)")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--xcc", action="store_true", help="print the XCC id of each block (placement)")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
     ap.add_argument("--emu-pairs", default="", help="block:items:aos:lds,... pairs memory pattern (SoA vs AoS)")
     a = ap.parse_args()
@@ -61,11 +62,29 @@ def main():
     st2 = torch.zeros_like(st)
     torch.cuda.synchronize()
 
+    xr_hist = {}
+
+    def range_hist(kb, tile):
+        """per-XCD-range digit-0 histograms [8][256] and the range size in tiles (OPT 1048576)"""
+        if (kb, tile) not in xr_hist:
+            keys = bufs[kb][0]
+            tiles = (n + tile - 1) // tile
+            R = ((tiles + 7) // 8 + 7) // 8 * 8
+            k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64) & 255
+            hs = [torch.bincount(k64[min(n, c * R * tile):min(n, (c + 1) * R * tile)], minlength=256)
+                  for c in range(8)]
+            xr_hist[(kb, tile)] = (torch.stack(hs).to(torch.int32).view(torch.uint32).contiguous(), R)
+        return xr_hist[(kb, tile)]
+
     def run(v):
         kind, kb, pairs, block, items = v[:5]
         keys, out, hist = bufs[kb]
+        stride, rtiles = 0, 0
+        if kind in ("v4", "v6") and v[6] & 1048576:
+            hist, rtiles = range_hist(kb, block * items)
+            stride = 256
         args = (P(keys), P(out), P(vin), P(vout), ctypes.c_uint32(n), P(hist), P(ticket), P(st),
-                P(st2), P(err), 0, sp)
+                P(st2), P(err), 0, sp, ctypes.c_uint32(stride), ctypes.c_uint32(rtiles))
         if kind == "r4":   # r4:32:0:block:items:minw:opt  (4-bit digits, low nibble)
             rc = L.lab2_v4rb4(block, items, v[5], v[6], P(keys), P(out), ctypes.c_uint32(n),
                               P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
@@ -99,6 +118,14 @@ def main():
             if r == 0:
                 print(f"   {times[v][-1]:.4f} ms  err={int(err[0].item())}", flush=True)
     print(f"n={n}  error word={int(err[0].item())}", flush=True)
+    if a.xcc:
+        o = torch.zeros(4096, dtype=torch.uint32, device=dev)
+        assert L.lab2_xcc(P(o), 4096, sp) == 0
+        torch.cuda.synchronize()
+        x = o.cpu().numpy()
+        b = np.arange(4096)
+        print("xcc ids of blocks 0..31:", x[:32].tolist())
+        print("blocks whose xcc == (b - b0) % 8 + xcc0:", int(((b % 8 + x[0]) % 8 == x).sum()), "of 4096")
     if a.lds_atomic:
         o = torch.zeros(1024, dtype=torch.uint32, device=dev)
         for d in (64, 32, 16, 8, 1):
