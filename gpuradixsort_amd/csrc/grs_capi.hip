@@ -282,6 +282,7 @@ struct grs_sorter {
   bool xev_recorded = false;
   uint64_t x_sent = 0, x_recv = 0;
   int x_presorted = 0;
+  uint64_t x_region_redo = 0;      // sharded partitions redone into contiguous buckets (spills)
   int tile_mode = -1;              // GRS_OPT_TILE: -1 by size, 0 small, 1 big
   int pass_mode = 0;               // GRS_OPT_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
   bool sharded_general = false;    // GRS_OPT_SHARDED_PATH: one rank takes the G-rank path too
@@ -1447,14 +1448,24 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   hipLaunchKernelGGL((grs::grs_shard_splitters<K, N>), dim3(1), dim3(1024), 0, st, ak, ap,
                      static_cast<uint32_t>(g), S, static_cast<uint32_t>(me), dig);
   GRS_HIP(hipGetLastError());
-  // 4. partition into the send buffer: G regions of n items each (bucket b at b * n), so no
-  //    bucket histogram pass is needed (grs_partition's region mode); when G * n reaches 2^32
-  //    the buckets go contiguously into the sorter's ping-pong scratch (free until step 8)
-  const bool regions = n > 0 && static_cast<uint64_t>(g) * n < (1ull << 32) && !s->sharded_contig;
+  // 4. partition into the send buffer: G regions of `region` items (bucket b at b * region), so
+  //    no bucket histogram pass is needed (grs_partition's region mode).  region is the even
+  //    share plus 25 % and 64K items of slack (a balanced bucket fits: the splitters are
+  //    quantiles with ties broken by index); the buffer holds (G - 1) regions + n items, so even
+  //    a last bucket of all n items stays inside it.  A bucket larger than its region spills
+  //    into the next region: the count matrix shows it at the host synchronisation, and the
+  //    partition is then redone with a bucket histogram into contiguous buckets in the sorter's
+  //    ping-pong scratch (free until step 8) -- the counts, and so the exchange plan, are the
+  //    same.  Contiguous buckets are also the path when G * region reaches 2^32.
+  const uint32_t region =
+      n == 0 ? 0u
+             : static_cast<uint32_t>(std::min<uint64_t>(n, static_cast<uint64_t>(n) * 5 / 4 / g + 65536));
+  bool regions = n > 0 && static_cast<uint64_t>(g) * region < (1ull << 32) && !s->sharded_contig;
   K* send_k = static_cast<K*>(s->alt_keys);
   uint32_t* send_v = s->alt_vals;
+  const size_t xitems = static_cast<size_t>(g - 1) * region + n;   // region-mode buffer items
   if (regions) {
-    const size_t need = static_cast<size_t>(g) * n * (sizeof(K) + (PAIRS ? 4 : 0));
+    const size_t need = xitems * (sizeof(K) + (PAIRS ? 4 : 0));
     if (s->xbuf_bytes < need) {
       if (s->xbuf) (void)hipFree(s->xbuf);
       s->xbuf = nullptr;
@@ -1466,11 +1477,11 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
       s->xbuf_bytes = need;
     }
     send_k = static_cast<K*>(s->xbuf);
-    send_v = PAIRS ? reinterpret_cast<uint32_t*>(send_k + static_cast<size_t>(g) * n) : nullptr;
+    send_v = PAIRS ? reinterpret_cast<uint32_t*>(send_k + xitems) : nullptr;
   }
   if (n > 0) {
     const grs_status r = run_partition_n<K, PAIRS, N>(s, keys, vals, send_k, send_v, n, Dig{}, dig,
-                                                      g - 1, cnt, st, regions ? n : 0u);
+                                                      g - 1, cnt, st, regions ? region : 0u);
     if (r != GRS_OK) return r;
   } else {
     GRS_HIP(hipMemsetAsync(cnt, 0, static_cast<size_t>(g) * 4, st));
@@ -1486,8 +1497,19 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   }
   uint64_t soff[16], roff[16], total = 0;
   shard_plan(s->shard_host, g, me, soff, roff, &total);
+  bool spilled = false;
+  for (int p = 0; regions && p < g; ++p) spilled |= s->shard_host[me * g + p] > region;
+  if (spilled) {   // a bucket outgrew its region: contiguous buckets instead (same counts)
+    s->x_region_redo++;
+    regions = false;
+    send_k = static_cast<K*>(s->alt_keys);
+    send_v = s->alt_vals;
+    const grs_status r = run_partition_n<K, PAIRS, N>(s, keys, vals, send_k, send_v, n, Dig{}, dig,
+                                                      g - 1, cnt, st, 0u);
+    if (r != GRS_OK) return r;
+  }
   if (regions)
-    for (int p = 0; p < g; ++p) soff[p] = static_cast<uint64_t>(p) * n;
+    for (int p = 0; p < g; ++p) soff[p] = static_cast<uint64_t>(p) * region;
   if (total > out_cap || total > s->capacity)
     return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
                                       " items) exceeds out_capacity or the sorter capacity");

@@ -40,6 +40,10 @@
 #ifndef GRS_LB_GWIN
 #define GRS_LB_GWIN 8
 #endif
+// the same for two-round (XL) tiles, whose keys stay live in VGPRs beside the window
+#ifndef GRS_LB_GWIN_XL
+#define GRS_LB_GWIN_XL 4
+#endif
 
 // XCDs of an MI355X (8 x 32 CUs, each XCD with its own L2): the pass's XCD ranges.
 #define GRS_XCDS 8

@@ -472,7 +472,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   lds_barrier();  // B2
   V4_STAMP(2);
 
-  Lb3<RADIX, (ROUNDS > 1 ? 4 : GRS_LB_GWIN)> lb;
+  Lb3<RADIX, (ROUNDS > 1 ? GRS_LB_GWIN_XL : GRS_LB_GWIN)> lb;
   if (t < static_cast<uint32_t>(RADIX)) {
     for (uint32_t ww = 0; ww < w; ++ww) {
       lstart += sm.wsum[ww];

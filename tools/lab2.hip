@@ -293,6 +293,8 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 1024, 48, 1, 1049872) V(32, 0, 1024, 40, 1, 1049872) V(32, 0, 768, 56, 1, 1049616)
     V(32, 0, 768, 60, 1, 1049616) V(32, 0, 768, 48, 1, 1049616) V(32, 0, 768, 48, 1, 1040)
     V(64, 0, 768, 44, 1, 1049616) V(64, 1, 768, 28, 1, 1049616)
+    V(32, 0, 1024, 36, 1, 256) V(32, 0, 768, 64, 1, 1032)
+    V(32, 0, 1024, 36, 1, 264)
 #undef V
     default:
       return -1;
@@ -351,7 +353,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
                        (const grs::RadixDigit<uint32_t>*)nullptr);                             \
   } break;
     V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
-    V(1024, 32, 1, 8)
+    V(1024, 32, 1, 8) V(1024, 32, 1, 512) V(1024, 32, 1, 520) V(1024, 32, 1, 528)
 #undef V
     default:
       return -1;

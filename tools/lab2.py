@@ -29,10 +29,11 @@ def main():
     ap.add_argument("--rot", type=int, default=0, help="OPT 2048 store-sweep rotation per tile (keys)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--xcc", action="store_true", help="print the XCC id of each block (placement)")
+    ap.add_argument("--lib", default="", help="load tools/liblab2_LIB.so (a build with other knobs)")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
     ap.add_argument("--emu-pairs", default="", help="block:items:aos:lds,... pairs memory pattern (SoA vs AoS)")
     a = ap.parse_args()
-    L = ctypes.CDLL(os.path.join(HERE, "liblab2.so"))
+    L = ctypes.CDLL(os.path.join(HERE, f"liblab2{'_' + a.lib if a.lib else ''}.so"))
     vp = ctypes.c_void_p
     P = lambda t: vp(t.data_ptr())  # noqa: E731
     n = a.n
