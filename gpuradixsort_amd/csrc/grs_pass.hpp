@@ -143,8 +143,124 @@ struct Lb3 {
   }
 };
 
+// Wide look-back: the prefix of digit d is resolved by a group of L lanes (lane j of group d is
+// thread d * L + j; L a power of two, L lanes of one wave) instead of one digit thread: each
+// round reads L groups' inclusive + accumulator words at once (one load each per lane) and
+// finds, by two ballots, the newest published inclusive and the newest incomplete accumulator
+// among them.  At 4-bit digits L = 64 (one wave per digit): a round covers 64 groups = 512
+// tiles, so the look-back of a 2^24-key pass is one round trip instead of up to eight.
+template <int RADIX, int L>
+struct LbWide {
+  static constexpr int G = GRS_LB_GROUP;
+  static_assert((L & (L - 1)) == 0 && L >= 2 && L <= GRS_WAVE, "lane groups of 2..64 lanes");
+  static constexpr int NOWN = (G - 1 + L - 1) / L;   // own-group tile words per lane
+  static constexpr int W = L >= 16 ? 1 : 16 / L;      // groups per lane per round (>= 16 a round)
+  uint32_t tw[NOWN];  // own group: tile words j + k * L (first read)
+  uint32_t gi[W], ga[W];   // groups ph - (k * L + j)
+  int32_t ph, g0;
+  uint32_t gp_out;    // the group-level part of the last finish() (groups before the tile's)
+
+  __device__ __forceinline__ static uint32_t gsum(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) v += __shfl_xor(v, o, GRS_WAVE);
+    return v;
+  }
+  __device__ __forceinline__ static uint64_t gmask(bool pred, uint32_t lane) {
+    const uint64_t b = __builtin_amdgcn_ballot_w64(pred);
+    if constexpr (L == GRS_WAVE) return b;
+    else return (b >> (lane & ~static_cast<uint32_t>(L - 1))) & ((1ull << L) - 1ull);
+  }
+  __device__ __forceinline__ void load_groups(const uint32_t* gacc, const uint32_t* ginc,
+                                              uint32_t d, uint32_t j) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int32_t h = ph - static_cast<int32_t>(k * L + j);
+      gi[k] = h >= g0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      ga[k] = h >= g0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
+    }
+  }
+  __device__ __forceinline__ void issue(const uint32_t* status, const uint32_t* gacc,
+                                        const uint32_t* ginc, uint32_t tile, uint32_t d,
+                                        uint32_t j, int32_t first_group) {
+    g0 = first_group;
+    const uint32_t first = (tile / G) * G;
+#pragma unroll
+    for (int k = 0; k < NOWN; ++k) {
+      const uint32_t i = first + j + k * L;
+      tw[k] = i < tile ? ld_status(status + static_cast<size_t>(i) * RADIX + d) : 1u;
+    }
+    ph = static_cast<int32_t>(tile / G) - 1;
+    load_groups(gacc, ginc, d, j);
+  }
+  // the exclusive prefix of digit d over tiles [g0 * G, tile), in every lane of the group
+  __device__ __forceinline__ uint32_t finish(const uint32_t* status, const uint32_t* gacc,
+                                             const uint32_t* ginc, uint32_t tile, uint32_t d,
+                                             uint32_t j, uint32_t lane, uint32_t* error_word) {
+    const uint32_t first = (tile / G) * G;
+    uint32_t spins = 0, own = 0;
+#pragma unroll
+    for (int k = 0; k < NOWN; ++k) {
+      uint32_t v = tw[k];
+      while (v == 0u) {
+        if (++spins > GRS_SPIN_LIMIT) {
+          atomicOr(error_word, 1u);
+          v = 1u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = ld_status(status + static_cast<size_t>(first + j + k * L) * RADIX + d);
+      }
+      own += v - 1u;
+    }
+    own = gsum(own);
+    uint32_t gp = 0;
+    while (ph >= g0) {
+      // offsets o = k * L + j, newest first: the first published inclusive and the first
+      // incomplete accumulator among this round's L * W groups
+      uint32_t oinc = L * W, oblk = L * W;
+#pragma unroll
+      for (int k = W - 1; k >= 0; --k) {
+        const int32_t h = ph - static_cast<int32_t>(k * L + j);
+        const bool valid = h >= g0;
+        const bool inc = valid && gi[k] != 0u;
+        const bool cmpl = valid && !inc && (ga[k] >> 24) == static_cast<uint32_t>(G);
+        const uint64_t mi = gmask(inc, lane), mb = gmask(valid && !inc && !cmpl, lane);
+        if (mi) oinc = k * L + static_cast<uint32_t>(__builtin_ctzll(mi));
+        if (mb) oblk = k * L + static_cast<uint32_t>(__builtin_ctzll(mb));
+      }
+      uint32_t part = 0;
+      if (oinc < oblk) {   // a published inclusive before any incomplete group
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const uint32_t o = k * L + j;
+          part += o < oinc ? (ga[k] & 0xFFFFFFu) : (o == oinc ? gi[k] - 1u : 0u);
+        }
+        gp += gsum(part);
+        break;
+      }
+      const uint32_t nvalid = static_cast<uint32_t>(min(ph - g0 + 1, L * W));
+      const uint32_t c = min(oblk, nvalid);   // complete groups before the first blocked one
+#pragma unroll
+      for (int k = 0; k < W; ++k) part += (k * L + j) < c ? (ga[k] & 0xFFFFFFu) : 0u;
+      gp += gsum(part);
+      ph -= static_cast<int32_t>(c);
+      if (ph < g0) break;
+      if (c == 0) {
+        if (++spins > GRS_SPIN_LIMIT) {
+          atomicOr(error_word, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      load_groups(gacc, ginc, d, j);
+    }
+    gp_out = gp;
+    return gp + own;
+  }
+};
+
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
-          bool IDX = false, int ROUNDS = 1, bool ALIGN = false>
+          bool IDX = false, int ROUNDS = 1, bool ALIGN = false, bool WIDE = false>
 struct V4Smem {
   static constexpr int RADIX = 1 << RB;
   static constexpr int WAVES = BLOCK / GRS_WAVE;
@@ -167,10 +283,15 @@ struct V4Smem {
   uint32_t lst[ALIGN ? RADIX : 1];
   uint32_t rlen[ALIGN ? RADIX : 1];
   uint32_t jsplit;
+  // wide look-back (OPT 2097152): per digit the group-accumulator add's old value, the
+  // published count and the base without the prefix, handed from the digit threads to the
+  // lane group that resolves the digit's prefix
+  uint32_t lbv[WIDE ? 3 * RADIX : 1];
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
-                         (OPT & 1024) != 0 ? 2 : 1, (OPT & 65536) != 0 && !DigitF::kIndexed>;
+                         (OPT & 1024) != 0 ? 2 : 1, (OPT & 65536) != 0 && !DigitF::kIndexed,
+                         (OPT & 2097152) != 0>;
 
 // OPT bits (lab ablations; the library uses OPT = 0):
 //   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
@@ -437,6 +558,12 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   V4_STAMP(1);
 
   constexpr bool ALIGN = (OPT & 65536) != 0 && !IDX;
+  constexpr bool WIDE = (OPT & 2097152) != 0;
+  // lanes per digit of the wide look-back: the largest power of two <= BLOCK / RADIX, <= 64
+  constexpr int LW = (BLOCK / RADIX) >= 64 ? 64 : (BLOCK / RADIX) >= 32 ? 32 : (BLOCK / RADIX) >= 16 ? 16
+                   : (BLOCK / RADIX) >= 8 ? 8 : (BLOCK / RADIX) >= 4 ? 4 : 2;
+  static_assert(!WIDE || (BLOCK / RADIX >= 2 && !ALIGN && (OPT & 64) == 0),
+                "wide look-back: >= 2 lanes per digit, no aligned stores / estimated bases");
   uint32_t tile_cnt = 0, publish = 0, gold = 0, lstart = 0, gstart = 0, cstart = 0, cbound = 0;
   if (t < static_cast<uint32_t>(RADIX)) {
 #pragma unroll
@@ -473,6 +600,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   V4_STAMP(2);
 
   Lb3<RADIX, (ROUNDS > 1 ? GRS_LB_GWIN_XL : GRS_LB_GWIN)> lb;
+  LbWide<RADIX, WIDE ? LW : 2> lbw;
+  const uint32_t wd = t / LW, wj = t & (LW - 1);   // wide look-back: digit and lane in its group
   if (t < static_cast<uint32_t>(RADIX)) {
     for (uint32_t ww = 0; ww < w; ++ww) {
       lstart += sm.wsum[ww];
@@ -491,7 +620,16 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       sm.lstart[t] = lstart;
       if (t == static_cast<uint32_t>(RADIX - 1)) sm.lstart[RADIX] = TILE;
     }
-    if constexpr ((OPT & (16 | 64)) == 0 && !PF) lb.issue(status, gacc, ginc, tile, t, g0);
+    if constexpr (WIDE) {
+      sm.lbv[t] = gold;
+      sm.lbv[RADIX + t] = publish;
+      sm.lbv[2 * RADIX + t] = gstart + roff - lstart;
+    } else if constexpr ((OPT & (16 | 64)) == 0 && !PF) {
+      lb.issue(status, gacc, ginc, tile, t, g0);
+    }
+  }
+  if constexpr (WIDE && (OPT & 16) == 0 && !PF) {
+    if (wd < static_cast<uint32_t>(RADIX)) lbw.issue(status, gacc, ginc, tile, wd, wj, g0);
   }
   lds_barrier();  // B3
   V4_STAMP(3);
@@ -524,7 +662,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     }
   }
   if constexpr ((OPT & 16) != 0 || PF) {
-    if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t, g0);
+    if constexpr (WIDE) {
+      if (wd < static_cast<uint32_t>(RADIX)) lbw.issue(status, gacc, ginc, tile, wd, wj, g0);
+    } else {
+      if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t, g0);
+    }
   }
   uint32_t next = tiles;
   constexpr bool PF_LATE = (OPT & 262144) != 0;
@@ -537,7 +679,20 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     if (next < tiles && (!PF_SPLIT || w >= static_cast<uint32_t>(DW)))
       tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
-  if (t < static_cast<uint32_t>(RADIX)) {
+  if constexpr (WIDE) {
+    if (wd < static_cast<uint32_t>(RADIX)) {
+      const uint32_t prefix = lbw.finish(status, gacc, ginc, tile, wd, wj, lane, error_word);
+      if (wj == 0) {
+        const uint32_t wgold = sm.lbv[wd], wpub = sm.lbv[RADIX + wd];
+        sm.base[wd] = sm.lbv[2 * RADIX + wd] + prefix;
+        const uint32_t g = tile / G;
+        const uint32_t in_group = min(static_cast<uint32_t>(G), tiles - g * G);
+        if ((wgold >> 24) == in_group - 1u)   // this tile's add completed the group
+          st_status(ginc + static_cast<size_t>(g) * RADIX + wd,
+                    lbw.gp_out + (wgold & 0xFFFFFFu) + wpub + 1u);
+      }
+    }
+  } else if (t < static_cast<uint32_t>(RADIX)) {
     uint32_t prefix;
     if constexpr ((OPT & 64) != 0) {
       prefix = static_cast<uint32_t>((static_cast<uint64_t>(gh) * tile) / tiles) - roff;

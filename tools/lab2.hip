@@ -252,10 +252,10 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
             uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
             uint32_t hist_stride, uint32_t range_tiles) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 1000000 + opt;
+  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000000L + opt;
   switch (code) {
 #define V(KB, P, B, I, M, O)                                                                   \
-  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 1000000 + O: {                \
+  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000000L + O: {             \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                               \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
     hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
@@ -294,7 +294,9 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 768, 60, 1, 1049616) V(32, 0, 768, 48, 1, 1049616) V(32, 0, 768, 48, 1, 1040)
     V(64, 0, 768, 44, 1, 1049616) V(64, 1, 768, 28, 1, 1049616)
     V(32, 0, 1024, 36, 1, 256) V(32, 0, 768, 64, 1, 1032)
-    V(32, 0, 1024, 36, 1, 264)
+    V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 2097424) V(32, 0, 1024, 36, 1, 2097432)
+    V(32, 0, 768, 64, 1, 2098192) V(32, 0, 768, 64, 1, 2098200) V(32, 1, 768, 40, 1, 2098192)
+    V(64, 0, 1024, 17, 1, 2097424)
 #undef V
     default:
       return -1;
@@ -308,10 +310,10 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
             uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
             uint32_t hist_stride, uint32_t range_tiles) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 1000000 + opt;
+  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000000L + opt;
   switch (code) {
 #define V(KB, P, B, I, M, O)                                                                    \
-  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 1000000 + O: {                 \
+  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000000L + O: {              \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                           \
     const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
@@ -326,7 +328,7 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     V(32, 0, 768, 60, 1, 1040) V(32, 0, 1024, 36, 1, 65792)
     V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 36, 1, 280) V(32, 0, 1024, 36, 1, 262416)
     V(32, 0, 1024, 36, 1, 262424) V(32, 0, 1024, 36, 1, 524560) V(32, 0, 1024, 36, 1, 524568)
-    V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1573136)
+    V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1573136) V(32, 0, 1024, 36, 1, 2097424)
     V(32, 0, 768, 64, 1, 525328) V(32, 1, 1024, 17, 1, 524560) V(64, 0, 1024, 17, 1, 524560)
     V(32, 0, 1024, 36, 1, 524544) V(32, 0, 1024, 36, 1, 524552)
 #undef V
@@ -341,10 +343,10 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
                uint32_t n, const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2,
                uint32_t* err, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = ((block * 1000L + items) * 10 + minw) * 1000 + opt;
+  const long code = ((block * 1000L + items) * 10 + minw) * 10000000L + opt;
   switch (code) {
 #define V(B, I, M, O)                                                                          \
-  case ((B * 1000L + I) * 10 + M) * 1000 + O: {                                                \
+  case ((B * 1000L + I) * 10 + M) * 10000000L + O: {                                           \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
     const uint32_t g = std::min<uint32_t>(tiles, grid);                                        \
     hipLaunchKernelGGL((grs::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
@@ -354,6 +356,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
   } break;
     V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
     V(1024, 32, 1, 8) V(1024, 32, 1, 512) V(1024, 32, 1, 520) V(1024, 32, 1, 528)
+    V(1024, 32, 1, 2097152) V(1024, 32, 1, 2097160) V(1024, 32, 1, 2097168)
 #undef V
     default:
       return -1;
