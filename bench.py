@@ -18,8 +18,11 @@ Rank 0 prints ONE JSON line with the driver contract plus:
   roofline      dominant kernel (the pass: grs_onesweep_v4, or v6 on small grids): algorithmic bytes per launch
                 (n_local x 2 x (key + value bytes)) / its mean duration from
                 hipEvents recorded on the sort's stream during the timed steps; `traffic` is
-                the PMC-measured HBM bytes per launch when --traffic-json names the output of
-                tools/bench_pmc.py for this same workload (null otherwise)
+                the HBM bytes per launch that rocprofv3's FETCH_SIZE / WRITE_SIZE counters
+                measure in two child runs of this script (--pmc-probe: one sort of the same
+                workload + a known-byte calibration copy with the pass's access width, which
+                gives the counters' correction factors), after the timed region (rank 0, N = 1;
+                --no-traffic skips them, null on any failure)
   cpu_baseline  the oracle's host std::sort on a bounded sample (rank 0, N = 1 only)
 """
 from __future__ import annotations
@@ -62,6 +65,8 @@ def parse():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--n", type=int, default=0, help="override the total (c4) / per-GPU key count")
     ap.add_argument("--traffic-json", default="", help="tools/bench_pmc.py output of this workload")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child runs")
+    ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--sharded", action="store_true",
@@ -129,8 +134,105 @@ def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
     return out
 
 
+CAL_WORDS = 1 << 27   # calibration copy: 512 MiB read + 512 MiB written
+
+
+def pmc_probe(a, options):
+    """Child run under rocprofv3 --pmc (see measure_traffic): one warm sort, one measured sort
+    of the same workload, two calibration copies of known bytes."""
+    import gpuradixsort_amd as grs
+
+    cid, n_cfg, kb, pairs, rb, _ = CONFIGS[a.config]
+    n = a.n or n_cfg
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    seed = (0x6A09E667F3BCC908 + cid) & ((1 << 64) - 1)
+    k = torch.empty(n, dtype=torch.uint32 if kb == 32 else torch.uint64, device=dev)
+    v = torch.empty(n, dtype=torch.uint32, device=dev) if pairs else None
+    s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb, options=options)
+    for i in range(2):
+        grs.fill_splitmix(k, seed, first_index=i * n)
+        if pairs:
+            grs.iota_u32(v)
+        s.sort(k, v)
+    src = torch.ones(CAL_WORDS, dtype=torch.int32, device=dev)
+    dst = torch.empty_like(src)
+    from gpuradixsort_amd._lib import check, lib
+    import ctypes
+    for _ in range(2):
+        check(lib().grs_copy_u32(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                 CAL_WORDS, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+              "grs_copy_u32")
+    torch.cuda.synchronize()
+    s.check_error()
+
+
+def measure_traffic(a, options, n_local):
+    """HBM bytes per launch of the pass from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM):
+    one counter per rocprofv3 run (FETCH_SIZE, then WRITE_SIZE) over a child --pmc-probe run;
+    each counter is corrected by known bytes / counter bytes of the calibration copy, which
+    issues the pass's own access width (one dword per lane).  Returns (dict, None) or
+    (None, reason)."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import statistics
+    import subprocess
+    import tempfile
+
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return None, "rocprofv3 not found"
+    env = dict(os.environ, TMPDIR="/tmp")
+    extra = [f"--opt={k}={v}" for k, v in options.items()]
+    got = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(d, ctr)
+            cmd = [rp, "--pmc", ctr, "-d", out, "-o", "p", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-probe", "--config", a.config,
+                   "--n", str(n_local)] + extra
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
+                                 start_new_session=True)
+            try:
+                _, err = p.communicate(timeout=150)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return None, f"rocprofv3 --pmc {ctr} timed out"
+            if p.returncode != 0:
+                return None, f"rocprofv3 --pmc {ctr} rc={p.returncode}: {err.decode()[-300:]}"
+            vals = {"pass": [], "cal": []}
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if r["Counter_Name"] != ctr:
+                        continue
+                    name = r["Kernel_Name"]
+                    if "grs_onesweep_v" in name:
+                        vals["pass"].append(float(r["Counter_Value"]) * 1024.0)   # KiB -> bytes
+                    elif "grs_copy_u32" in name:
+                        vals["cal"].append(float(r["Counter_Value"]) * 1024.0)
+            if not vals["pass"] or not vals["cal"]:
+                return None, f"no {ctr} rows for the pass or the calibration copy"
+            got[ctr] = (statistics.mean(vals["pass"]), statistics.mean(vals["cal"]), len(vals["pass"]))
+    known = CAL_WORDS * 4
+    fr, fw = known / got["FETCH_SIZE"][1], known / got["WRITE_SIZE"][1]
+    rd, wr = fr * got["FETCH_SIZE"][0], fw * got["WRITE_SIZE"][0]
+    return {"bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
+            "read_factor": round(fr, 4), "write_factor": round(fw, 4),
+            "launches": got["FETCH_SIZE"][2],
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one counter per run, over "
+                      "bench.py --pmc-probe (2 sorts of this workload) with a grs_copy_u32 "
+                      "calibration of known bytes"}, None
+
+
 def main():
     a = parse()
+    if a.pmc_probe:
+        opts = dict(o.split("=", 1) for o in a.opt)
+        pmc_probe(a, {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in opts.items()})
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -250,8 +352,15 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(min(a.cpu_sample, n_local), kb, pairs, seed)
 
-    traffic = None   # PMC bytes need a separate rocprofv3 --pmc run (tools/bench_pmc.py)
-    if a.traffic_json and os.path.exists(a.traffic_json):
+    # PMC bytes per launch: rocprofv3 child runs of this workload (after the timed region)
+    traffic, traffic_info = None, None
+    if rank == 0 and world == 1 and not sharded and not a.no_traffic:
+        traffic_info, why = measure_traffic(a, options, n_local)
+        if traffic_info:
+            traffic = traffic_info["bytes_per_launch"]
+        else:
+            traffic_info = {"error": why}
+    elif a.traffic_json and os.path.exists(a.traffic_json):
         rec = json.load(open(a.traffic_json))
         if rec.get("n") == n_sorted_local and rec.get("config") == a.config:
             traffic = rec.get("hbm_bytes_per_launch")
@@ -273,7 +382,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "kernel": kernel_name,
                          "kernel_mean_ms": round(mean_pass_ms, 5),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "traffic_over_alg": round(traffic / alg_bytes, 4) if traffic else None},
             # whole-sort view of SURVEY.md §8d: B_alg = N x 2 x passes x (key + value bytes)
             # over the whole step (histogram and exchange included)
             "sort_roofline": {"achieved": round(sort_alg / (elapsed / a.steps) / 1e9, 1),
@@ -286,6 +396,8 @@ def main():
         }
         if options:
             out["config"]["options"] = options
+        if traffic_info:
+            out["traffic_pmc"] = traffic_info
         if sharded:
             out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
             out["config"]["exchange"] = exchange

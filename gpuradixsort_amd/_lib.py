@@ -107,6 +107,7 @@ SIGNATURES = [
                                  c_void_p, c_size_t, c_void_p, c_void_p]),
     ("grs_shard_decode_merge", c_int, [c_void_p, c_void_p, c_int, POINTER(c_uint64),
                                        POINTER(c_uint32), c_void_p, c_size_t, c_void_p]),
+    ("grs_copy_u32", c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     ("grs_iota_u32", c_int, [c_void_p, c_size_t, c_uint32, c_void_p]),
     ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),

@@ -1049,6 +1049,15 @@ grs_status grs_iota_u32(uint32_t* d_out, size_t n, uint32_t start, void* stream)
   return GRS_OK;
 }
 
+grs_status grs_copy_u32(const uint32_t* d_src, uint32_t* d_dst, size_t n, void* stream) {
+  if (n == 0) return GRS_OK;
+  if (!d_src || !d_dst) return set_err(GRS_EINVAL, "grs_copy_u32: NULL");
+  hipLaunchKernelGGL(grs::grs_copy_u32, dim3(grid_for(n, 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_src, d_dst, static_cast<uint64_t>(n));
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
 grs_status grs_gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
                               size_t record_bytes, void* stream) {
   if (n == 0) return GRS_OK;

@@ -441,6 +441,16 @@ __global__ void grs_iota_u32(uint32_t* __restrict__ out, uint64_t n, uint32_t st
     out[i] = start + static_cast<uint32_t>(i);
 }
 
+// Contiguous copy with the pass's access width (one dword per lane per instruction, 256 B per
+// wave-instruction): the known-byte calibration of rocprofv3's FETCH_SIZE / WRITE_SIZE for
+// bench.py's traffic figure.
+__global__ void grs_copy_u32(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                             uint64_t n) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    dst[i] = src[i];
+}
+
 // K5 generalised (SortOriginalData.comp:27-51): dst[i] = src[idx[i]] for records of
 // `rb` bytes.  Records that are a multiple of 4 bytes move as dwords.
 __global__ void grs_gather_records(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,

@@ -280,6 +280,11 @@ grs_status grs_iota_u32(uint32_t* d_out, size_t n, uint32_t start, void* stream)
 grs_status grs_gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
                               size_t record_bytes, void* stream);
 
+/* d_dst[i] = d_src[i] with the pass kernel's access width (one 4-byte word per lane, 256 B per
+ * wave-instruction): a kernel of known bytes that calibrates rocprofv3's FETCH_SIZE /
+ * WRITE_SIZE counters for the pass's loads and stores (bench.py's roofline.traffic). */
+grs_status grs_copy_u32(const uint32_t* d_src, uint32_t* d_dst, size_t n, void* stream);
+
 /* Synthetic keys of SURVEY §8(d): key[i] = splitmix64(seed ^ (first_index + i)) truncated
  * to key_bytes (4 or 8). */
 grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t seed,
