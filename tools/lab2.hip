@@ -51,6 +51,41 @@ __global__ __launch_bounds__(256) void read_u(const uint4* __restrict__ in, uint
 //   the unaligned boundaries of real digit runs); MODE 5: as 3 with MODE 2's tile mapping
 // POL (store policy): 0 default, 1 nontemporal, 2 agent-scope (sc1, write-through),
 // 3 nontemporal for lines inside a run and default for the run's partial head / tail lines
+// MODE 8: the runs of MODE 3 (every destination one key past alignment), but stored
+// destination-aligned: wave w writes runs w, w + WAVES, ...; a run starting at D is cut into
+// 64-key chunks at (D & ~63) + 64 k, lane l writing key A + l of its chunk when inside the run
+// (every wave-instruction writes one aligned 256-B window of one run).  POL 3: nontemporal
+// for lines wholly inside the run, default for its head / tail lines.
+template <int BLOCK, int ITEMS, int POL>
+__global__ __launch_bounds__(BLOCK) void scatter_emu_aligned(const uint32_t* __restrict__ in,
+                                                             uint32_t* __restrict__ out,
+                                                             uint32_t n) {
+  constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 256, WAVES = BLOCK / 64;
+  extern __shared__ uint32_t pad_lds[];
+  const uint32_t T = blockIdx.x;
+  if ((T + 1) * TILE > n) return;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t key[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) key[j] = in[T * TILE + w * 64 * ITEMS + j * 64 + lane];
+  if (n == 0) pad_lds[threadIdx.x] = key[0];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) acc ^= key[j];
+  for (uint32_t r = w; r < 256; r += WAVES) {
+    const uint32_t rs = r * (n / 256) + T * RUN + 1, re = rs + RUN;   // run [rs, re)
+    for (uint32_t A = rs & ~63u; A < re; A += 64) {
+      const uint32_t dst = A + lane;
+      if (dst >= rs && dst < re && dst < n) {
+        const uint32_t v = acc + dst;
+        const uint32_t ls = dst & ~31u;
+        if (POL == 3 && ls >= rs && ls + 32 <= re) __builtin_nontemporal_store(v, &out[dst]);
+        else out[dst] = v;
+      }
+    }
+  }
+}
+
 template <int BLOCK, int ITEMS, int MODE, int POL = 0>
 __global__ __launch_bounds__(BLOCK) void scatter_emu(const uint32_t* __restrict__ in,
                                                      uint32_t* __restrict__ out, uint32_t n) {
@@ -216,6 +251,10 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
     case 102407201: k = (const void*)scatter_emu<1024, 72, 1>; break;
     case 102407203: k = (const void*)scatter_emu<1024, 72, 3>; break;
     case 102407205: k = (const void*)scatter_emu<1024, 72, 5>; break;
+    case 102403608: k = (const void*)scatter_emu_aligned<1024, 36, 0>; break;
+    case 102403638: k = (const void*)scatter_emu_aligned<1024, 36, 3>; break;
+    case 102404808: k = (const void*)scatter_emu_aligned<1024, 48, 0>; break;
+    case 102404838: k = (const void*)scatter_emu_aligned<1024, 48, 3>; break;
     default: return -1;
   }
   void* args[] = {&i, &o, &n};
