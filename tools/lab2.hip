@@ -380,7 +380,7 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
 // v6 pass at 4-bit digits: block, items, minw, opt, grid
 int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in, void* out,
                uint32_t n, const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2,
-               uint32_t* err, void* stream) {
+               uint32_t* err, void* stream, uint32_t hist_stride, uint32_t range_tiles) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   const long code = ((block * 1000L + items) * 10 + minw) * 10000000L + opt;
   switch (code) {
@@ -391,11 +391,12 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
     hipLaunchKernelGGL((grs::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
                        dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
                        grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
-                       (const grs::RadixDigit<uint32_t>*)nullptr);                             \
+                       (const grs::RadixDigit<uint32_t>*)nullptr, hist_stride, range_tiles);   \
   } break;
     V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
     V(1024, 32, 1, 8) V(1024, 32, 1, 512) V(1024, 32, 1, 520) V(1024, 32, 1, 528)
     V(1024, 32, 1, 2097152) V(1024, 32, 1, 2097160) V(1024, 32, 1, 2097168)
+    V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
 #undef V
     default:
       return -1;

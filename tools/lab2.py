@@ -65,17 +65,17 @@ def main():
 
     xr_hist = {}
 
-    def range_hist(kb, tile):
-        """per-XCD-range digit-0 histograms [8][256] and the range size in tiles (OPT 1048576)"""
-        if (kb, tile) not in xr_hist:
+    def range_hist(kb, tile, radix=256):
+        """per-XCD-range digit-0 histograms [8][radix] and the range size in tiles (OPT 1048576)"""
+        if (kb, tile, radix) not in xr_hist:
             keys = bufs[kb][0]
             tiles = (n + tile - 1) // tile
             R = ((tiles + 7) // 8 + 7) // 8 * 8
-            k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64) & 255
-            hs = [torch.bincount(k64[min(n, c * R * tile):min(n, (c + 1) * R * tile)], minlength=256)
+            k64 = keys.view(torch.int32 if kb == 32 else torch.int64).to(torch.int64) & (radix - 1)
+            hs = [torch.bincount(k64[min(n, c * R * tile):min(n, (c + 1) * R * tile)], minlength=radix)
                   for c in range(8)]
-            xr_hist[(kb, tile)] = (torch.stack(hs).to(torch.int32).view(torch.uint32).contiguous(), R)
-        return xr_hist[(kb, tile)]
+            xr_hist[(kb, tile, radix)] = (torch.stack(hs).to(torch.int32).view(torch.uint32).contiguous(), R)
+        return xr_hist[(kb, tile, radix)]
 
     def run(v):
         kind, kb, pairs, block, items = v[:5]
@@ -90,8 +90,13 @@ def main():
             rc = L.lab2_v4rb4(block, items, v[5], v[6], P(keys), P(out), ctypes.c_uint32(n),
                               P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
         elif kind == "r6":   # r6:32:0:block:items:minw:opt:grid  (4-bit digits, persistent)
+            h4, stride, rtiles = hist4[kb], 0, 0
+            if v[6] & 1048576:
+                h4, rtiles = range_hist(kb, block * items, 16)
+                stride = 16
             rc = L.lab2_v6rb4(block, items, v[5], v[6], v[7], P(keys), P(out), ctypes.c_uint32(n),
-                              P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)
+                              P(h4), P(ticket), P(st), P(st2), P(err), sp, ctypes.c_uint32(stride),
+                              ctypes.c_uint32(rtiles))
         elif kind == "v4":
             rc = L.lab2_v4(kb, pairs, block, items, v[5], v[6], *args)
         elif kind == "v6":   # v6:kb:pairs:block:items:minw:opt:grid
