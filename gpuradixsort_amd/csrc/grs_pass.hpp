@@ -674,7 +674,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // after their look-back has finished: vmcnt retires loads in issue order, so a look-back poll
   // issued behind the prefetch would wait for all of it
   constexpr bool PF_SPLIT = (OPT & 524288) != 0;
-  if constexpr (PF && ROUNDS == 1 && !PF_LATE) {   // two rounds: after round 2 sits in LDS
+  // NOPF (OPT 8388608): persistent workgroups without prefetch: the next ticket is drawn during
+  // the ranking, its tile loaded by the caller's loop once this tile is stored
+  constexpr bool NOPF = (OPT & 8388608) != 0;
+  if constexpr (PF && ROUNDS == 1 && !PF_LATE && !NOPF) {   // two rounds: after round 2 sits in LDS
     next = __builtin_amdgcn_readfirstlane(sm.next);
     if (next < tiles && (!PF_SPLIT || w >= static_cast<uint32_t>(DW)))
       tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
@@ -709,7 +712,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         sm.jsplit = cstart + ((D + (LTILE - lstart)) - (D & ~63u)) / 64u;
     }
   }
-  if constexpr (PF && ROUNDS == 1 && !PF_LATE && PF_SPLIT) {
+  if constexpr (PF && ROUNDS == 1 && !PF_LATE && PF_SPLIT && !NOPF) {
     if (next < tiles && w < static_cast<uint32_t>(DW))
       tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
@@ -798,7 +801,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         }
       }
       lds_barrier();
-      if constexpr (PF) {
+      if constexpr (PF && !NOPF) {
         // the last round's keys are in LDS: the registers take the next tile's loads, which
         // fly behind this round's stores
         if (rr == ROUNDS - 1) {
@@ -837,7 +840,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       }
     }
   }
-  if constexpr (PF && ROUNDS == 1 && PF_LATE) {   // the next tile's loads behind the stores
+  if constexpr (PF && NOPF) next = __builtin_amdgcn_readfirstlane(sm.next);
+  if constexpr (PF && ROUNDS == 1 && PF_LATE && !NOPF) {   // the next tile's loads behind the stores
     next = __builtin_amdgcn_readfirstlane(sm.next);
     if (next < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
@@ -885,6 +889,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
     lds_barrier();
     tile = __builtin_amdgcn_readfirstlane(sm.ticket);
     if (tile != guess) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
+  } else if constexpr ((OPT & 4194304) != 0) {
+    // tile = blockIdx.x: no ticket round trip before the loads (see DISPATCH_ORDER below)
+    tile = blockIdx.x;
+    tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
+    for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    lds_barrier();
   } else {
     if (t == 0)
       sm.ticket = XR ? draw_ticket_xr(ticket, (n + SM::TILE - 1) / SM::TILE, range_tiles)
@@ -956,6 +966,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     // every LDS read of the finished tile is done before the counters are reset
     lds_barrier();
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    if constexpr ((OPT & 8388608) != 0) {
+      if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);
+    }
     lds_barrier();
   }
 }

@@ -336,6 +336,8 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 2097424) V(32, 0, 1024, 36, 1, 2097432)
     V(32, 0, 768, 64, 1, 2098192) V(32, 0, 768, 64, 1, 2098200) V(32, 1, 768, 40, 1, 2098192)
     V(64, 0, 1024, 17, 1, 2097424)
+    V(32, 0, 1024, 36, 1, 4194576) V(32, 0, 1024, 36, 1, 4194584) V(32, 0, 768, 64, 1, 4195344)
+    V(32, 0, 768, 64, 1, 4195352) V(32, 1, 768, 40, 1, 4195344) V(64, 0, 768, 44, 1, 4195344)
 #undef V
     default:
       return -1;
@@ -370,6 +372,8 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1573136) V(32, 0, 1024, 36, 1, 2097424)
     V(32, 0, 768, 64, 1, 525328) V(32, 1, 1024, 17, 1, 524560) V(64, 0, 1024, 17, 1, 524560)
     V(32, 0, 1024, 36, 1, 524544) V(32, 0, 1024, 36, 1, 524552)
+    V(32, 0, 1024, 36, 1, 8388880) V(32, 0, 1024, 36, 1, 8388888) V(32, 0, 768, 64, 1, 8389648)
+    V(32, 0, 768, 64, 1, 8389656)
 #undef V
     default:
       return -1;
@@ -397,6 +401,8 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
     V(1024, 32, 1, 8) V(1024, 32, 1, 512) V(1024, 32, 1, 520) V(1024, 32, 1, 528)
     V(1024, 32, 1, 2097152) V(1024, 32, 1, 2097160) V(1024, 32, 1, 2097168)
     V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
+    V(1024, 32, 1, 524288) V(1024, 32, 1, 524296) V(512, 32, 2, 524288) V(512, 32, 2, 8)
+    V(1024, 32, 1, 64) V(1024, 32, 1, 72)
 #undef V
     default:
       return -1;
