@@ -62,6 +62,7 @@ OPTIONS = {
     "sharded_path": (6, {"auto": 0, "general": 1}),
     "sharded_send": (7, {"regions": 0, "contig": 1}),
     "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
+    "merge": (9, {"rounds": 0, "kway": 1}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares

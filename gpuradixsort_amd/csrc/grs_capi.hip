@@ -276,6 +276,7 @@ struct grs_sorter {
   size_t codec_bytes = 0;
   // options (grs_set_option; defaults pick by size; nothing is read from the environment)
   int sharded_exchange = 0;        // GRS_OPT_EXCHANGE: 0 auto, 1 partition-first, 2 presorted
+  int merge_mode = 0;              // GRS_OPT_MERGE: 0 ceil(log2 k) 2-way rounds, 1 one k-way pass
   // last grs_sort_sharded call, with profiling on: events at call start / exchange start /
   // exchange end / call end, and the bytes that crossed the links (self part excluded)
   hipEvent_t xev[4] = {};
@@ -438,6 +439,10 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value < 0 || value > 2) return bad();
       s->sharded_exchange = value;
       break;
+    case GRS_OPT_MERGE:
+      if (value < 0 || value > 1) return bad();
+      s->merge_mode = value;
+      break;
 
     default:
       return set_err(GRS_EINVAL, "grs_set_option: unknown option");
@@ -474,6 +479,7 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_SHARDED_PATH: *value = s->sharded_general ? 1 : 0; break;
     case GRS_OPT_SHARDED_SEND: *value = s->sharded_contig ? 1 : 0; break;
     case GRS_OPT_EXCHANGE: *value = s->sharded_exchange; break;
+    case GRS_OPT_MERGE: *value = s->merge_mode; break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -1591,7 +1597,10 @@ grs_status codec_scratch(grs_sorter* s, size_t n_enc, size_t n_merge, int g, Cod
   auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
   const size_t nb = codec_blocks_max(n_enc, g);
   const size_t scan = grs_scan_scratch_bytes(nb + 1);
-  const size_t cor = n_merge / grs::kMergeTile + 2 * grs::kMaxRanks + 2;
+  // co-ranks: the 2-way rounds' boundaries, or the k-way merge's samples + (tiles + 1) rows
+  const size_t ns = n_merge / grs::kMkSpacing + grs::kMaxRanks + 1;
+  const size_t cor = std::max(n_merge / grs::kMergeTile + 2 * grs::kMaxRanks + 2,
+                              ns + 64 + (ns / grs::kMkSPT + 2) * grs::kMkStride);
   const size_t need = al(4 * (2 * g + 2)) + al(4 * 2 * g) + 2 * al(4 * (nb + 1)) + al(8 * nb) +
                       al(scan) + al(4 * cor);
   const grs_status r = grow_buf(&s->codec_buf, &s->codec_bytes, need, "presorted exchange scratch");
@@ -1654,6 +1663,8 @@ grs_status codec_decode_merge(grs_sorter* s, const uint32_t* recv, int g, const 
   src.blk_base[g] = blocks;
   int rounds = 0;
   for (int k = g; k > 1; k = (k + 1) / 2) ++rounds;
+  const bool kway = s->merge_mode == 1;
+  if (kway) rounds = g > 1 ? 1 : 0;
   uint32_t* alt = static_cast<uint32_t*>(s->alt_keys);
   uint32_t* in = (rounds & 1) ? alt : out;   // the last round writes out
   uint32_t* o = (rounds & 1) ? out : alt;
@@ -1661,6 +1672,33 @@ grs_status codec_decode_merge(grs_sorter* s, const uint32_t* recv, int g, const 
     hipLaunchKernelGGL(grs::grs_codec_unpack, dim3((blocks + 4 * grs::kCodecBPW - 1) / (4 * grs::kCodecBPW)),
                        dim3(256), 0, st, recv, src, in);
     GRS_HIP(hipGetLastError());
+  }
+  if (kway) {
+    if (g <= 1 || n_total == 0) return GRS_OK;
+    grs::MergeK mk{};
+    mk.k = static_cast<uint32_t>(g);
+    mk.kp = 1;
+    while (mk.kp < mk.k) mk.kp <<= 1;
+    uint32_t ns = 0;
+    for (int p = 0; p < g; ++p) {
+      mk.off[p] = src.run_off[p];
+      mk.sbase[p] = ns;
+      ns += (lens[p] + grs::kMkSpacing - 1) / grs::kMkSpacing;
+    }
+    mk.off[g] = static_cast<uint32_t>(n_total);
+    mk.sbase[g] = ns;
+    uint32_t* samp = cs.corank;
+    uint32_t* cor = cs.corank + ((ns + 63u) & ~63u);
+    hipLaunchKernelGGL(grs::grs_mergek_samples, dim3((ns + 255) / 256), dim3(256), 0, st, in, mk, samp);
+    GRS_HIP(hipGetLastError());
+    const uint64_t threads = static_cast<uint64_t>(ns + 1) * mk.kp;
+    hipLaunchKernelGGL(grs::grs_mergek_bounds, dim3(static_cast<uint32_t>((threads + 255) / 256)), dim3(256),
+                       0, st, in, mk, samp, cor);
+    GRS_HIP(hipGetLastError());
+    hipLaunchKernelGGL(grs::grs_mergek_tiles, dim3(grs::mk_tiles(mk)), dim3(grs::kMkBlock), 0, st, in, o,
+                       mk, cor);
+    GRS_HIP(hipGetLastError());
+    return GRS_OK;
   }
   uint32_t off[grs::kMaxRanks + 2];
   for (int p = 0; p < g; ++p) off[p] = src.run_off[p];

@@ -16,8 +16,11 @@
 //                                                   exclusive scan of the block words, grs_codec_pack
 //   exchange        one send / recv of u32 words per peer (RCCL, or any transport)
 //   decode          every received block -> its run, runs in source-rank order  grs_codec_unpack
-//   merge           2-way merge-path rounds over the runs (ties: the lower run first, i.e.
-//                   global input order), ceil(log2 G) rounds         grs_merge_corank/tiles
+//   merge           ceil(log2 G) rounds of a 2-way merge path over the runs (ties: the lower
+//                   run first, i.e. global input order)               grs_merge_corank/tiles
+//                   or (option GRS_OPT_MERGE = 1) ONE k-way pass: sample-delimited tiles
+//                   merged in LDS, grs_mergek_samples/bounds/tiles -- correct, and measured
+//                   slower at 8 ranks
 //
 // The order of the result is the same as the partition-first path's: bucket b holds the
 // range of the global (key, global index) order between splitters b-1 and b.
@@ -431,6 +434,215 @@ __global__ __launch_bounds__(256) void grs_merge_tiles(const uint32_t* __restric
   for (int v = 0; v < kMergeVT; ++v) {
     const uint32_t q = threadIdx.x + 256 * v;
     if (q < len) O[q] = lout[q + (q >> 5)];
+  }
+}
+
+// ---- one-round k-way merge ----------------------------------------------------------------
+// The k <= 16 received runs are merged in ONE pass over HBM (read 4 B + write 4 B per key)
+// instead of ceil(log2 k) 2-way rounds.  Total order: (key, run, index), i.e. ties go to the
+// lower run (= global input order).
+//   samples   every kMkSpacing-th element of every run (the decoded blocks' first keys)
+//   bounds    each sample's rank among ALL samples (k binary searches in the runs' sample
+//             lists, one lane per run); every kMkSPT-th sample in that merged order is a tile
+//             boundary, and since a boundary is an element of the input, its exact co-rank in
+//             run q is one binary search inside the kMkSpacing-wide window the sample rank
+//             leaves: for runs before its own the count of keys <= it, for runs after it the
+//             count of keys < it, for its own run its index
+//   tiles     tile j = the elements between boundaries j and j + 1: at most (kMkSPT + k)
+//             blocks of kMkSpacing elements (each run adds at most one partial block to its
+//             samples in the range), loaded into LDS, merged in log2(k) 2-way rounds inside
+//             LDS (merge path per thread, ties to the lower group), written out contiguously
+constexpr int kMkSpacing = kCodecBlock;
+constexpr int kMkSPT = 16;
+constexpr int kMkMaxTile = kMkSpacing * (kMkSPT + kMaxRanks);   // 8192
+constexpr int kMkBlock = 1024;
+constexpr int kMkVT = kMkMaxTile / kMkBlock;                      // 8 loads / stores per thread
+constexpr int kMkChunk = 8;                                       // outputs per merge step
+constexpr int kMkStride = kMaxRanks;                              // co-rank row stride
+
+struct MergeK {
+  uint32_t k;                      // runs (1..kMaxRanks)
+  uint32_t kp;                     // k rounded up to a power of two (lanes per sample)
+  uint32_t off[kMaxRanks + 1];     // run q = in[off[q], off[q + 1])
+  uint32_t sbase[kMaxRanks + 1];   // run q's samples = samp[sbase[q], sbase[q + 1])
+};
+
+__host__ __device__ __forceinline__ uint32_t mk_tiles(const MergeK& m) {
+  return (m.sbase[m.k] + kMkSPT - 1) / kMkSPT;
+}
+
+__device__ __forceinline__ uint32_t mk_run_of(const MergeK& m, uint32_t s) {
+  uint32_t p = 0;
+  while (p + 1 < m.k && m.sbase[p + 1] <= s) ++p;
+  return p;
+}
+
+// samp[s] = element kMkSpacing * (s - sbase[p]) of run p
+__global__ __launch_bounds__(256) void grs_mergek_samples(const uint32_t* __restrict__ in,
+                                                          const MergeK m,
+                                                          uint32_t* __restrict__ samp) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= m.sbase[m.k]) return;
+  const uint32_t p = mk_run_of(m, s);
+  samp[s] = in[m.off[p] + (s - m.sbase[p]) * kMkSpacing];
+}
+
+// First index i in [lo, hi) of a[] where key <= v (LE) / key < v (!LE) fails; the predicate
+// holds before lo.
+template <bool LE>
+__device__ __forceinline__ uint32_t mk_search(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint32_t x = a[mid];
+    if (LE ? x <= v : x < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// kp lanes per sample: lane q resolves run q.  corank[j * kMkStride + q] = elements of run q
+// before tile j's first element; row mk_tiles(m) = the run lengths.
+__global__ __launch_bounds__(256) void grs_mergek_bounds(const uint32_t* __restrict__ in,
+                                                         const MergeK m,
+                                                         const uint32_t* __restrict__ samp,
+                                                         uint32_t* __restrict__ corank) {
+  // grid: (samples + 1) * kp threads; a lane group (kp lanes of one wave) shares its sample
+  const uint32_t tid = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t s = tid / m.kp, q = tid % m.kp;
+  const uint32_t ns = m.sbase[m.k];
+  if (s > ns) return;
+  if (s == ns) {   // the end row
+    if (q < m.k) corank[static_cast<size_t>(mk_tiles(m)) * kMkStride + q] = m.off[q + 1] - m.off[q];
+    return;
+  }
+  const uint32_t p = mk_run_of(m, s);
+  const uint32_t mi = s - m.sbase[p];
+  const uint32_t v = samp[s];
+  uint32_t rank = 0;
+  if (q < m.k) {
+    const uint32_t* sq = samp + m.sbase[q];
+    const uint32_t nq = m.sbase[q + 1] - m.sbase[q];
+    rank = q == p ? mi : q < p ? mk_search<true>(sq, 0, nq, v) : mk_search<false>(sq, 0, nq, v);
+  }
+  uint32_t r = rank;
+  for (uint32_t o = 1; o < m.kp; o <<= 1) r += __shfl_xor(r, o, GRS_WAVE);
+  if (r % kMkSPT != 0 || q >= m.k) return;
+  uint32_t c;
+  if (q == p) {
+    c = mi * kMkSpacing;
+  } else {
+    const uint32_t len = m.off[q + 1] - m.off[q];
+    const uint32_t lo = rank ? (rank - 1) * kMkSpacing + 1 : 0;
+    const uint32_t hi = rank ? min(rank * kMkSpacing, len) : 0;
+    const uint32_t* rq = in + m.off[q];
+    c = q < p ? mk_search<true>(rq, lo, hi, v) : mk_search<false>(rq, lo, hi, v);
+  }
+  corank[static_cast<size_t>(r / kMkSPT) * kMkStride + q] = c;
+}
+
+// LDS address of tile element x: one pad word per 8 (a lane's 8-output chunk starts 9 words
+// after its neighbour's: the chunk writes of a wave hit 64 different banks)
+__device__ __forceinline__ uint32_t mk_pad(uint32_t x) { return x + (x >> 3); }
+
+// One workgroup per tile (2 per CU: 2 x 72 KB of LDS, 32 waves).
+__global__ __launch_bounds__(kMkBlock, 2) void grs_mergek_tiles(const uint32_t* __restrict__ in,
+                                                                uint32_t* __restrict__ out,
+                                                                const MergeK m,
+                                                                const uint32_t* __restrict__ corank) {
+  constexpr uint32_t PADN = kMkMaxTile + kMkMaxTile / 8;
+  __shared__ uint32_t buf[2][PADN];
+  __shared__ uint32_t P[kMaxRanks + 1];    // segment starts in the tile (kp segments, padded)
+  __shared__ uint32_t S[kMaxRanks];        // segment starts in the runs
+  __shared__ uint32_t O0;
+  const uint32_t j = blockIdx.x, t = threadIdx.x;
+  if (t < GRS_WAVE) {   // wave 0: lane q loads run q's two co-ranks (one round trip), DPP scans
+    const uint32_t c0 = t < m.k ? corank[static_cast<size_t>(j) * kMkStride + t] : 0u;
+    const uint32_t c1 = t < m.k ? corank[static_cast<size_t>(j + 1) * kMkStride + t] : 0u;
+    const uint32_t l = c1 - c0;
+    const uint32_t li = wave_scan_dpp(l), oi = wave_scan_dpp(c0);
+    if (t <= m.kp) P[t] = li - l;   // lanes past k hold l = 0: P[kp] = the tile's length
+    if (t < m.kp) S[t] = m.off[min(t, m.k)] + c0;
+    if (t == GRS_WAVE - 1) O0 = oi;
+  }
+  __syncthreads();
+  const uint32_t len = min(P[m.kp], static_cast<uint32_t>(kMkMaxTile));
+  // the tile's segments, all loads in flight, then LDS
+  uint32_t x[kMkVT];
+  uint32_t q = 0;   // segment of element e (e grows with v)
+#pragma unroll
+  for (int v = 0; v < kMkVT; ++v) {
+    const uint32_t e = t + kMkBlock * v;
+    x[v] = 0;
+    if (e < len) {
+      while (q + 1 < m.kp && P[q + 1] <= e) ++q;
+      x[v] = in[S[q] + (e - P[q])];
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < kMkVT; ++v) {
+    const uint32_t e = t + kMkBlock * v;
+    if (e < len) buf[0][mk_pad(e)] = x[v];
+  }
+  __syncthreads();
+  // log2(kp) rounds; round w merges segment groups [g, g + w) and [g + w, g + 2w) in chunks of
+  // kMkChunk outputs: a chunk's merge-path co-rank, kMkChunk candidates from each side (all
+  // loads in flight), one 2 kMkChunk-element bitonic merge in registers, its first outputs.  (The values are
+  // bare keys: which of two equal keys lands first cannot be told apart.)
+  uint32_t cur = 0;
+  for (uint32_t w = 1; w < m.kp; w <<= 1) {
+    const uint32_t* src = buf[cur];
+    uint32_t* dst = buf[cur ^ 1];
+    const uint32_t npairs = m.kp / (2 * w);
+    for (uint32_t c = t;; c += kMkBlock) {
+      uint32_t acc = 0, a0 = 0, b0 = 0, b1 = 0;
+      bool found = false;
+      for (uint32_t g = 0; g < npairs; ++g) {
+        a0 = P[2 * g * w];
+        b0 = P[2 * g * w + w];
+        b1 = P[2 * g * w + 2 * w];
+        const uint32_t nch = (b1 - a0 + kMkChunk - 1) / kMkChunk;
+        if (c < acc + nch) {
+          found = true;
+          break;
+        }
+        acc += nch;
+      }
+      if (!found) break;
+      const uint32_t d = (c - acc) * kMkChunk;
+      const uint32_t al = b0 - a0, bl = b1 - b0;
+      const uint32_t nout = min(static_cast<uint32_t>(kMkChunk), al + bl - d);
+      const uint32_t ia = merge_corank(d, al, bl, [&](uint32_t i) { return src[mk_pad(a0 + i)]; },
+                                       [&](uint32_t i) { return src[mk_pad(b0 + i)]; });
+      const uint32_t ib = d - ia;
+      constexpr int C = kMkChunk;
+      uint32_t v[2 * C];
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        v[i] = ia + i < al ? src[mk_pad(a0 + ia + i)] : 0xFFFFFFFFu;
+        v[2 * C - 1 - i] = ib + i < bl ? src[mk_pad(b0 + ib + i)] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int st = C; st >= 1; st >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 2 * C; ++i) {
+          if ((i & st) == 0) {
+            const uint32_t lo = min(v[i], v[i + st]), hi = max(v[i], v[i + st]);
+            v[i] = lo;
+            v[i + st] = hi;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < C; ++i)
+        if (static_cast<uint32_t>(i) < nout) dst[mk_pad(a0 + d + i)] = v[i];
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  uint32_t* o = out + O0;
+#pragma unroll
+  for (int v = 0; v < kMkVT; ++v) {
+    const uint32_t e = t + kMkBlock * v;
+    if (e < len) o[e] = buf[cur][mk_pad(e)];
   }
 }
 

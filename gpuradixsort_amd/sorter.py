@@ -57,7 +57,7 @@ class RadixSorter:
     def set_option(self, name: str, value) -> None:
         """Pin a kernel choice the defaults make by size (grs_set_option): name is one of
         _lib.OPTIONS ("tile", "xl", "pass", "records", "rank", "sharded_path", "sharded_send",
-        "exchange"), value an int or one of that option's value names."""
+        "exchange", "merge"), value an int or one of that option's value names."""
         opt, names = OPTIONS[name]
         v = names[value] if isinstance(value, str) else int(value)
         check(lib().grs_set_option(self._h, opt, v), f"grs_set_option({name}={value})")

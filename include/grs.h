@@ -123,7 +123,10 @@ typedef enum grs_option {
                                 1 the G-rank path (a one-GPU rehearsal of the exchange) */
   GRS_OPT_SHARDED_SEND = 7,  /* partition-first exchange: 0 (default) G regions of n_local items
                                 where they fit, 1 bucket histogram + contiguous buckets */
-  GRS_OPT_EXCHANGE = 8       /* 0 by rank count (default), 1 partition-first, 2 presorted */
+  GRS_OPT_EXCHANGE = 8,      /* 0 by rank count (default), 1 partition-first, 2 presorted */
+  GRS_OPT_MERGE = 9          /* presorted exchange, receive side: 0 (default) ceil(log2 k)
+                                2-way merge rounds over the k received runs, 1 one k-way merge
+                                pass (sample-delimited tiles merged in LDS; slower at 8 ranks) */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);

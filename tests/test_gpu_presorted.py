@@ -31,9 +31,10 @@ def _dist(name, n, rng):
     raise ValueError(name)
 
 
-def sim_presorted(shards, gpu, cap=None):
+def sim_presorted(shards, gpu, cap=None, merge="rounds"):
     """Simulate grs_sort_sharded's presorted exchange over len(shards) ranks on one device.
-    Returns the ranks' outputs (numpy) and the G x 2G size matrix."""
+    Returns the ranks' outputs (numpy) and the G x 2G size matrix.  merge: the receive side's
+    2-way rounds ("rounds", the default) or its one k-way pass ("kway")."""
     import gpuradixsort_amd as grs
     from gpuradixsort_amd import _lib
     from gpuradixsort_amd.sharded import shard_decode_merge, shard_encode, shard_sample
@@ -42,7 +43,7 @@ def sim_presorted(shards, gpu, cap=None):
     S = int(_lib.lib().grs_shard_samples_per_rank(G))
     total = sum(len(s) for s in shards)
     cap = cap or max(total, 1)
-    sorter = grs.RadixSorter(cap, key_bits=32, device=gpu.index)
+    sorter = grs.RadixSorter(cap, key_bits=32, device=gpu.index, options={"merge": merge})
     sorted_, sks, sps = [], [], []
     for sh in shards:
         k = torch.from_numpy(sh).to(gpu)
@@ -78,13 +79,14 @@ def sim_presorted(shards, gpu, cap=None):
     return outs, mat
 
 
-@pytest.mark.parametrize("G", [1, 2, 3, 4, 8, 16])
+@pytest.mark.parametrize("merge", ["kway", "rounds"])
+@pytest.mark.parametrize("G", [1, 2, 3, 4, 5, 8, 16])
 @pytest.mark.parametrize("name", ["uniform", "all_equal", "few_unique", "skewed"])
-def test_presorted_sim_matches_sort(gpu, G, name):
+def test_presorted_sim_matches_sort(gpu, G, name, merge):
     rng = np.random.default_rng(G * 31 + len(name))
     n_local = 200_003
     shards = [_dist(name, n_local + 1000 * r, rng) for r in range(G)]
-    outs, mat = sim_presorted(shards, gpu)
+    outs, mat = sim_presorted(shards, gpu, merge=merge)
     allk = np.concatenate(shards)
     got = np.concatenate(outs)
     assert np.array_equal(got, np.sort(allk))
@@ -95,13 +97,14 @@ def test_presorted_sim_matches_sort(gpu, G, name):
         assert sizes.max() / sizes.mean() <= 1.1, sizes
 
 
+@pytest.mark.parametrize("merge", ["kway", "rounds"])
 @pytest.mark.parametrize("name", ["max_gaps", "sorted_desc", "uniform"])
-def test_presorted_sim_edges(gpu, name):
+def test_presorted_sim_edges(gpu, name, merge):
     """32-bit delta widths, ragged last blocks, empty shards, tiny shards, one-key shards."""
     rng = np.random.default_rng(5)
     for lens in ([0, 0, 0], [1, 0, 5, 255], [256, 257, 1, 4095, 4097], [0, 100_000], [70_001] * 5):
         shards = [_dist(name, n, rng) for n in lens]
-        outs, _ = sim_presorted(shards, gpu)
+        outs, _ = sim_presorted(shards, gpu, merge=merge)
         assert np.array_equal(np.concatenate(outs), np.sort(np.concatenate(shards))), lens
 
 
@@ -166,3 +169,43 @@ def test_presorted_world1_empty_and_tiny(gpu, monkeypatch):
         s.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("merge", ["kway", "rounds"])
+@pytest.mark.parametrize("k", [2, 3, 7, 8, 13, 16])
+def test_merge_at_run_and_tie_boundaries(gpu, k, merge):
+    """The k-way merge on its own (grs_shard_decode_merge of encoded sorted runs): runs of very
+    different lengths, long runs of one key crossing the sample spacing and the tile boundaries
+    in several runs at once, and keys whose only difference is the run they come from."""
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd import _lib
+    from gpuradixsort_amd.sharded import shard_decode_merge, shard_encode, shard_sample
+
+    S = int(_lib.lib().grs_shard_samples_per_rank(1))
+    rng = np.random.default_rng(100 + k)
+    runs = []
+    for q in range(k):
+        n = int(rng.choice([0, 1, 255, 256, 257, 4096 * 3 + 17, 60_000 + 1000 * q]))
+        base = rng.integers(0, 50, n, dtype=np.uint64).astype(np.uint32) * np.uint32(1 << 26)
+        noise = rng.integers(0, 3, n, dtype=np.uint64).astype(np.uint32)
+        runs.append(np.sort(base + noise))
+    total = sum(len(r) for r in runs)
+    sorter = grs.RadixSorter(max(total, 1), key_bits=32, device=gpu.index, options={"merge": merge})
+    # each run becomes the single bucket of a one-rank encode (G = 1: the whole shard)
+    parts, offs, lens, off = [], [], [], 0
+    for r in runs:
+        t = torch.from_numpy(r).to(gpu) if len(r) else torch.zeros(1, dtype=torch.uint32, device=gpu)
+        sk, sp = shard_sample(t, len(r), S)
+        send, sz = shard_encode(sorter, t, len(r), sk, sp, 1, 0)
+        w = int(sz.cpu().numpy()[1])
+        parts.append(send[:w])
+        offs.append(off)
+        lens.append(len(r))
+        off += w
+    recv = torch.cat(parts) if off else torch.zeros(1, dtype=torch.uint32, device=gpu)
+    out = torch.empty(max(total, 1), dtype=torch.uint32, device=gpu)
+    m = shard_decode_merge(sorter, recv, offs, lens, out)
+    sorter.check_error()
+    assert m == total
+    assert np.array_equal(out[:m].cpu().numpy(), np.sort(np.concatenate(runs)))
+    sorter.close()

@@ -8,7 +8,8 @@ python tools/bench_presorted_steps.py [--ranks 8] [--total 2^30] [--reps 10] [--
 Prints one JSON line per step and an estimate of the step at N ranks:
   local_sort       grs_sort of one shard
   encode           grs_shard_encode of rank 0 (splitters, bounds, block widths, scan, pack)
-  decode_merge     grs_shard_decode_merge of receiver 0 (decode + ceil(log2 N) merge rounds)
+  decode_merge     grs_shard_decode_merge of receiver 0: decode + ceil(log2 N) 2-way merge
+                   rounds (the default), and decode + the one-pass k-way merge (option)
   exchange_words   encoded bytes per key; the busiest link's bytes / link-gbs gives the exchange
 """
 import argparse
@@ -99,11 +100,17 @@ def main():
     recv = torch.cat(parts)
     m = sum(lens)
     out = torch.empty(m, dtype=torch.uint32, device=dev)
-    ms_dm = timed(lambda: shard_decode_merge(s, recv, offs, lens, out), a.reps)
-    s.check_error()
-    o64 = out.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-    ok = bool(torch.all(o64[1:] >= o64[:-1]).item())
-    print(json.dumps({"step": "decode_merge", "n": m, "ms": round(ms_dm, 4), "sorted": ok}), flush=True)
+    ms_modes = {}
+    for mode in ("rounds", "kway"):   # the receive side's two merges (GRS_OPT_MERGE)
+        s.set_option("merge", mode)
+        ms_modes[mode] = timed(lambda: shard_decode_merge(s, recv, offs, lens, out), a.reps)
+        s.check_error()
+        o64 = out.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        ok = bool(torch.all(o64[1:] >= o64[:-1]).item())
+        print(json.dumps({"step": "decode_merge", "merge": mode, "n": m, "ms": round(ms_modes[mode], 4),
+                          "sorted": ok}), flush=True)
+    ms_dm = ms_modes["rounds"]
+    s.set_option("merge", "rounds")
 
     # busiest link: the largest off-diagonal bucket (one xGMI link per rank pair)
     off_diag = [int(words[p, q]) for p in range(G) for q in range(G) if p != q]
