@@ -3,8 +3,9 @@
 // The pass driver replaces ParallelSort::Sort (Source/ComputeControllers/ParallelSort.cpp:168-298):
 // where the reference issues 1 + 32 x 4 GLSL dispatches with a glMemoryBarrier after each,
 // one grs_sort call issues
-//     hipMemsetAsync(control block)  -> grs_upfront_hist2  -> P x grs_onesweep_v4 / v6
-// on one stream (P = ceil((end_bit - begin_bit) / radix_bits); 4 launches for u32 at 8-bit
+//     grs_upfront_hist2  -> P x grs_onesweep_v4 / v6
+// on one stream (no memset: the histogram kernel zeroes the other of two control blocks for
+// the next call, see grs_sorter::cb_i) (P = ceil((end_bit - begin_bit) / radix_bits); 4 launches for u32 at 8-bit
 // digits), plus one D2D copy when P is odd so the result lands back in the caller's buffer
 // (the reference's glCopyBufferSubData, ParallelSort.cpp:312-318).
 #include <hip/hip_runtime.h>
@@ -53,13 +54,19 @@ grs_status set_err(grs_status s, const std::string& msg) {
 // in VGPRs, LDS takes half the tile at a time; 32-bit wave counters): 22K-pair tiles, same
 // process (tools/lab2.py, 2^28 pairs, ms per pass) 1.37 vs 1.48 and 1.45 vs 1.72 on two boxes
 // against one-round 11K tiles.  u32 pairs (26K tiles) and u64 keys (28K-32K) measured no gain.
+// Store policy of the 8-bit passes (grs_pass.hpp OPT 33554432): nontemporal stores for the
+// 128-B lines wholly inside a tile's digit run, default stores for its head and tail lines.
+#ifndef GRS_RUN_NT_STORES
+#define GRS_RUN_NT_STORES 0
+#endif
+constexpr uint32_t kRunNt = GRS_RUN_NT_STORES ? 33554432u : 0u;
 template <typename K, bool PAIRS>
 struct BigTile {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr bool TWO_ROUNDS = sizeof(K) == 8 && PAIRS;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 22 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
-  static constexpr uint32_t OPT = TWO_ROUNDS ? (1024u | 16u) : (256u | 16u);
+  static constexpr uint32_t OPT = (TWO_ROUNDS ? (1024u | 16u) : (256u | 16u)) | kRunNt;
 };
 // u32 keys at 8-bit digits, large grids: 48K-key tiles of 768 threads x 64 keys reordered in
 // two rounds (LDS takes half the tile; 168 VGPRs at 3 waves per SIMD).  Longer digit runs per
@@ -74,7 +81,7 @@ struct XLTile {
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 40 : 64) : (PAIRS ? 28 : 44);
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr bool TWO_ROUNDS = true;
-  static constexpr uint32_t OPT = 1024u | 16u;
+  static constexpr uint32_t OPT = 1024u | 16u | kRunNt;
 };
 // 4-bit digits (BASELINE C2): 32-bit wave counters (16-bit ones put 64 lanes on 8 words) and
 // the look-back before the reorder (tools/lab2.py at 2^24 keys: 1024 x 32 0.042 ms per pass).
@@ -247,6 +254,12 @@ struct grs_sorter {
   uint32_t* status = nullptr;      // 2 x status_words
   size_t status_words = 0;         // per buffer
   uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
+  // run_sort's histogram + ticket block alternates between ctrl and ctrl2: cb[cb_i] is zero at
+  // the start of the next call (each call's histogram kernel zeroes the other one for the
+  // call after it), so a sort launches no memset; cb_dirty: the partition pass used ctrl
+  uint32_t* ctrl2 = nullptr;       // GRS_CTRL_ERROR words (no error word)
+  int cb_i = 0;
+  bool cb_dirty = false;
   uint32_t* h_err = nullptr;       // pinned host word: the error word read back by checked calls
   size_t scratch_bytes = 0;
   // Profiling ring: the last `ring` calls keep their per-phase hipEvents.
@@ -321,6 +334,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->alt_vals && !s->alt_joint) (void)hipFree(s->alt_vals);
   if (s->status) (void)hipFree(s->status);
   if (s->ctrl) (void)hipFree(s->ctrl);
+  if (s->ctrl2) (void)hipFree(s->ctrl2);
   if (s->h_err) (void)hipHostFree(s->h_err);
   if (s->seg_buf) (void)hipFree(s->seg_buf);
   if (s->seg64) grs_destroy(s->seg64);
@@ -537,7 +551,9 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   }
   alloc(reinterpret_cast<void**>(&s->status), 2 * s->status_words * 4);
   alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
-  if (st == GRS_OK && hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess)
+  alloc(reinterpret_cast<void**>(&s->ctrl2), GRS_CTRL_ERROR * 4);
+  if (st == GRS_OK && (hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess ||
+                       hipMemset(s->ctrl2, 0, GRS_CTRL_ERROR * 4) != hipSuccess))
     st = set_err(GRS_EHIP, "grs_create: hipMemset failed");
   if (st == GRS_OK && hipHostMalloc(reinterpret_cast<void**>(&s->h_err), 4, hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
@@ -668,8 +684,10 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* st0 = s->status;
   uint32_t* st1 = s->status + s->status_words;
-  uint32_t* hist = s->ctrl;
-  uint32_t* tickets = s->ctrl + GRS_CTRL_TICKETS;
+  uint32_t* const cb[2] = {s->ctrl, s->ctrl2};
+  uint32_t* hist = cb[s->cb_i];
+  uint32_t* tickets = hist + GRS_CTRL_TICKETS;
+  uint32_t* hist_next = cb[s->cb_i ^ 1];   // zeroed by this call's histogram kernel
   // one look-back chain over all tiles (no XCD ranges: see kMatchOpt's note)
   const uint32_t range_tiles = std::max<uint32_t>(tiles, 1);
   int ev = 0;
@@ -681,8 +699,10 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
 
   grs_status r;
   if ((r = mark()) != GRS_OK) return r;
-  // zero histograms + tickets (the error word is sticky: only the checks clear it)
-  GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
+  // histograms + tickets are zero (the previous call's histogram kernel cleared them) unless
+  // the partition pass used the block since (the error word is sticky: only the checks clear it)
+  if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
+  s->cb_dirty = false;
   {
     // grs_upfront_hist2: 2 blocks of 512 per CU; a multiple of the resident slots so the
     // grid-stride loop ends evenly, and > n >> kHist2GridShift blocks (16-bit counters)
@@ -695,9 +715,10 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream,
                        src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words), 0u,
-                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE));
+                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE), hist_next);
     GRS_HIP(hipGetLastError());
   }
+  s->cb_i ^= 1;   // the next call's block (zero once this call's histogram kernel has run)
   if ((r = mark()) != GRS_OK) return r;
 
   K* src = keys;
@@ -808,6 +829,7 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* hist = s->ctrl;
   GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
+  s->cb_dirty = true;   // run_sort's block may be this one (sorter.cb_i)
   if (region) {
     // "digit counts" of `region` each: the pass's digit-start scan yields b * region
     GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(hist), static_cast<int>(region),

@@ -205,7 +205,7 @@ template <typename K, int RB, bool FULL>
 __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
     uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words,
-    uint32_t range_keys = 0, uint32_t hist_stride = 0) {
+    uint32_t range_keys = 0, uint32_t hist_stride = 0, uint32_t* __restrict__ clear_ctrl = nullptr) {
   static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
   using HL = Hist2Layout<K>;
   constexpr int MAXQ = HL::MAXQ;
@@ -219,6 +219,12 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     for (uint32_t i = t; i < HL::WORDS / 4; i += HB) z[i] = make_uint4(0, 0, 0, 0);
   }
   for (uint32_t i = blockIdx.x * HB + t; i < clear_words; i += gridDim.x * HB) clear[i] = 0;
+  // the next sort's control block: its range-0 histograms and its tickets
+  if (clear_ctrl != nullptr) {
+    constexpr uint32_t H = GRS_CTRL_HIST_STRIDE, TK = GRS_MAX_PASSES * GRS_XCDS;
+    for (uint32_t i = blockIdx.x * HB + t; i < H + TK; i += gridDim.x * HB)
+      clear_ctrl[i < H ? i : GRS_CTRL_TICKETS + (i - H)] = 0;
+  }
   __syncthreads();
 
   const int supers = (end_bit - begin_bit + 7) / 8;

@@ -26,6 +26,8 @@
 // serial chain, so overlap comes from co-resident tiles.
 #pragma once
 
+#include <type_traits>
+
 #include "grs_kernels.hpp"
 
 namespace grs {
@@ -260,7 +262,8 @@ struct LbWide {
 };
 
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
-          bool IDX = false, int ROUNDS = 1, bool ALIGN = false, bool WIDE = false>
+          bool IDX = false, int ROUNDS = 1, bool ALIGN = false, bool WIDE = false,
+          bool RUNS = false>
 struct V4Smem {
   static constexpr int RADIX = 1 << RB;
   static constexpr int WAVES = BLOCK / GRS_WAVE;
@@ -287,11 +290,14 @@ struct V4Smem {
   // published count and the base without the prefix, handed from the digit threads to the
   // lane group that resolves the digit's prefix
   uint32_t lbv[WIDE ? 3 * RADIX : 1];
+  // run-line store policy (OPT 33554432): global [begin, end) of each digit's run of this tile
+  uint32_t rbeg[RUNS ? RADIX : 1];
+  uint32_t rend[RUNS ? RADIX : 1];
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
                          (OPT & 1024) != 0 ? 2 : 1, (OPT & 65536) != 0 && !DigitF::kIndexed,
-                         (OPT & 2097152) != 0>;
+                         (OPT & 2097152) != 0, (OPT & 33554432) != 0>;
 
 // OPT bits (lab ablations; the library uses OPT = 0):
 //   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
@@ -323,6 +329,11 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //       range of neighbouring tiles on one XCD
 //   131072 speculative tile load (grs_onesweep_v4): tile blockIdx.x is loaded while the ticket
 //       is in flight; a ticket that differs reloads
+//   4194304 tile = blockIdx.x, no ticket (grs_onesweep_v4)
+//   8388608 persistent pass without prefetch (grs_onesweep_v6)
+//   16777216 every store of the pass nontemporal
+//   33554432 nontemporal stores for the 128-B lines wholly inside the tile's digit run, default
+//       stores for the run's head and tail lines
 
 // XCD ranges (OPT 1048576): the tiles form GRS_XCDS contiguous ranges of range_tiles tiles
 // (a multiple of the look-back group), one per XCD, each with its own ticket counter and its
@@ -703,6 +714,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
     }
     sm.base[t] = gstart + roff + prefix - lstart;
+    if constexpr ((OPT & 33554432) != 0) {
+      sm.rbeg[t] = gstart + roff + prefix;
+      sm.rend[t] = gstart + roff + prefix + publish;
+    }
     if constexpr (ALIGN && ROUNDS > 1) {
       // the run holding tile position LTILE (the round boundary) names the first chunk of
       // round 2: the chunk of that position (it is stored partly in each round)
@@ -724,19 +739,42 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // its digit only moves forward through the tile-local digit starts (at most RADIX - 1 steps
   // per tile, over empty digits too).
   uint32_t dcur = 0;
-  auto put = [&](uint32_t dst, K kk, uint32_t i) {
+  // store policy (lab): OPT 16777216 every store nontemporal; OPT 33554432 nontemporal for the
+  // 128-B lines wholly inside this tile's run of the digit, default for the run's head / tail
+  // lines (the ones the neighbouring tiles' runs share)
+  auto stv = [&](auto* p, auto v, bool nt) {
+    if constexpr (sizeof(v) == 8 && !std::is_integral_v<decltype(v)>) {   // uint2 record
+      auto* q = reinterpret_cast<unsigned long long*>(p);
+      const unsigned long long x = (static_cast<unsigned long long>(v.y) << 32) | v.x;
+      if (nt) __builtin_nontemporal_store(x, q);
+      else *q = x;
+    } else {
+      if (nt) __builtin_nontemporal_store(v, p);
+      else *p = v;
+    }
+  };
+  auto put = [&](uint32_t dst, K kk, uint32_t i, bool nt = (OPT & 16777216) != 0) {
     if constexpr ((OPT & 8192) != 0) {
       static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
       const uint2 r = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
       if constexpr ((OPT & 32768) != 0) {   // split records: [n/2, n) in vals_out
-        if (dst >= n / 2) reinterpret_cast<uint2*>(vals_out)[dst - n / 2] = r;
-        else reinterpret_cast<uint2*>(keys_out)[dst] = r;
+        if (dst >= n / 2) stv(reinterpret_cast<uint2*>(vals_out) + (dst - n / 2), r, nt);
+        else stv(reinterpret_cast<uint2*>(keys_out) + dst, r, nt);
       } else {
-        reinterpret_cast<uint2*>(keys_out)[dst] = r;
+        stv(reinterpret_cast<uint2*>(keys_out) + dst, r, nt);
       }
     } else {
-      keys_out[dst] = kk;
-      if constexpr (PAIRS) vals_out[dst] = sm.vals[i];
+      stv(keys_out + dst, kk, nt);
+      if constexpr (PAIRS) stv(vals_out + dst, sm.vals[i], nt);
+    }
+  };
+  auto line_in_run = [&](uint32_t dst, uint32_t d) -> bool {
+    if constexpr ((OPT & 33554432) != 0) {
+      constexpr uint32_t LE = 128 / ((OPT & 8192) != 0 ? 8 : sizeof(K));   // elements per line
+      const uint32_t ls = dst & ~(LE - 1);
+      return ls >= sm.rbeg[d] && ls + LE <= sm.rend[d];
+    } else {
+      return (OPT & 16777216) != 0;
     }
   };
   auto dig_at = [&](uint32_t i, K kk) -> uint32_t {
@@ -823,10 +861,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       for (int k = 0; k < LITEMS; ++k) {
         const uint32_t i = k * BLOCK + t;
         const K kk = sm.keys[i];
-        uint32_t dst = sm.base[dig_at(roff + i, kk)] + roff + i;
+        const uint32_t d = dig_at(roff + i, kk);
+        uint32_t dst = sm.base[d] + roff + i;
         if constexpr ((OPT & 64) != 0) dst = min(dst, n - 1);
         if constexpr ((OPT & 32) != 0) dst = tile_base + roff + i;
-        put(dst, kk, i);
+        put(dst, kk, i, line_in_run(dst, d));
       }
     } else {
 #pragma unroll
@@ -834,8 +873,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         const uint32_t i = k * BLOCK + t;
         if (roff + i < valid) {
           const K kk = sm.keys[i];
-          const uint32_t dst = sm.base[dig_at(roff + i, kk)] + roff + i;
-          put(dst, kk, i);
+          const uint32_t d = dig_at(roff + i, kk);
+          const uint32_t dst = sm.base[d] + roff + i;
+          put(dst, kk, i, line_in_run(dst, d));
         }
       }
     }

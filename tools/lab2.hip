@@ -336,6 +336,9 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 2097424) V(32, 0, 1024, 36, 1, 2097432)
     V(32, 0, 768, 64, 1, 2098192) V(32, 0, 768, 64, 1, 2098200) V(32, 1, 768, 40, 1, 2098192)
     V(64, 0, 1024, 17, 1, 2097424)
+    V(32, 0, 1024, 36, 1, 16777488) V(32, 0, 1024, 36, 1, 33554704) V(32, 0, 768, 64, 1, 16778256)
+    V(32, 0, 768, 64, 1, 33555472) V(32, 1, 768, 40, 1, 16778256) V(32, 1, 768, 40, 1, 33555472)
+    V(64, 0, 768, 44, 1, 16778256) V(64, 0, 768, 44, 1, 33555472)
     V(32, 0, 1024, 36, 1, 4194576) V(32, 0, 1024, 36, 1, 4194584) V(32, 0, 768, 64, 1, 4195344)
     V(32, 0, 768, 64, 1, 4195352) V(32, 1, 768, 40, 1, 4195344) V(64, 0, 768, 44, 1, 4195344)
 #undef V
@@ -386,10 +389,10 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
                uint32_t n, const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2,
                uint32_t* err, void* stream, uint32_t hist_stride, uint32_t range_tiles) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = ((block * 1000L + items) * 10 + minw) * 10000000L + opt;
+  const long code = ((block * 1000L + items) * 10 + minw) * 100000000L + opt;
   switch (code) {
 #define V(B, I, M, O)                                                                          \
-  case ((B * 1000L + I) * 10 + M) * 10000000L + O: {                                           \
+  case ((B * 1000L + I) * 10 + M) * 100000000L + O: {                                          \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
     const uint32_t g = std::min<uint32_t>(tiles, grid);                                        \
     hipLaunchKernelGGL((grs::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
@@ -402,7 +405,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
     V(1024, 32, 1, 2097152) V(1024, 32, 1, 2097160) V(1024, 32, 1, 2097168)
     V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
     V(1024, 32, 1, 524288) V(1024, 32, 1, 524296) V(512, 32, 2, 524288) V(512, 32, 2, 8)
-    V(1024, 32, 1, 64) V(1024, 32, 1, 72)
+    V(1024, 32, 1, 64) V(1024, 32, 1, 72) V(1024, 32, 1, 16777216) V(1024, 32, 1, 33554432)
 #undef V
     default:
       return -1;
