@@ -263,10 +263,10 @@ struct LbWide {
 
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
           bool IDX = false, int ROUNDS = 1, bool ALIGN = false, bool WIDE = false,
-          bool RUNS = false>
+          bool RUNS = false, int VG = 1>
 struct V4Smem {
   static constexpr int RADIX = 1 << RB;
-  static constexpr int WAVES = BLOCK / GRS_WAVE;
+  static constexpr int WAVES = BLOCK / GRS_WAVE * VG;   // counter sets: VG per wave
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr int LTILE = TILE / ROUNDS;   // reordered positions held at once
   // per-wave digit counters -> tile position of (wave, digit); CNT16: 16-bit, two per word
@@ -293,11 +293,15 @@ struct V4Smem {
   // run-line store policy (OPT 33554432): global [begin, end) of each digit's run of this tile
   uint32_t rbeg[RUNS ? RADIX : 1];
   uint32_t rend[RUNS ? RADIX : 1];
+  // G16: tile count and tile-local start of each digit (wave d scans digit d's counter sets)
+  uint32_t tcnt[VG > 1 ? RADIX : 1];
+  uint32_t lst16[VG > 1 ? RADIX : 1];
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
                          (OPT & 1024) != 0 ? 2 : 1, (OPT & 65536) != 0 && !DigitF::kIndexed,
-                         (OPT & 2097152) != 0, (OPT & 33554432) != 0>;
+                         (OPT & 2097152) != 0, (OPT & 33554432) != 0,
+                         (OPT & 67108864) != 0 ? 4 : 1>;
 
 // OPT bits (lab ablations; the library uses OPT = 0):
 //   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
@@ -373,13 +377,19 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
   const uint32_t lane = t & (GRS_WAVE - 1);
   const uint32_t w = t >> 6;
   const uint32_t tile_base = tile * TILE;
-  const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS) + lane;
+  // G16 (OPT 67108864): each 16-lane group of a wave holds its own 16 * ITEMS consecutive keys
+  // (item j of lane l: group offset (l / 16) * 16 * ITEMS + j * 16 + l % 16)
+  constexpr bool G16 = (OPT & 67108864) != 0;
+  constexpr uint32_t JS = G16 ? 16u : static_cast<uint32_t>(GRS_WAVE);   // item stride
+  const uint32_t loff = G16 ? (lane >> 4) * (16u * ITEMS) + (lane & 15u) : lane;
+  const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS) + loff;
   auto ld = [&](const auto* p, uint32_t i) {
     if constexpr ((OPT & 128) != 0) return __builtin_nontemporal_load(p + i);
     else return p[i];
   };
   constexpr bool IN_REC = (OPT & 4096) != 0;
   static_assert(!IN_REC || (PAIRS && sizeof(K) == 4), "records: u32 key + u32 value");
+  static_assert(!IN_REC || !G16, "record loads: wave-striped layout");
   if constexpr (IN_REC) {
     const uint2* rec = reinterpret_cast<const uint2*>(keys_in);
     const uint2* rec_hi = reinterpret_cast<const uint2*>(vals_in);   // split: records [n/2, n)
@@ -397,21 +407,21 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
     }
   } else if (n - tile_base >= TILE) {
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) key[j] = ld(keys_in, wbase + j * GRS_WAVE);
+    for (int j = 0; j < ITEMS; ++j) key[j] = ld(keys_in, wbase + j * JS);
     if constexpr (PAIRS) {
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) val[j] = ld(vals_in, wbase + j * GRS_WAVE);
+      for (int j = 0; j < ITEMS; ++j) val[j] = ld(vals_in, wbase + j * JS);
     }
   } else {
     // the last tile: compare tile-local offsets, never global indices (tile_base + TILE can
     // pass 2^32 when n is near GRS_MAX_N, and a wrapped index would read as in range)
     const uint32_t valid = n - tile_base;
-    const uint32_t lbase = w * (GRS_WAVE * ITEMS) + lane;
+    const uint32_t lbase = w * (GRS_WAVE * ITEMS) + loff;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const bool in = lbase + j * GRS_WAVE < valid;
-      key[j] = in ? keys_in[wbase + j * GRS_WAVE] : static_cast<K>(~static_cast<K>(0));
-      if constexpr (PAIRS) val[j] = in ? vals_in[wbase + j * GRS_WAVE] : 0u;
+      const bool in = lbase + j * JS < valid;
+      key[j] = in ? keys_in[wbase + j * JS] : static_cast<K>(~static_cast<K>(0));
+      if constexpr (PAIRS) val[j] = in ? vals_in[wbase + j * JS] : 0u;
     }
   }
 }
@@ -438,7 +448,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr int RADIX = SM::RADIX;
-  constexpr int WAVES = SM::WAVES;
+  constexpr int WAVES = SM::WAVES;   // counter sets (hardware waves x 4 with G16)
   constexpr int TILE = SM::TILE;
   constexpr int ROUNDS = TILE / SM::LTILE;
   constexpr int LTILE = SM::LTILE;
@@ -511,6 +521,12 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // Indexed digits cost tens of VALU each (the splitter compares), so theirs is computed once
   // and kept in the rank field's top 4 bits for the reorder (ranks < 2^12, digits < 16).
   static_assert(GRS_WAVE * ITEMS < 65536, "16-bit ranks");
+  constexpr bool G16 = (OPT & 67108864) != 0;
+  static_assert(!G16 || (!IDX && !C16 && (OPT & 512) == 0 && (OPT & 4096) == 0 &&
+                         (OPT & 65536) == 0),
+                "16-lane counter sets: plain atomic ranking of loaded keys");
+  // counter set of this lane: its wave's, or (G16) its 16-lane group's
+  const uint32_t vw = G16 ? w * 4 + (lane >> 4) : w;
   static_assert(!IDX || (GRS_WAVE * ITEMS <= 4096 && RADIX <= 16 && ROUNDS == 1 && !C16),
                 "indexed digits ride in the rank field, with 32-bit wave counters");
   uint32_t rank[(ITEMS + 1) / 2];
@@ -546,7 +562,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       const uint32_t sh = (d & 1u) << 4;
       r = (atomicAdd(&sm.cnt[(w * RADIX + d) >> 1], 1u << sh) >> sh) & 0xFFFFu;
     } else {
-      r = atomicAdd(&sm.cnt[w * RADIX + dig_of(j)], 1u);
+      r = atomicAdd(&sm.cnt[vw * RADIX + dig_of(j)], 1u);
     }
     if (j & 1)
       rank[j / 2] |= r << 16;
@@ -567,6 +583,16 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   }
   lds_barrier();  // B1
   V4_STAMP(1);
+  if constexpr (G16) {
+    // wave d, lane v: the start of counter set v within digit d's part of the tile (a DPP
+    // scan per wave, instead of a digit thread walking 64 sets)
+    static_assert(RADIX * GRS_WAVE == BLOCK, "G16: one wave per digit, one lane per counter set");
+    const uint32_t c = sm.cnt[lane * RADIX + w];
+    const uint32_t incl = wave_scan_dpp(c);
+    sm.cnt[lane * RADIX + w] = incl - c;
+    if (lane == GRS_WAVE - 1) sm.tcnt[w] = incl;
+    lds_barrier();
+  }
 
   constexpr bool ALIGN = (OPT & 65536) != 0 && !IDX;
   constexpr bool WIDE = (OPT & 2097152) != 0;
@@ -577,11 +603,15 @@ __device__ __forceinline__ uint32_t onesweep_tile(
                 "wide look-back: >= 2 lanes per digit, no aligned stores / estimated bases");
   uint32_t tile_cnt = 0, publish = 0, gold = 0, lstart = 0, gstart = 0, cstart = 0, cbound = 0;
   if (t < static_cast<uint32_t>(RADIX)) {
+    if constexpr (G16) {
+      tile_cnt = sm.tcnt[t];
+    } else {
 #pragma unroll
-    for (int ww = 0; ww < WAVES; ++ww) {
-      const uint32_t c = cnt_ld(ww * RADIX + t);
-      cnt_st(ww * RADIX + t, tile_cnt);
-      tile_cnt += c;
+      for (int ww = 0; ww < WAVES; ++ww) {
+        const uint32_t c = cnt_ld(ww * RADIX + t);
+        cnt_st(ww * RADIX + t, tile_cnt);
+        tile_cnt += c;
+      }
     }
     publish = (t == dmask) ? tile_cnt - pad : tile_cnt;  // padding is ranked, never counted
     st_status(status + static_cast<size_t>(tile) * RADIX + t, publish + 1u);
@@ -606,6 +636,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     lstart = li - tile_cnt;
     gstart = gi - gh;
     cstart = ci - cbound;
+    if constexpr (G16) {   // one digit wave (RADIX <= 64): lstart is final here
+      if (t < static_cast<uint32_t>(RADIX)) sm.lst16[t] = lstart;
+    }
   }
   lds_barrier();  // B2
   V4_STAMP(2);
@@ -625,8 +658,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       sm.lst[t] = lstart;
       sm.rlen[t] = publish;
     }
+    if constexpr (!G16) {
 #pragma unroll
-    for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
+      for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
+    }
     if constexpr (IDX) {
       sm.lstart[t] = lstart;
       if (t == static_cast<uint32_t>(RADIX - 1)) sm.lstart[RADIX] = TILE;
@@ -642,6 +677,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   if constexpr (WIDE && (OPT & 16) == 0 && !PF) {
     if (wd < static_cast<uint32_t>(RADIX)) lbw.issue(status, gacc, ginc, tile, wd, wj, g0);
   }
+  if constexpr (G16) sm.cnt[lane * RADIX + w] += sm.lst16[w];   // the fold, one counter a thread
   lds_barrier();  // B3
   V4_STAMP(3);
 
@@ -660,7 +696,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     } else {
       d = dig_of(j);
     }
-    const uint32_t pos = cnt_ld(w * RADIX + d) + r;
+    const uint32_t pos = cnt_ld(vw * RADIX + d) + r;
     if (ROUNDS == 1 || pos < static_cast<uint32_t>(LTILE)) {
       sm.keys[pos] = key[j];
       if constexpr (PAIRS) sm.vals[pos] = val[j];

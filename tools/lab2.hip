@@ -336,6 +336,7 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 2097424) V(32, 0, 1024, 36, 1, 2097432)
     V(32, 0, 768, 64, 1, 2098192) V(32, 0, 768, 64, 1, 2098200) V(32, 1, 768, 40, 1, 2098192)
     V(64, 0, 1024, 17, 1, 2097424)
+
     V(32, 0, 1024, 36, 1, 16777488) V(32, 0, 1024, 36, 1, 33554704) V(32, 0, 768, 64, 1, 16778256)
     V(32, 0, 768, 64, 1, 33555472) V(32, 1, 768, 40, 1, 16778256) V(32, 1, 768, 40, 1, 33555472)
     V(64, 0, 768, 44, 1, 16778256) V(64, 0, 768, 44, 1, 33555472)
@@ -406,6 +407,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
     V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
     V(1024, 32, 1, 524288) V(1024, 32, 1, 524296) V(512, 32, 2, 524288) V(512, 32, 2, 8)
     V(1024, 32, 1, 64) V(1024, 32, 1, 72) V(1024, 32, 1, 16777216) V(1024, 32, 1, 33554432)
+    V(1024, 32, 1, 67108864) V(1024, 32, 1, 67108872) V(1024, 32, 1, 67108880)
 #undef V
     default:
       return -1;
