@@ -137,7 +137,12 @@ const char* grs_pass_kernel(const grs_sorter* s, size_t n);
 
 /* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a
  * payload, d_vals[0..n) is permuted with its keys (d_vals may be NULL otherwise).
- * Replaces ParallelSort::Sort() (ParallelSort.cpp:168-422). */
+ * Replaces ParallelSort::Sort() (ParallelSort.cpp:168-422).
+ * Asynchronous on `stream`: until the call's work has completed, the contents of d_keys /
+ * d_vals are unspecified (between passes they can hold 8-byte (key, value) records).  Keys
+ * and payload must be naturally aligned (GRS_EINVAL otherwise); the passes that move 8-byte
+ * records on the caller's two u32 arrays run only when both are 8-byte aligned.  Calls on one
+ * sorter must be ordered (one stream, or synchronised): they share its scratch. */
 grs_status grs_sort(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, void* stream);
 
 /* As grs_sort, restricted to key bits [begin_bit, end_bit) (the reference's fixed
