@@ -708,6 +708,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     // grid-stride loop ends evenly, and > n >> kHist2GridShift blocks (16-bit counters)
     const int slots = 2 * s->cus;
     const int need = static_cast<int>(n >> grs::kHist2GridShift<K>) + 1;
+    // (one block per CU up to 2^25 keys: two measured slower at C2, 24.8 vs 21.5 us)
     int grid = n <= (1u << 25) ? s->cus : slots;
     if (grid < need) grid = (need + slots - 1) / slots * slots;
     const bool full = begin_bit == 0 && end_bit == static_cast<int>(8 * sizeof(K));
