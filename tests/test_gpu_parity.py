@@ -462,6 +462,46 @@ def test_repeated_sorts_reuse_scratch(gpu):
         assert np.array_equal(gv, perm)
 
 
+def test_control_blocks_alternate_across_calls(gpu):
+    """A sort launches no memset: its histogram kernel zeroes the OTHER of the sorter's two
+    control blocks for the next call, and a partition (which clears and dirties the first
+    block itself) makes the next sort clear it again.  Interleave sorts of different sizes,
+    digit widths and bit ranges with partitions on one sorter, on one stream, without
+    synchronising in between, and check every result."""
+    import gpuradixsort_amd as grs
+
+    rng = np.random.default_rng(12)
+    s = grs.RadixSorter(300_000, key_bits=32, pairs=True, radix_bits=8)
+    s4 = grs.RadixSorter(300_000, key_bits=32, pairs=True, radix_bits=4)
+    jobs = []
+    for step, n in enumerate((300_000, 1, 65_537, 0, 123_457, 300_000, 4_096)):
+        keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        k = to_dev(keys, gpu)
+        v = to_dev(np.arange(n, dtype=np.uint32), gpu)
+        if step % 3 == 1:     # a bit-range sort (bits [8, 24))
+            s.sort(k, v, begin_bit=8, end_bit=24)
+            perm = np.argsort((keys >> 8) & 0xFFFF, kind="stable")
+        elif step % 3 == 2:   # a partition, then a sort on the same sorter
+            ko, vo = torch.empty_like(k), torch.empty_like(v)
+            sp = np.sort(rng.integers(0, 2**32, 5, dtype=np.uint64).astype(np.uint32))
+            cnt = torch.zeros(6, dtype=torch.uint32, device=gpu)
+            s.partition(k, ko, sp, cnt, v, vo)
+            bucket = np.searchsorted(sp, keys, side="right")
+            jobs.append(("partition", ko, vo, keys, np.argsort(bucket, kind="stable")))
+            s.sort(k, v)
+            perm = np.argsort(keys, kind="stable")
+        else:
+            (s4 if step % 2 else s).sort(k, v)
+            perm = np.argsort(keys, kind="stable")
+        jobs.append(("sort", k, v, keys, perm))
+    torch.cuda.synchronize()
+    s.check_error()
+    s4.check_error()
+    for what, k, v, keys, perm in jobs:
+        assert np.array_equal(k.cpu().numpy(), keys[perm]), what
+        assert np.array_equal(v.cpu().numpy(), perm), what
+
+
 @pytest.mark.parametrize("kb", [32, 64])
 @pytest.mark.parametrize("pairs", [False, True])
 def test_partition_is_stable_range_split(gpu, kb, pairs):
