@@ -338,6 +338,8 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //   16777216 every store of the pass nontemporal
 //   33554432 nontemporal stores for the 128-B lines wholly inside the tile's digit run, default
 //       stores for the run's head and tail lines
+//   67108864 16-lane counter sets (4-bit digits): each 16-lane group ranks its own 16 * ITEMS
+//       consecutive keys
 
 // XCD ranges (OPT 1048576): the tiles form GRS_XCDS contiguous ranges of range_tiles tiles
 // (a multiple of the look-back group), one per XCD, each with its own ticket counter and its
