@@ -340,6 +340,8 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //       stores for the run's head and tail lines
 //   67108864 16-lane counter sets (4-bit digits): each 16-lane group ranks its own 16 * ITEMS
 //       consecutive keys
+//   268435456 with 8388608: the tile's stores drained (vmcnt(0)) before the next tile's loads
+//   536870912 the group-accumulator add issued at the look-back's finish (not at B1)
 
 // XCD ranges (OPT 1048576): the tiles form GRS_XCDS contiguous ranges of range_tiles tiles
 // (a multiple of the look-back group), one per XCD, each with its own ticket counter and its
@@ -617,8 +619,12 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     }
     publish = (t == dmask) ? tile_cnt - pad : tile_cnt;  // padding is ranked, never counted
     st_status(status + static_cast<size_t>(tile) * RADIX + t, publish + 1u);
-    gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
-                                  (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // OPT 536870912: the group-accumulator add is issued just before the look-back's finish
+    // (its return is used only there): a value returned here stays live across the reorder,
+    // and at 1024 threads (128 VGPRs) it gets spilled, i.e. waited for, right here
+    if constexpr ((OPT & 536870912) == 0)
+      gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
+                                    (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (w < static_cast<uint32_t>(DW)) {
     const uint32_t li = wave_scan_dpp(tile_cnt);
@@ -749,6 +755,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     if constexpr ((OPT & 64) != 0) {
       prefix = static_cast<uint32_t>((static_cast<uint64_t>(gh) * tile) / tiles) - roff;
     } else {
+      if constexpr ((OPT & 536870912) != 0)
+        gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
+                                      (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
     }
     sm.base[t] = gstart + roff + prefix - lstart;
@@ -1045,6 +1054,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     lds_barrier();
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
     if constexpr ((OPT & 8388608) != 0) {
+      // OPT 268435456: the tile's stores drained before the next tile's loads go out
+      if constexpr ((OPT & 268435456) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);
     }
     lds_barrier();
