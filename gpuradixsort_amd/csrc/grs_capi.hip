@@ -60,13 +60,23 @@ grs_status set_err(grs_status s, const std::string& msg) {
 #define GRS_RUN_NT_STORES 0
 #endif
 constexpr uint32_t kRunNt = GRS_RUN_NT_STORES ? 33554432u : 0u;
+// Group-accumulator add without a return value, read back by the look-back (grs_pass.hpp OPT
+// 1073741824): at 1024 threads the returned value is spilled, so the digit waves wait for the
+// atomic before B2 (2.7K -> 1.1K cycles there; a lone pass in tools/lab2.py: 2^28 big tiles
+// 0.517 -> 0.505 ms, XL 1.901 -> 1.892 at 2^30; profiles/r03/lab/r3zd_acc_readback_last.txt).
+// Inside the sort it measured equal (profiles/r03/s2/ab_acc_readback.txt), so the returning
+// add, whose last adder always publishes the group's inclusive, stays the default.
+#ifndef GRS_ACC_READBACK
+#define GRS_ACC_READBACK 0
+#endif
+constexpr uint32_t kAccRb = GRS_ACC_READBACK ? 1073741824u : 0u;
 template <typename K, bool PAIRS>
 struct BigTile {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr bool TWO_ROUNDS = sizeof(K) == 8 && PAIRS;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 22 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
-  static constexpr uint32_t OPT = (TWO_ROUNDS ? (1024u | 16u) : (256u | 16u)) | kRunNt;
+  static constexpr uint32_t OPT = (TWO_ROUNDS ? (1024u | 16u) : (256u | 16u)) | kRunNt | kAccRb;
 };
 // u32 keys at 8-bit digits, large grids: 48K-key tiles of 768 threads x 64 keys reordered in
 // two rounds (LDS takes half the tile; 168 VGPRs at 3 waves per SIMD).  Longer digit runs per
@@ -81,7 +91,7 @@ struct XLTile {
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 40 : 64) : (PAIRS ? 28 : 44);
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr bool TWO_ROUNDS = true;
-  static constexpr uint32_t OPT = 1024u | 16u | kRunNt;
+  static constexpr uint32_t OPT = 1024u | 16u | kRunNt | kAccRb;
 };
 // 4-bit digits (BASELINE C2): 32-bit wave counters (16-bit ones put 64 lanes on 8 words) and
 // the look-back before the reorder (tools/lab2.py at 2^24 keys: 1024 x 32 0.042 ms per pass).

@@ -58,13 +58,14 @@ __host__ __device__ constexpr size_t lb3_status_words(size_t tiles, size_t radix
 // after it).  issue() sends the first round of loads, finish() consumes them.
 // GW: groups polled per round.  The two-round (XL) tiles use 4: the window's registers are
 // live across the reorder there, beside the tile's keys and positions.
-template <int RADIX, int GW = GRS_LB_GWIN>
+template <int RADIX, int GW = GRS_LB_GWIN, bool OWNACC = false>
 struct Lb3 {
   static constexpr int G = GRS_LB_GROUP;
   uint32_t tw[G - 1];
   uint32_t gi[GW], ga[GW];
   int32_t ph;
   int32_t g0;   // first group of this tile's chain (XCD ranges: the range's first group)
+  uint32_t gown;   // OWNACC: this tile's group accumulator, read with the first round
 
   __device__ __forceinline__ void load_groups(const uint32_t* gacc, const uint32_t* ginc,
                                               uint32_t d) {
@@ -85,8 +86,11 @@ struct Lb3 {
       tw[k] = first + k < tile ? ld_status(status + static_cast<size_t>(first + k) * RADIX + d) : 1u;
     ph = static_cast<int32_t>(tile / G) - 1;
     load_groups(gacc, ginc, d);
+    if constexpr (OWNACC) gown = ld_status(gacc + static_cast<size_t>(tile / G) * RADIX + d);
   }
   // gold: the value this tile's add to its group accumulator returned; publish: its count
+  // (OWNACC: the add returned nothing; the group's last tile publishes the inclusive when the
+  // accumulator it read back is complete)
   __device__ __forceinline__ uint32_t finish(const uint32_t* status, const uint32_t* gacc,
                                              uint32_t* ginc, uint32_t tile, uint32_t tiles,
                                              uint32_t d, uint32_t gold, uint32_t publish,
@@ -139,8 +143,15 @@ struct Lb3 {
       load_groups(gacc, ginc, d);
     }
     const uint32_t in_group = min(static_cast<uint32_t>(G), tiles - g * G);
-    if ((gold >> 24) == in_group - 1u)  // this tile's add completed the group
+    if constexpr (OWNACC) {
+      // only the group's last tile publishes (one writer per line); if it read the accumulator
+      // before an earlier tile's add landed, no inclusive appears and the successors sum the
+      // complete accumulator instead (a longer walk, the same prefix)
+      if (tile - g * G == in_group - 1u && (gown >> 24) == in_group)
+        st_status(ginc + static_cast<size_t>(g) * RADIX + d, gp + (gown & 0xFFFFFFu) + 1u);
+    } else if ((gold >> 24) == in_group - 1u) {  // this tile's add completed the group
       st_status(ginc + static_cast<size_t>(g) * RADIX + d, gp + (gold & 0xFFFFFFu) + publish + 1u);
+    }
     return gp + own;
   }
 };
@@ -342,6 +353,8 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //       consecutive keys
 //   268435456 with 8388608: the tile's stores drained (vmcnt(0)) before the next tile's loads
 //   536870912 the group-accumulator add issued at the look-back's finish (not at B1)
+//   1073741824 the group-accumulator add at B1 returns nothing; the look-back reads the
+//       accumulator back and the group's last tile publishes the inclusive if it is complete
 
 // XCD ranges (OPT 1048576): the tiles form GRS_XCDS contiguous ranges of range_tiles tiles
 // (a multiple of the look-back group), one per XCD, each with its own ticket counter and its
@@ -622,7 +635,12 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     // OPT 536870912: the group-accumulator add is issued just before the look-back's finish
     // (its return is used only there): a value returned here stays live across the reorder,
     // and at 1024 threads (128 VGPRs) it gets spilled, i.e. waited for, right here
-    if constexpr ((OPT & 536870912) == 0)
+    // OPT 1073741824: the add returns nothing (no value to keep live, or to spill and so wait
+    // for, across the reorder); the look-back reads the group's accumulator back instead
+    if constexpr ((OPT & 1073741824) != 0)
+      __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
+                             (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr ((OPT & 536870912) == 0)
       gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
                                     (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -651,7 +669,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   lds_barrier();  // B2
   V4_STAMP(2);
 
-  Lb3<RADIX, (ROUNDS > 1 ? GRS_LB_GWIN_XL : GRS_LB_GWIN)> lb;
+  static_assert((OPT & 1073741824) == 0 || ((OPT & 2097152) == 0 && (OPT & 536870912) == 0),
+                "accumulator read-back: the one-thread-per-digit look-back, add at B1");
+  Lb3<RADIX, (ROUNDS > 1 ? GRS_LB_GWIN_XL : GRS_LB_GWIN), (OPT & 1073741824) != 0> lb;
   LbWide<RADIX, WIDE ? LW : 2> lbw;
   const uint32_t wd = t / LW, wj = t & (LW - 1);   // wide look-back: digit and lane in its group
   if (t < static_cast<uint32_t>(RADIX)) {

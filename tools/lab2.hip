@@ -337,8 +337,8 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 768, 64, 1, 2098192) V(32, 0, 768, 64, 1, 2098200) V(32, 1, 768, 40, 1, 2098192)
     V(64, 0, 1024, 17, 1, 2097424)
 
-    V(32, 0, 1024, 36, 1, 536871184) V(32, 0, 1024, 36, 1, 536871192) V(32, 0, 768, 64, 1, 536871952)
-    V(32, 0, 768, 64, 1, 536871960) V(32, 1, 768, 40, 1, 536871952) V(64, 0, 768, 44, 1, 536871952)
+    V(32, 0, 1024, 36, 1, 1073742096) V(32, 0, 1024, 36, 1, 1073742104) V(32, 0, 768, 64, 1, 1073742864)
+    V(32, 0, 768, 64, 1, 1073742872) V(32, 1, 768, 40, 1, 1073742864) V(64, 0, 768, 44, 1, 1073742864)
     V(32, 0, 512, 36, 2, 272) V(32, 0, 512, 32, 2, 272) V(32, 0, 512, 48, 2, 1040)
     V(32, 0, 512, 56, 2, 1040) V(32, 0, 512, 64, 2, 1040) V(32, 0, 512, 36, 2, 280)
     V(32, 0, 1024, 36, 1, 16777488) V(32, 0, 1024, 36, 1, 33554704) V(32, 0, 768, 64, 1, 16778256)
