@@ -192,7 +192,8 @@ def test_c4_presorted_eight_ranks_on_one_gpu(gpu):
     C-ABI steps: each 2^27-key shard sorted, sampled, split by the tie-breaking splitters and
     encoded; each receiver decodes and merges the eight encoded runs it gets.  The ranks'
     outputs concatenated must hash to the committed digest; the encoding must be about a byte
-    per key; the receivers must be balanced."""
+    per key; the receivers must be balanced.  Each receiver's runs are also merged by the
+    one-pass k-way merge (option "merge"), which must give the same keys."""
     import gpuradixsort_amd as grs
     from gpuradixsort_amd import _lib
     from gpuradixsort_amd.sharded import shard_decode_merge, shard_encode, shard_sample
@@ -223,6 +224,7 @@ def test_c4_presorted_eight_ranks_on_one_gpu(gpu):
     h = hashlib.sha256()
     sizes = []
     out = torch.empty(n + n // 4, dtype=torch.uint32, device=gpu)
+    out_k = torch.empty_like(out)
     for r in range(G):
         parts, offs, lens, off = [], [], [], 0
         for p in range(G):
@@ -233,7 +235,11 @@ def test_c4_presorted_eight_ranks_on_one_gpu(gpu):
             off += w
         recv = torch.cat(parts)
         m = shard_decode_merge(s, recv, offs, lens, out)
+        s.set_option("merge", "kway")
+        assert shard_decode_merge(s, recv, offs, lens, out_k) == m
+        s.set_option("merge", "rounds")
         s.check_error()
+        assert torch.equal(out[:m], out_k[:m]), f"k-way merge differs at receiver {r}"
         sizes.append(m)
         _host_sha_update(h, out[:m])
         del recv
