@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child runs")
     ap.add_argument("--pmc-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the second leg (north star: 2^28 u32 keys) after the c4 headline")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--sharded", action="store_true",
                     help="N = 1 through grs_sort_sharded's multi-rank code path (option "
@@ -167,7 +169,7 @@ def pmc_probe(a, options):
     s.check_error()
 
 
-def measure_traffic(a, options, n_local):
+def measure_traffic(a, config, options, n_local):
     """HBM bytes per launch of the pass from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM):
     one counter per rocprofv3 run (FETCH_SIZE, then WRITE_SIZE) over a child --pmc-probe run;
     each counter is corrected by known bytes / counter bytes of the calibration copy, which
@@ -191,7 +193,7 @@ def measure_traffic(a, options, n_local):
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             out = os.path.join(d, ctr)
             cmd = [rp, "--pmc", ctr, "-d", out, "-o", "p", "--output-format", "csv", "--",
-                   sys.executable, os.path.abspath(__file__), "--pmc-probe", "--config", a.config,
+                   sys.executable, os.path.abspath(__file__), "--pmc-probe", "--config", config,
                    "--n", str(n_local)] + extra
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
                                  start_new_session=True)
@@ -227,46 +229,23 @@ def measure_traffic(a, options, n_local):
                       "calibration of known bytes"}, None
 
 
-def main():
-    a = parse()
-    if a.pmc_probe:
-        opts = dict(o.split("=", 1) for o in a.opt)
-        pmc_probe(a, {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in opts.items()})
-        return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and not (world == 1 and a.gpus == 1):
-        if world == 1:
-            raise SystemExit("--gpus N > 1 must be launched with torchrun (one rank per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    sharded = world > 1 or a.sharded
-    if sharded and world == 1:
-        import socket
-
-        with socket.socket() as so:
-            so.bind(("127.0.0.1", 0))
-            port = so.getsockname()[1]
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
-
+def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
+    """One workload of CONFIGS, timed per the driver contract; returns rank 0's JSON dict."""
     import gpuradixsort_amd as grs
 
-    cid, n_cfg, kb, pairs, rb, desc = CONFIGS[a.config]
+    cid, n_cfg, kb, pairs, rb, desc = CONFIGS[config]
     options = dict(o.split("=", 1) for o in a.opt)
     options = {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in options.items()}
     if sharded and world == 1:
         options.setdefault("sharded_path", "general")
-    if a.n:
+    if a.n and config == a.config:
         n_cfg = a.n
-    strong = a.config == "c4"
+    strong = config == "c4"
     n_local = n_cfg // world if strong else n_cfg
     seed = (0x6A09E667F3BCC908 + cid) & ((1 << 64) - 1)
     kdt = torch.uint32 if kb == 32 else torch.uint64
     step_bytes = n_local * (kb // 8 + (4 if pairs else 0))
-    pool = max(1, min(a.warmup + a.steps, int(a.pool_gib * 2**30 // step_bytes)))
+    pool = max(1, min(warmup + steps, int(a.pool_gib * 2**30 // step_bytes)))
 
     # distinct unsorted inputs, one per step (step s uses global indices offset by s * N_total)
     n_total = n_local * world
@@ -309,11 +288,11 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
-    for i in range(a.warmup):
+    for i in range(warmup):
         step(i)
     barrier()
     t0 = time.perf_counter()
-    for i in range(a.warmup, a.warmup + a.steps):
+    for i in range(warmup, warmup + steps):
         step(i)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -325,16 +304,16 @@ def main():
     # look-back timeouts of the timed steps surface here (error word; raises GrsError)
     (sorter.sorter if sharded else sorter).check_error()
     # correctness of the last timed step (cheap property: sortedness on device)
-    last = (a.warmup + a.steps - 1) % pool
+    last = (warmup + steps - 1) % pool
     inversions = sorter.count_inversions() if sharded else grs.count_inversions(keys_pool[last])
 
     # per-phase GPU times: the same steps again, untimed, with libgrs's per-phase hipEvent ring
     # on (events between the launches cost 2-5 us each, 13 % of a C2 sort; the timed steps above
     # run without them, as a caller's sorts do)
-    nprof = min(a.steps, pool)
+    nprof = min(steps, pool)
     sorter.set_profiling(nprof)
     barrier()
-    for i in range(a.warmup, a.warmup + nprof):
+    for i in range(warmup, warmup + nprof):
         # the timed steps sorted these buffers: fresh unsorted inputs of the same workload
         grs.fill_splitmix(keys_pool[i % pool], seed, first_index=i * n_total + rank * n_local)
         if pairs:
@@ -358,6 +337,9 @@ def main():
     kernel_name = (sorter.sorter if sharded else sorter).pass_kernel_for(n_sorted_local)
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
+    passes = tims[0]["passes"]
+    del keys_pool, vals_pool, sorter
+    torch.cuda.empty_cache()
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -366,58 +348,100 @@ def main():
     # PMC bytes per launch: rocprofv3 child runs of this workload (after the timed region)
     traffic, traffic_info = None, None
     if rank == 0 and world == 1 and not sharded and not a.no_traffic:
-        traffic_info, why = measure_traffic(a, options, n_local)
+        traffic_info, why = measure_traffic(a, config, options, n_local)
         if traffic_info:
             traffic = traffic_info["bytes_per_launch"]
         else:
             traffic_info = {"error": why}
     elif a.traffic_json and os.path.exists(a.traffic_json):
         rec = json.load(open(a.traffic_json))
-        if rec.get("n") == n_sorted_local and rec.get("config") == a.config:
+        if rec.get("n") == n_sorted_local and rec.get("config") == config:
             traffic = rec.get("hbm_bytes_per_launch")
 
-    sort_alg = n_local * 2 * tims[0]["passes"] * (kb // 8 + (4 if pairs else 0))
-    if rank == 0:
-        value = n_total * a.steps / elapsed / 1e9
-        out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Gkeys/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32" if kb == 32 else "u64",
-            "data": "synthetic: splitmix64(seed ^ global_index) uniform keys, a distinct unsorted "
-                    "buffer per step resident in HBM" + ("; payload = global index" if pairs else ""),
-            "config": {"workload": desc, "keys_per_gpu": n_local, "total_keys": n_total,
-                       "key_bits": kb, "payload": "u32" if pairs else None, "radix_bits": rb,
-                       "passes": tims[0]["passes"], "parallelism": f"range-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "kernel": kernel_name,
-                         "kernel_mean_ms": round(mean_pass_ms, 5),
-                         "alg_bytes_per_launch": alg_bytes,
-                         "traffic_over_alg": round(traffic / alg_bytes, 4) if traffic else None},
-            # whole-sort view of SURVEY.md §8d: B_alg = N x 2 x passes x (key + value bytes)
-            # over the whole step (histogram and exchange included)
-            "sort_roofline": {"achieved": round(sort_alg / (elapsed / a.steps) / 1e9, 1),
-                              "frac": round(sort_alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBPS, 4),
-                              "alg_bytes_per_step": sort_alg, "unit": "GB/s"},
-            "cpu_baseline": cpu,
-            "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
-                          "sort_total_gpu": round(sort_ms, 5)},
-            "check": {"inversions_last_step": inversions},
-        }
-        if options:
-            out["config"]["options"] = options
-        if traffic_info:
-            out["traffic_pmc"] = traffic_info
-        if sharded:
-            out["phases_ms"]["recv_keys_rank0"] = sorter.last_n_out
-            out["config"]["exchange"] = exchange
-            xms = max(xt["exchange_ms"], 1e-6)
-            out["exchange_rank0"] = {
-                "before_ms": round(xt["before_ms"], 4), "exchange_ms": round(xt["exchange_ms"], 4),
-                "after_ms": round(xt["after_ms"], 4), "bytes_sent": xt["bytes_sent"],
-                "bytes_received": xt["bytes_received"],
-                "xgmi_GBps_sent": round(xt["bytes_sent"] / xms / 1e6, 1)}
+    sort_alg = n_local * 2 * passes * (kb // 8 + (4 if pairs else 0))
+    if rank != 0:
+        return None
+    value = n_total * steps / elapsed / 1e9
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Gkeys/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32" if kb == 32 else "u64",
+        "data": "synthetic: splitmix64(seed ^ global_index) uniform keys, a distinct unsorted "
+                "buffer per step resident in HBM" + ("; payload = global index" if pairs else ""),
+        "config": {"workload": desc, "keys_per_gpu": n_local, "total_keys": n_total,
+                   "key_bits": kb, "payload": "u32" if pairs else None, "radix_bits": rb,
+                   "passes": passes, "parallelism": f"range-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic, "kernel": kernel_name,
+                     "kernel_mean_ms": round(mean_pass_ms, 5),
+                     "alg_bytes_per_launch": alg_bytes,
+                     "traffic_over_alg": round(traffic / alg_bytes, 4) if traffic else None},
+        # whole-sort view of SURVEY.md §8d: B_alg = N x 2 x passes x (key + value bytes)
+        # over the whole step (histogram and exchange included)
+        "sort_roofline": {"achieved": round(sort_alg / (elapsed / steps) / 1e9, 1),
+                          "frac": round(sort_alg / (elapsed / steps) / 1e9 / HBM_PEAK_GBPS, 4),
+                          "alg_bytes_per_step": sort_alg, "unit": "GB/s"},
+        "cpu_baseline": cpu,
+        "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
+                      "sort_total_gpu": round(sort_ms, 5)},
+        "check": {"inversions_last_step": inversions},
+    }
+    if options:
+        out["config"]["options"] = options
+    if traffic_info:
+        out["traffic_pmc"] = traffic_info
+    if sharded:
+        out["phases_ms"]["recv_keys_rank0"] = n_sorted_local
+        out["config"]["exchange"] = exchange
+        xms = max(xt["exchange_ms"], 1e-6)
+        out["exchange_rank0"] = {
+            "before_ms": round(xt["before_ms"], 4), "exchange_ms": round(xt["exchange_ms"], 4),
+            "after_ms": round(xt["after_ms"], 4), "bytes_sent": xt["bytes_sent"],
+            "bytes_received": xt["bytes_received"],
+            "xgmi_GBps_sent": round(xt["bytes_sent"] / xms / 1e6, 1)}
+    return out
+
+
+def main():
+    a = parse()
+    if a.pmc_probe:
+        opts = dict(o.split("=", 1) for o in a.opt)
+        pmc_probe(a, {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in opts.items()})
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and not (world == 1 and a.gpus == 1):
+        if world == 1:
+            raise SystemExit("--gpus N > 1 must be launched with torchrun (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    sharded = world > 1 or a.sharded
+    if sharded and world == 1:
+        import socket
+
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+
+    out = run_config(a, a.config, world, rank, local, dev, sharded, a.steps, a.warmup)
+    # the north star's own 1-GPU target (BASELINE.json: >= 60 % of the HBM roofline on 256 M
+    # uniform uint32 keys) as a second leg of the same driver-timed run, after the headline
+    if world == 1 and not sharded and a.config == "c4" and not a.n and not a.no_north_star:
+        ns = run_config(a, "ns", world, rank, local, dev, sharded, a.steps, a.warmup)
+        if out is not None and ns is not None:
+            out["north_star"] = {k: ns[k] for k in ("value", "unit", "ms_per_step", "steps",
+                                                    "warmup", "roofline", "sort_roofline",
+                                                    "phases_ms", "check")}
+            out["north_star"]["config"] = ns["config"]
+            if "traffic_pmc" in ns:
+                out["north_star"]["traffic_pmc"] = ns["traffic_pmc"]
+    if out is not None:
         print(json.dumps(out), flush=True)
     if sharded:
         dist.destroy_process_group()

@@ -60,9 +60,10 @@ OPTIONS = {
     "records": (4, {"arrays": 0, "scratch": 1, "split": 2}),
     "rank": (5, {"probe": 0, "match": 1}),
     "sharded_path": (6, {"auto": 0, "general": 1}),
-    "sharded_send": (7, {"regions": 0, "contig": 1}),
+    "sharded_send": (7, {"regions": 0, "contig": 1, "shrunk": 2}),
     "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
     "merge": (9, {"rounds": 0, "kway": 1}),
+    "fault_tile": (10, {"off": -1}),   # test hook: tile v of every pass never publishes
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares
@@ -92,6 +93,7 @@ SIGNATURES = [
     ("grs_sort_sharded", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                  c_size_t, POINTER(c_size_t), c_void_p, c_void_p]),
     ("grs_sharded_last_timing", c_int, [c_void_p, POINTER(grs_sharded_timing)]),
+    ("grs_sharded_redo_count", c_int, [c_void_p, POINTER(c_uint64)]),
     ("grs_rccl_unique_id", c_int, [c_void_p]),
     ("grs_rccl_comm_init", c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int]),
     ("grs_rccl_comm_destroy", None, [c_void_p]),

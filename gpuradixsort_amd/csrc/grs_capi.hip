@@ -54,29 +54,13 @@ grs_status set_err(grs_status s, const std::string& msg) {
 // in VGPRs, LDS takes half the tile at a time; 32-bit wave counters): 22K-pair tiles, same
 // process (tools/lab2.py, 2^28 pairs, ms per pass) 1.37 vs 1.48 and 1.45 vs 1.72 on two boxes
 // against one-round 11K tiles.  u32 pairs (26K tiles) and u64 keys (28K-32K) measured no gain.
-// Store policy of the 8-bit passes (grs_pass.hpp OPT 33554432): nontemporal stores for the
-// 128-B lines wholly inside a tile's digit run, default stores for its head and tail lines.
-#ifndef GRS_RUN_NT_STORES
-#define GRS_RUN_NT_STORES 0
-#endif
-constexpr uint32_t kRunNt = GRS_RUN_NT_STORES ? 33554432u : 0u;
-// Group-accumulator add without a return value, read back by the look-back (grs_pass.hpp OPT
-// 1073741824): at 1024 threads the returned value is spilled, so the digit waves wait for the
-// atomic before B2 (2.7K -> 1.1K cycles there; a lone pass in tools/lab2.py: 2^28 big tiles
-// 0.517 -> 0.505 ms, XL 1.901 -> 1.892 at 2^30; profiles/r03/lab/r3zd_acc_readback_last.txt).
-// Inside the sort it measured equal (profiles/r03/s2/ab_acc_readback.txt), so the returning
-// add, whose last adder always publishes the group's inclusive, stays the default.
-#ifndef GRS_ACC_READBACK
-#define GRS_ACC_READBACK 0
-#endif
-constexpr uint32_t kAccRb = GRS_ACC_READBACK ? 1073741824u : 0u;
 template <typename K, bool PAIRS>
 struct BigTile {
   static constexpr int BLOCK = 1024, MINW = 1;
   static constexpr bool TWO_ROUNDS = sizeof(K) == 8 && PAIRS;
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 22 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
-  static constexpr uint32_t OPT = (TWO_ROUNDS ? (1024u | 16u) : (256u | 16u)) | kRunNt | kAccRb;
+  static constexpr uint32_t OPT = TWO_ROUNDS ? (1024u | 16u) : (256u | 16u);
 };
 // u32 keys at 8-bit digits, large grids: 48K-key tiles of 768 threads x 64 keys reordered in
 // two rounds (LDS takes half the tile; 168 VGPRs at 3 waves per SIMD).  Longer digit runs per
@@ -91,7 +75,7 @@ struct XLTile {
   static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 40 : 64) : (PAIRS ? 28 : 44);
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr bool TWO_ROUNDS = true;
-  static constexpr uint32_t OPT = 1024u | 16u | kRunNt | kAccRb;
+  static constexpr uint32_t OPT = 1024u | 16u;
 };
 // 4-bit digits (BASELINE C2): 32-bit wave counters (16-bit ones put 64 lanes on 8 words) and
 // the look-back before the reorder (tools/lab2.py at 2^24 keys: 1024 x 32 0.042 ms per pass).
@@ -135,9 +119,9 @@ struct PartTile {
 constexpr uint32_t kBig4Opt = 0;
 constexpr uint32_t kSmallOpt = 16;
 constexpr uint32_t kMatchOpt = 512 | 16;               // ballot-match ranking (fallback)
-// (XCD ranges, grs_pass.hpp draw_ticket_xr, stay a lab option: they need the digit counts of
-// every range for every pass, and a range of pass p > 0 holds the keys pass p - 1 scattered
-// there, which no upfront histogram of the input positions gives)
+// (XCD ranges stay a lab option, tools/lab_pass.hpp: they need the digit counts of every
+// range for every pass, and a range of pass p > 0 holds the keys pass p - 1 scattered there,
+// which no upfront histogram of the input positions gives)
 
 // Status words of one look-back buffer for `tiles` tiles of radix `radix`.
 size_t status_words_for(size_t tiles, size_t radix) { return grs::lb3_status_words(tiles, radix); }
@@ -310,9 +294,11 @@ struct grs_sorter {
   int tile_mode = -1;              // GRS_OPT_TILE: -1 by size, 0 small, 1 big
   int pass_mode = 0;               // GRS_OPT_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
   bool sharded_general = false;    // GRS_OPT_SHARDED_PATH: one rank takes the G-rank path too
-  bool sharded_contig = false;     // GRS_OPT_SHARDED_SEND: histogram + contiguous send buckets
+  int sharded_send = 0;            // GRS_OPT_SHARDED_SEND: 0 regions, 1 histogram + contiguous
+                                   // buckets, 2 test: regions of n / (2G) (full buckets spill)
   int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
+  int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
 };
 
 extern "C" {
@@ -457,12 +443,26 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       break;
     case GRS_OPT_SHARDED_SEND:
       if (value < 0 || value > 1) return bad();
-      s->sharded_contig = value == 1;
+      s->sharded_send = value;
       break;
     case GRS_OPT_EXCHANGE:
       if (value < 0 || value > 2) return bad();
       s->sharded_exchange = value;
       break;
+    case GRS_OPT_FAULT_TILE: {
+      if (value < -1) return bad();
+      // the pass's debug words after the error word (grs_pass.hpp PassDebug): fault tile + 1,
+      // spin bound
+      const uint32_t w[2] = {static_cast<uint32_t>(value + 1), value >= 0 ? (1u << 12) : 0u};
+      int prev = 0;
+      GRS_HIP(hipGetDevice(&prev));
+      GRS_HIP(hipSetDevice(s->device));
+      const hipError_t e = hipMemcpy(s->ctrl + GRS_CTRL_ERROR + 1, w, sizeof(w), hipMemcpyHostToDevice);
+      (void)hipSetDevice(prev);
+      if (e != hipSuccess) return set_err(GRS_EHIP, "grs_set_option: hipMemcpy failed");
+      s->fault_tile = value;
+      break;
+    }
     case GRS_OPT_MERGE:
       if (value < 0 || value > 1) return bad();
       s->merge_mode = value;
@@ -501,9 +501,10 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_RECORDS: *value = s->rec_mode; break;
     case GRS_OPT_RANK: *value = s->rank_mode; break;
     case GRS_OPT_SHARDED_PATH: *value = s->sharded_general ? 1 : 0; break;
-    case GRS_OPT_SHARDED_SEND: *value = s->sharded_contig ? 1 : 0; break;
+    case GRS_OPT_SHARDED_SEND: *value = s->sharded_send; break;
     case GRS_OPT_EXCHANGE: *value = s->sharded_exchange; break;
     case GRS_OPT_MERGE: *value = s->merge_mode; break;
+    case GRS_OPT_FAULT_TILE: *value = s->fault_tile; break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -624,7 +625,7 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
                        uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
                        uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream,
-                       uint32_t expect_tile = 0, uint32_t range_tiles = 0) {
+                       uint32_t expect_tile = 0) {
   const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
   if (status_words_for(tiles, 1u << RB) > s->status_words)
     return set_err(GRS_ECAPACITY, "status buffer too small");
@@ -635,14 +636,12 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
     hipLaunchKernelGGL((grs::grs_onesweep_v6<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(grid), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev,
-                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE), range_tiles);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
   } else {
     hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev,
-                       static_cast<uint32_t>(GRS_CTRL_HIST_STRIDE), range_tiles);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
   }
   GRS_HIP(hipGetLastError());
   return GRS_OK;
@@ -654,16 +653,16 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_rec(int kind, grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc,
                       uint32_t* vdst, uint32_t n, const grs::RadixDigit<K>& dig,
                       const uint32_t* hist, uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt,
-                      hipStream_t stream, uint32_t expect_tile, uint32_t range_tiles) {
+                      hipStream_t stream, uint32_t expect_tile) {
   using Dig = grs::RadixDigit<K>;
   constexpr bool R = sizeof(K) == 4 && PAIRS && RB == 8;
   constexpr uint32_t W = R ? 8192u : 0u, Rd = R ? 4096u : 0u, RS = R ? 16384u : 0u, WS = R ? 32768u : 0u;
   switch (R ? kind : 0) {
-    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
-    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
-    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
-    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
-    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, range_tiles);
+    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
   }
 }
 
@@ -698,8 +697,6 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   uint32_t* hist = cb[s->cb_i];
   uint32_t* tickets = hist + GRS_CTRL_TICKETS;
   uint32_t* hist_next = cb[s->cb_i ^ 1];   // zeroed by this call's histogram kernel
-  // one look-back chain over all tiles (no XCD ranges: see kMatchOpt's note)
-  const uint32_t range_tiles = std::max<uint32_t>(tiles, 1);
   int ev = 0;
   hipEvent_t* evs = s->ring ? s->ev + (s->calls % s->ring) * grs_sorter::EV_PER_CALL : nullptr;
   auto mark = [&]() -> grs_status {
@@ -776,21 +773,20 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     const Dig dig{shift, (1u << bits) - 1u};
     const uint32_t* ph = hist + p * RADIX;
     uint32_t* tk = tickets + p * GRS_XCDS;
-    const uint32_t rt = range_tiles;
     if (s->rank_mode != 0) {
-      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt)
-              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt);
+      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile)
+              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile);
     } else if (xl) {
       if constexpr (kXlType)
-        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, rt);
+        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
-        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, rt);
+        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else if (big && rec) {
-      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, rt);
+      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else {
-      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt)
-              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, rt);
+      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile)
+              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile);
     }
     if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;
@@ -1505,10 +1501,14 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   //    partition is then redone with a bucket histogram into contiguous buckets in the sorter's
   //    ping-pong scratch (free until step 8) -- the counts, and so the exchange plan, are the
   //    same.  Contiguous buckets are also the path when G * region reaches 2^32.
+  //    (GRS_OPT_SHARDED_SEND = 2, a test hook: regions of n / (2G), so that full buckets spill
+  //    and the redo path runs even on one rank)
   const uint32_t region =
       n == 0 ? 0u
-             : static_cast<uint32_t>(std::min<uint64_t>(n, static_cast<uint64_t>(n) * 5 / 4 / g + 65536));
-  bool regions = n > 0 && static_cast<uint64_t>(g) * region < (1ull << 32) && !s->sharded_contig;
+      : s->sharded_send == 2
+          ? std::max<uint32_t>(1u, n / (2u * static_cast<uint32_t>(g)))
+          : static_cast<uint32_t>(std::min<uint64_t>(n, static_cast<uint64_t>(n) * 5 / 4 / g + 65536));
+  bool regions = n > 0 && static_cast<uint64_t>(g) * region < (1ull << 32) && s->sharded_send != 1;
   K* send_k = static_cast<K*>(s->alt_keys);
   uint32_t* send_v = s->alt_vals;
   const size_t xitems = static_cast<size_t>(g - 1) * region + n;   // region-mode buffer items
@@ -1555,6 +1555,14 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
     const grs_status r = run_partition_n<K, PAIRS, N>(s, keys, vals, send_k, send_v, n, Dig{}, dig,
                                                       g - 1, cnt, st, 0u);
     if (r != GRS_OK) return r;
+    // the redone partition's look-back must not have timed out before its buckets are sent
+    // (one more synchronisation, on this rare path only)
+    GRS_HIP(hipMemcpyAsync(s->shard_host + g * g, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st));
+    GRS_HIP(hipStreamSynchronize(st));
+    if (s->shard_host[g * g] != 0) {
+      GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
+      return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a partition look-back spin exceeded its bound");
+    }
   }
   if (regions)
     for (int p = 0; p < g; ++p) soff[p] = static_cast<uint64_t>(p) * region;
@@ -2033,6 +2041,12 @@ grs_status grs_shard_decode_merge(grs_sorter* s, const uint32_t* d_recv, int nra
   return r;
 }
 
+grs_status grs_sharded_redo_count(const grs_sorter* s, uint64_t* count) {
+  if (!s || !count) return set_err(GRS_EINVAL, "grs_sharded_redo_count: NULL argument");
+  *count = s->x_region_redo;
+  return GRS_OK;
+}
+
 grs_status grs_sharded_last_timing(grs_sorter* s, grs_sharded_timing* out) {
   if (!s || !out) return set_err(GRS_EINVAL, "grs_sharded_last_timing: NULL argument");
   std::memset(out, 0, sizeof(*out));
@@ -2134,13 +2148,28 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
   return GRS_OK;
 }
 
-// The record sort's scratch (first use, grown on demand): n keys | n indices | n records.
-static grs_status records_scratch(grs_sorter* s, size_t n, size_t record_bytes, void** keys,
-                                  uint32_t** idx, void** copy) {
+// The record sort's scratch (first use, grown on demand): keys | indices | record copy, laid
+// out for the sorter's CAPACITY, never for one call's n: the key and index buffers that
+// grs_records_key_buffers hands out sit at the same place whatever n a later call sorts (a
+// layout by n would put a smaller call's record copy over the caller's indices).  Growing
+// (a larger record size) frees the buffer, so it is refused while `held` (the caller's keys or
+// indices of this call) points into it.
+static grs_status records_scratch(grs_sorter* s, size_t record_bytes, void** keys, uint32_t** idx,
+                                  void** copy, const void* held0 = nullptr,
+                                  const void* held1 = nullptr) {
   const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  const size_t cap = std::max<size_t>(s->capacity, 1);
   auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
-  const size_t need = al(n * kb) + al(n * 4) + al(n * record_bytes);
+  const size_t need = al(cap * kb) + al(cap * 4) + al(cap * record_bytes);
   if (s->rec_bytes < need) {
+    auto inside = [&](const void* p) {
+      const char* b = static_cast<const char*>(s->rec_buf);
+      return p && b && static_cast<const char*>(p) >= b && static_cast<const char*>(p) < b + s->rec_bytes;
+    };
+    if (inside(held0) || inside(held1))
+      return set_err(GRS_EINVAL, "grs_sort_records_by_keys: the record scratch must grow for this "
+                                 "record size while the key buffers passed live in it (call "
+                                 "grs_records_key_buffers with this record size first)");
     if (s->rec_buf) (void)hipFree(s->rec_buf);
     s->rec_buf = nullptr;
     s->rec_bytes = 0;
@@ -2152,8 +2181,8 @@ static grs_status records_scratch(grs_sorter* s, size_t n, size_t record_bytes, 
   }
   char* b = static_cast<char*>(s->rec_buf);
   *keys = b;
-  *idx = reinterpret_cast<uint32_t*>(b + al(n * kb));
-  *copy = b + al(n * kb) + al(n * 4);
+  *idx = reinterpret_cast<uint32_t*>(b + al(cap * kb));
+  *copy = b + al(cap * kb) + al(cap * 4);
   return GRS_OK;
 }
 
@@ -2168,7 +2197,7 @@ grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes,
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
   void* copy = nullptr;
-  const grs_status r = records_scratch(s, std::max<size_t>(n, 1), record_bytes, d_keys, d_idx, &copy);
+  const grs_status r = records_scratch(s, record_bytes, d_keys, d_idx, &copy);
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
 }
@@ -2189,7 +2218,7 @@ grs_status grs_sort_records_by_keys(grs_sorter* s, void* d_records, size_t n, si
   void* keys = nullptr;
   uint32_t* idx = nullptr;
   void* copy = nullptr;
-  grs_status r = records_scratch(s, n, record_bytes, &keys, &idx, &copy);
+  grs_status r = records_scratch(s, record_bytes, &keys, &idx, &copy, d_keys, d_idx);
   // the caller's keys / indices may live in the scratch (grs_records_key_buffers) or anywhere
   if (r == GRS_OK) r = grs_sort(s, d_keys, d_idx, n, stream);                     // stable pairs
   if (r == GRS_OK) r = grs_gather_records(d_records, copy, d_idx, n, record_bytes, stream);  // K5
@@ -2220,7 +2249,7 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
   void* keys = nullptr;
   uint32_t* idx = nullptr;
   void* copy = nullptr;
-  grs_status r = records_scratch(s, n, record_bytes, &keys, &idx, &copy);
+  grs_status r = records_scratch(s, record_bytes, &keys, &idx, &copy);
   const grs::KeyExtract kx{key->kind, key->offset, key->transform,
                            {key->lo[0], key->lo[1], key->lo[2]}, {key->hi[0], key->hi[1], key->hi[2]}};
   if (r == GRS_OK) {   // K1: one fused pre-pass, key + index

@@ -457,6 +457,12 @@ constexpr int kMkSPT = 16;
 constexpr int kMkMaxTile = kMkSpacing * (kMkSPT + kMaxRanks);   // 8192
 constexpr int kMkBlock = 1024;
 constexpr int kMkVT = kMkMaxTile / kMkBlock;                      // 8 loads / stores per thread
+// A tile holds at most (kMkSPT + k) blocks of kMkSpacing elements for k <= kMaxRanks runs (the
+// boundaries are every kMkSPT-th sample, and each run adds at most one partial block), so the
+// tile kernel's buffers must hold exactly that bound: changing kMaxRanks, kMkSPT or the block
+// size without kMkMaxTile would otherwise truncate tiles.
+static_assert(kMkMaxTile == kMkSpacing * (kMkSPT + kMaxRanks) && kMkVT * kMkBlock == kMkMaxTile,
+              "k-way merge tile bound");
 constexpr int kMkChunk = 8;                                       // outputs per merge step
 constexpr int kMkStride = kMaxRanks;                              // co-rank row stride
 
@@ -564,6 +570,8 @@ __global__ __launch_bounds__(kMkBlock, 2) void grs_mergek_tiles(const uint32_t* 
     if (t == GRS_WAVE - 1) O0 = oi;
   }
   __syncthreads();
+  // <= kMkMaxTile by construction (static_assert above); the min only keeps a corrupt co-rank
+  // table inside the LDS buffers
   const uint32_t len = min(P[m.kp], static_cast<uint32_t>(kMkMaxTile));
   // the tile's segments, all loads in flight, then LDS
   uint32_t x[kMkVT];

@@ -9,6 +9,9 @@
 //        grs_demo distance [N] [seed]
 //        a user-defined key functor (ParallelSortBy<Particle, DistanceKey>): particles by their
 //        float distance from a point, through grs::OrderedBits, verified the same way
+//        grs_demo fault [N] [seed]
+//        the main call pattern with the look-back fault hook set (GRS_OPT_FAULT_TILE = 0):
+//        Sort() must throw grs::Error(GRS_ETIMEOUT); the demo prints it and exits 2
 // The reference's std::random_shuffle (main.cpp:125) is replaced by a seeded Fisher-Yates
 // over splitmix64 so the run is reproducible; verification strengthens the reference's
 // adjacent-order check (ParallelSort.cpp:336-352) to "output == 0..N-1".
@@ -149,6 +152,11 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
+  const bool fault = argc > 1 && std::strcmp(argv[1], "fault") == 0;
+  if (fault) {
+    --argc;
+    ++argv;
+  }
   const unsigned n = argc > 1 ? static_cast<unsigned>(std::strtoul(argv[1], nullptr, 10)) : 1000000u;
   uint64_t seed = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1;
   try {
@@ -159,6 +167,7 @@ int main(int argc, char** argv) {
     originalData->Upload(demoData);                                 // main.cpp:146-149
 
     ParallelSort parallelSort(originalData);                        // main.cpp:152
+    if (fault) parallelSort.SetOption(GRS_OPT_FAULT_TILE, 0);
     parallelSort.SetProfiling(true);
     parallelSort.Sort();                                            // main.cpp:159-160
     parallelSort.Sort();

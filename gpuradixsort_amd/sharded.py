@@ -142,6 +142,12 @@ class ShardedSorter:
                 "bytes_received": int(t.bytes_received),
                 "exchange": "presorted" if t.presorted else "partition-first"}
 
+    def redo_count(self) -> int:
+        """Partition-first calls redone into contiguous buckets after a region spill."""
+        c = ctypes.c_uint64()
+        check(lib().grs_sharded_redo_count(self.sorter._h, ctypes.byref(c)), "grs_sharded_redo_count")
+        return int(c.value)
+
     def count_inversions(self) -> int:
         from .sorter import count_inversions
 

@@ -121,12 +121,22 @@ typedef enum grs_option {
   GRS_OPT_RANK = 5,          /* 0 (default) the device probe's choice, 1 ballot-match ranking */
   GRS_OPT_SHARDED_PATH = 6,  /* grs_sort_sharded on ONE rank: 0 (default) copy + local sort,
                                 1 the G-rank path (a one-GPU rehearsal of the exchange) */
-  GRS_OPT_SHARDED_SEND = 7,  /* partition-first exchange: 0 (default) G regions of n_local items
-                                where they fit, 1 bucket histogram + contiguous buckets */
+  GRS_OPT_SHARDED_SEND = 7,  /* partition-first exchange: 0 (default) one region per bucket in a
+                                send buffer of (G - 1) regions + n_local items, a region being the
+                                even share + 25 % + 64K items (a bucket may spill into the next
+                                region; a spill is detected at the count exchange and the
+                                partition is redone into contiguous buckets), 1 bucket histogram
+                                + contiguous buckets always, 2 test hook: regions of n / (2G)
+                                items, so full buckets spill and the redo path runs */
   GRS_OPT_EXCHANGE = 8,      /* 0 by rank count (default), 1 partition-first, 2 presorted */
-  GRS_OPT_MERGE = 9          /* presorted exchange, receive side: 0 (default) ceil(log2 k)
+  GRS_OPT_MERGE = 9,         /* presorted exchange, receive side: 0 (default) ceil(log2 k)
                                 2-way merge rounds over the k received runs, 1 one k-way merge
                                 pass (sample-delimited tiles merged in LDS; slower at 8 ranks) */
+  GRS_OPT_FAULT_TILE = 10    /* TEST HOOK: -1 (default) off; v >= 0: tile v of every pass never
+                                publishes its look-back tile words and spins give up after 2^12
+                                polls, so the later tiles of its look-back group time out: the
+                                sort's output is wrong and GRS_ETIMEOUT surfaces through
+                                grs_check_error / grs_stream_check_error (the error path's test) */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);
@@ -225,6 +235,9 @@ typedef struct grs_sharded_timing {
   int presorted;
 } grs_sharded_timing;
 grs_status grs_sharded_last_timing(grs_sorter* s, grs_sharded_timing* out);
+/* Partition-first calls whose region send buffer overflowed (a bucket larger than its region)
+ * and were redone into contiguous buckets, since the sorter was created. */
+grs_status grs_sharded_redo_count(const grs_sorter* s, uint64_t* count);
 
 /* RCCL communicator helpers for callers without their own RCCL binding (ctypes, tests):
  * rank 0 creates the id (GRS_RCCL_ID_BYTES bytes), every rank passes it to comm_init. */
@@ -357,8 +370,10 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
  * written d_keys[i] = key of record i (the sorter's key width) and d_idx[i] = i, stream-ordered
  * before this call; the (key, index) pairs are sorted stably (both buffers are overwritten),
  * the records gathered by index and copied back, so d_records[0..n) ends up sorted in place.
- * grs_records_key_buffers hands out sorter-owned device buffers for the keys and indices
- * (valid until the next record-sort call on this sorter grows them).  The C++ template
+ * grs_records_key_buffers hands out sorter-owned device buffers for the keys and indices,
+ * laid out for the sorter's capacity (any n <= capacity may be sorted with them); they stay
+ * valid until a record-sort call with a LARGER record size grows the scratch, which
+ * grs_sort_records_by_keys refuses (GRS_EINVAL) while the buffers it is passed live in it.  The C++ template
  * grs::ParallelSortBy (grs_parallel_sort.hpp) wraps both around a __device__ key functor. */
 grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes, void** d_keys,
                                    uint32_t** d_idx);

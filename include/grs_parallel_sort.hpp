@@ -215,6 +215,12 @@ class ParallelSort {
   }
   void CheckError() { grs::check(grs_stream_check_error(_sorter, _stream), "ParallelSort::CheckError"); }
 
+  // Pins a kernel choice of the sorter (grs_set_option; A/B runs, and the error path's test
+  // hook GRS_OPT_FAULT_TILE).
+  void SetOption(grs_option opt, int value) {
+    grs::check(grs_set_option(_sorter, opt, value), "ParallelSort::SetOption");
+  }
+
   // Per-phase GPU times of the last Sort() when profiling is on (durations.txt successor).
   void SetProfiling(bool on) { grs::check(grs_set_profiling(_sorter, on ? 1 : 0), "SetProfiling"); }
   grs_timing LastTiming() {

@@ -74,6 +74,41 @@ def test_record_sort_gathers_whole_records(gpu):
     assert np.array_equal(d7.cpu().numpy(), rec7[perm])
 
 
+def test_record_key_buffers_at_capacity_then_smaller_n(gpu):
+    """grs_records_key_buffers hands out the sorter's key / index buffers once (at capacity);
+    a later grs_sort_records_by_keys of FEWER records must not lay its record copy over those
+    buffers (the scratch layout follows the capacity, not the call's n), and growing the
+    scratch under them (a larger record size) is refused instead of freeing them."""
+    import ctypes
+
+    import gpuradixsort_amd as grs
+    from gpuradixsort_amd._lib import lib
+
+    L = lib()
+    cap, rb = 1 << 20, 16
+    s = grs.RadixSorter(cap, key_bits=32, pairs=True)
+    keys_p, idx_p = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.grs_records_key_buffers(s._h, cap, rb, ctypes.byref(keys_p), ctypes.byref(idx_p)) == 0
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rng = np.random.default_rng(21)
+    for n in (cap, cap // 2, 4097, 1):
+        rec = rng.integers(0, 256, (n, rb), dtype=np.uint8)
+        keys = rng.integers(0, 1 << 10, n).astype(np.uint32)   # ties: the sort must be stable
+        d_rec = torch.from_numpy(rec).to(gpu)
+        d_keys = torch.from_numpy(keys).to(gpu)
+        # the caller's "key kernel": key and index into the sorter-owned buffers
+        assert L.grs_copy_u32(ctypes.c_void_p(d_keys.data_ptr()), keys_p, n, stream) == 0
+        assert L.grs_iota_u32(idx_p, n, 0, stream) == 0
+        assert L.grs_sort_records_by_keys(s._h, ctypes.c_void_p(d_rec.data_ptr()), n, rb, keys_p,
+                                          idx_p, stream) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(d_rec.cpu().numpy(), rec[oracle.stable_argsort(keys)]), n
+    # a larger record size would grow (free) the scratch the key buffers live in: refused
+    d_big = torch.zeros((16, 64), dtype=torch.uint8, device=gpu)
+    assert L.grs_sort_records_by_keys(s._h, ctypes.c_void_p(d_big.data_ptr()), 16, 64, keys_p,
+                                      idx_p, stream) == 1   # GRS_EINVAL
+
+
 @pytest.mark.parametrize("kb", [32, 64])
 def test_record_sort_key_extraction_hook(gpu, kb):
     """grs_sort_records (the K1 hook in the C-ABI): 28-byte particles sorted by the Morton

@@ -152,3 +152,40 @@ def test_sharded_capacity_errors(gpu, world1):
                                      ctypes.byref(n_out), None, None)
     assert rc == _lib.GRS_EINVAL        # NULL communicator / output
     s.sorter.close()
+
+
+@pytest.mark.parametrize("key_bits,pairs", [(32, True), (64, False), (64, True), (32, False)])
+def test_region_spill_redo(gpu, world1, key_bits, pairs):
+    """The partition-first exchange's region send buffer (include/grs.h GRS_OPT_SHARDED_SEND):
+    a bucket larger than its region spills into the next one, the count matrix shows it at
+    the host synchronisation and the partition is redone into contiguous buckets.  The test
+    hook sharded_send=shrunk (regions of n / 2G) makes every full bucket spill, so the redo
+    runs on one rank too: u32 pairs (the joint key + payload scratch), u64 keys and u64 pairs,
+    2^20 + 3 items; the output must be the exact stable sort and the redo counted."""
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    rng = np.random.default_rng(31 + key_bits + pairs)
+    dt = np.uint32 if key_bits == 32 else np.uint64
+    n = (1 << 20) + 3
+    keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+    keys[::5] = 77                                   # ties: stability across the redo
+    perm = oracle.stable_argsort(keys)
+    s = ShardedSorter(n, key_bits=key_bits, pairs=pairs, device=gpu, comm=world1,
+                      options={"sharded_path": "general", "exchange": "partition",
+                               "sharded_send": "shrunk"})
+    k = torch.from_numpy(keys).to(gpu)
+    v = torch.arange(n, dtype=torch.int64, device=gpu).to(torch.uint32) if pairs else None
+    before = s.redo_count()
+    for i in range(2):
+        ko, vo = s.sort(k.clone(), v.clone() if pairs else None)
+        assert s.redo_count() == before + i + 1
+        assert s.last_n_out == n
+        assert np.array_equal(ko.cpu().numpy(), keys[perm])
+        if pairs:
+            assert np.array_equal(vo.cpu().numpy(), perm)
+    # the default regions (even share + 25 % + 64K) hold a one-rank bucket: no redo
+    s.sorter.set_option("sharded_send", "regions")
+    ko, _ = s.sort(k.clone(), v.clone() if pairs else None)
+    assert s.redo_count() == before + 2
+    assert np.array_equal(ko.cpu().numpy(), keys[perm])
+    s.sorter.close()

@@ -5,7 +5,7 @@
 
 #include <type_traits>
 
-#include "../gpuradixsort_amd/csrc/grs_pass.hpp"
+#include "lab_pass.hpp"
 
 namespace {
 
@@ -170,6 +170,96 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu_pairs(const uint32_t* __res
   }
 }
 
+// MODE 3's runs (every run boundary 4 B past a 128-B line; tiles T and T + 1 = blocks b, b + 1
+// on different XCDs) with the boundary lines HANDED OFF instead of written twice partially:
+// tile T writes the tail of each run, [floor32(E), E), into one whole 128-B slot line of a ring
+// (sc1 stores), publishes a flag (vmcnt(0), barrier, sc1 flag store), stores the rest of its
+// runs, then waits for tile T - 1's flag and writes the head of each of its runs,
+// [floor32(D), D), from T - 1's slot line: every boundary line reaches memory once, whole,
+// from one CU.  VAR 0: as described; 1: no flag wait (timing of the traffic alone, wrong
+// data); 2: the slot lines are written by plain stores (no sc1) and no flag (traffic, wrong).
+constexpr uint32_t kEmuRing = 2048;
+template <int BLOCK, int ITEMS, int VAR>
+__global__ __launch_bounds__(BLOCK) void scatter_emu_handoff(const uint32_t* __restrict__ in,
+                                                             uint32_t* __restrict__ out, uint32_t n,
+                                                             uint32_t* __restrict__ ring,
+                                                             uint32_t* __restrict__ flags,
+                                                             uint32_t epoch, uint32_t* err) {
+  constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 256, WAVES = BLOCK / 64;
+  extern __shared__ uint32_t pad_lds[];
+  const uint32_t T = blockIdx.x;
+  const uint32_t tiles = n / TILE;
+  if (T >= tiles) return;
+  const uint32_t region = n / 256;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t key[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) key[j] = in[T * TILE + w * 64 * ITEMS + j * 64 + lane];
+  if (n == 0) pad_lds[threadIdx.x] = key[0];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) acc ^= key[j];
+  // run r of tile T: [D, E) with D = r * region + T * RUN + 1
+  const bool defer_tail = T + 1 < tiles;   // every E is 4 B past a line here (RUN % 32 = 16)
+  const bool take_head = T > 0;
+  // (1) slot lines: two runs per wave-instruction (lanes 0-31: run r, 32-63: run r + 1)
+  uint32_t* slot = ring + static_cast<size_t>(T % kEmuRing) * 256 * 32;
+  if (defer_tail) {
+    for (uint32_t r = w * 2 + (lane >> 5); r < 256; r += 2 * WAVES) {
+      const uint32_t E = r * region + T * RUN + 1 + RUN;
+      const uint32_t j = lane & 31;
+      const uint32_t v = acc + (E & ~31u) + j;
+      if (VAR == 2) slot[r * 32 + j] = v;
+      else __hip_atomic_store(&slot[r * 32 + j], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (VAR == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_store(&flags[T % kEmuRing], epoch * 65536u + T, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // (2) the runs, minus the deferred tails
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * BLOCK + threadIdx.x;
+    const uint32_t r = i / RUN;
+    const uint32_t dst = r * region + T * RUN + i % RUN + 1;
+    const uint32_t E = r * region + T * RUN + 1 + RUN;
+    if (!(defer_tail && dst >= (E & ~31u))) out[dst] = key[k];
+  }
+  // (3) the heads from T - 1's slot lines
+  if (take_head) {
+    const uint32_t* ps = ring + static_cast<size_t>((T - 1) % kEmuRing) * 256 * 32;
+    if (VAR == 0) {
+      if (threadIdx.x == 0) {
+        const uint32_t want = epoch * 65536u + (T - 1);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(&flags[(T - 1) % kEmuRing], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) != want) {
+          if (++spins > (1u << 20)) {
+            atomicOr(err, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+    }
+    for (uint32_t r = w * 2 + (lane >> 5); r < 256; r += 2 * WAVES) {
+      const uint32_t D = r * region + T * RUN + 1;
+      const uint32_t j = lane & 31;
+      if (j < (D & 31u)) {
+        const uint32_t v = VAR == 2 ? ps[r * 32 + j]
+                                    : __hip_atomic_load(&ps[r * 32 + j], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        out[(D & ~31u) + j] = v;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 
@@ -197,7 +287,7 @@ __global__ __launch_bounds__(1024) void lds_atomic_rate(uint32_t* out, int iters
 
 // XCC id of every block (placement check of draw_ticket_xr's counter choice)
 __global__ void xcc_probe(uint32_t* out) {
-  if (threadIdx.x == 0) out[blockIdx.x] = grs::xcc_id();
+  if (threadIdx.x == 0) out[blockIdx.x] = grs_lab::xcc_id();
 }
 
 extern "C" {
@@ -262,6 +352,27 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
   return 0;
 }
 
+// boundary-line hand-off emulation (scatter_emu_handoff): block, items, variant
+int lab2_emu_handoff(int block, int items, int var, int lds, const void* in, void* out, uint32_t n,
+                     uint32_t* ring, uint32_t* flags, uint32_t epoch, uint32_t* err, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t tiles = n / (block * items);
+  const void* k = nullptr;
+  switch (block * 100000 + items * 100 + var) {
+    case 102403600: k = (const void*)scatter_emu_handoff<1024, 36, 0>; break;
+    case 102403601: k = (const void*)scatter_emu_handoff<1024, 36, 1>; break;
+    case 102403602: k = (const void*)scatter_emu_handoff<1024, 36, 2>; break;
+    case 102404800: k = (const void*)scatter_emu_handoff<1024, 48, 0>; break;
+    case 102404801: k = (const void*)scatter_emu_handoff<1024, 48, 1>; break;
+    default: return -1;
+  }
+  const uint32_t* i = static_cast<const uint32_t*>(in);
+  uint32_t* o = static_cast<uint32_t*>(out);
+  void* args[] = {&i, &o, &n, &ring, &flags, &epoch, &err};
+  if (hipLaunchKernel(k, dim3(tiles), dim3(block), args, lds, s) != hipSuccess) return -2;
+  return 0;
+}
+
 // pairs memory-pattern emulation: block, items, aos, dynamic LDS bytes; AoS buffers are 2n words
 int lab2_emu_pairs(int block, int items, int aos, int lds, const void* kin, const void* vin, void* kout,
                    void* vout, uint32_t n, void* stream) {
@@ -297,7 +408,7 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
   case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000000L + O: {             \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                               \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
-    hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
+    hipLaunchKernelGGL((grs_lab::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
                        0, s, (const KT*)in, (KT*)out, vin, vout, n,                            \
                        grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
                        (const grs::RadixDigit<KT>*)nullptr, hist_stride, range_tiles);        \
@@ -366,7 +477,7 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                           \
     const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
-    hipLaunchKernelGGL((grs::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O>), dim3(g), dim3(B), 0,   \
+    hipLaunchKernelGGL((grs_lab::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O>), dim3(g), dim3(B), 0,   \
                        s, (const KT*)in, (KT*)out, vin, vout, n, grs::RadixDigit<KT>{shift, 255u}, \
                        hist, ticket, st, st2, err, (const grs::RadixDigit<KT>*)nullptr,         \
                        hist_stride, range_tiles);                                               \
@@ -401,7 +512,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
   case ((B * 1000L + I) * 10 + M) * 100000000L + O: {                                          \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
     const uint32_t g = std::min<uint32_t>(tiles, grid);                                        \
-    hipLaunchKernelGGL((grs::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
+    hipLaunchKernelGGL((grs_lab::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
                        dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
                        grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
                        (const grs::RadixDigit<uint32_t>*)nullptr, hist_stride, range_tiles);   \
@@ -430,7 +541,7 @@ int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* ou
 #define V(B, I, M, O)                                                                          \
   case ((B * 1000L + I) * 10 + M) * 1000 + O: {                                                \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
-    hipLaunchKernelGGL((grs::grs_onesweep_v4<uint32_t, false, 4, B, I, M, O>), dim3(tiles),     \
+    hipLaunchKernelGGL((grs_lab::grs_onesweep_v4<uint32_t, false, 4, B, I, M, O>), dim3(tiles),     \
                        dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
                        grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
                        (const grs::RadixDigit<uint32_t>*)nullptr);                             \

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--xcc", action="store_true", help="print the XCC id of each block (placement)")
     ap.add_argument("--lib", default="", help="load tools/liblab2_LIB.so (a build with other knobs)")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
+    ap.add_argument("--emu-handoff", default="", help="block:items:var:lds,... boundary-line hand-off emulation")
     ap.add_argument("--emu-pairs", default="", help="block:items:aos:lds,... pairs memory pattern (SoA vs AoS)")
     a = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, f"liblab2{'_' + a.lib if a.lib else ''}.so"))
@@ -174,6 +175,26 @@ def main():
                 ts.append(e0.elapsed_time(e1))
             med = statistics.median(ts)
             print(f"emu {e:20s} median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s", flush=True)
+    if a.emu_handoff:
+        keys, out, _ = bufs[32]
+        ring = torch.zeros(2048 * 256 * 32, dtype=torch.uint32, device=dev)
+        flags = torch.zeros(2048, dtype=torch.uint32, device=dev)
+        herr = torch.zeros(4, dtype=torch.uint32, device=dev)
+        epoch = 1
+        for e in a.emu_handoff.split(","):
+            b, it, var, lds = (int(x) for x in e.split(":"))
+            ts = []
+            for _ in range(a.rounds):
+                epoch += 1
+                e0.record()
+                assert L.lab2_emu_handoff(b, it, var, lds, P(keys), P(out), ctypes.c_uint32(n), P(ring),
+                                          P(flags), ctypes.c_uint32(epoch), P(herr), sp) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            print(f"emu_handoff {e:16s} median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s "
+                  f"err={int(herr[0].item())}", flush=True)
     if a.emu_pairs:
         # 2^28-pair C3 shape unless --n says otherwise: SoA (two arrays) vs AoS (one 8-B array)
         npair = n
