@@ -45,17 +45,20 @@
 #define GRS_LB_GWIN_XL 4
 #endif
 
-// XCDs of an MI355X (8 x 32 CUs, each XCD with its own L2): the pass's XCD ranges.
+// XCDs of an MI355X (8 x 32 CUs, each XCD with its own L2): ticket counters are XCD-strided.
 #define GRS_XCDS 8
 
 // Layout of the per-sorter control block (uint32 words), zeroed once per sort call.
-//   [0, GRS_CTRL_HIST_WORDS)           digit histograms, [xcd range][pass][radix]: range c at
-//                                      c * GRS_CTRL_HIST_STRIDE (range 0 only without ranges)
-//   GRS_CTRL_TICKETS + pass * 8 + c    per-pass tile ticket counter of XCD range c
+//   [0, GRS_CTRL_HIST_WORDS)           digit histograms, [pass][row][256]: row 0 holds what the
+//                                      upfront histogram kernel counted; with the histogram
+//                                      fold, pass p - 1's tiles add pass p's digit counts into
+//                                      row (tile % GRS_FOLD_ROWS) and pass p sums the rows
+//   GRS_CTRL_TICKETS + pass * 8        per-pass tile ticket counter
 //   GRS_CTRL_ERROR                     nonzero = a bounded spin timed out
 #define GRS_MAX_PASSES 16               // u64 keys at 4-bit digits
-#define GRS_CTRL_HIST_STRIDE 2048       // >= max over configs of passes * radix (8*256, 16*16)
-#define GRS_CTRL_HIST_WORDS (GRS_XCDS * GRS_CTRL_HIST_STRIDE)
+#define GRS_FOLD_ROWS 16                // rows the fold's atomic adds are spread over
+#define GRS_HIST_PASS_STRIDE (GRS_FOLD_ROWS * 256)
+#define GRS_CTRL_HIST_WORDS (GRS_MAX_PASSES * GRS_HIST_PASS_STRIDE)
 #define GRS_CTRL_TICKETS GRS_CTRL_HIST_WORDS
 #define GRS_CTRL_ERROR (GRS_CTRL_TICKETS + GRS_MAX_PASSES * GRS_XCDS)
 #define GRS_CTRL_WORDS (GRS_CTRL_ERROR + 16)   // multiple of 4 words (16-B memset)

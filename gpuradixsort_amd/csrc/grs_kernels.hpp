@@ -197,18 +197,18 @@ struct Hist2Layout {
 template <typename K>
 constexpr int kHist2GridShift = sizeof(K) == 4 ? 20 : 19;
 
-// range_keys > 0 (the pass's XCD ranges, grs_pass.hpp): block b counts range b % GRS_XCDS
-// (keys [c * range_keys, (c + 1) * range_keys)) with the other blocks of its range and
-// flushes into g_hist + c * hist_stride: per-range histograms (the grid is a multiple of
-// GRS_XCDS, range_keys a multiple of the 16-byte vector).
-template <typename K, int RB, bool FULL>
+// QN: super digits counted (MAXQ, or 1 with the histogram fold, where each pass counts the
+// next pass's digit itself and this kernel only pass 0's).  Pass p's counts go to
+// g_hist[p * GRS_HIST_PASS_STRIDE + d] (row 0 of its rows).
+template <typename K, int RB, bool FULL, int QN = Hist2Layout<K>::MAXQ>
 __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
     uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words,
-    uint32_t range_keys = 0, uint32_t hist_stride = 0, uint32_t* __restrict__ clear_ctrl = nullptr) {
+    uint32_t* __restrict__ clear_ctrl = nullptr) {
   static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
   using HL = Hist2Layout<K>;
   constexpr int MAXQ = HL::MAXQ;
+  static_assert(QN >= 1 && QN <= MAXQ, "super digits counted");
   constexpr int COPIES = HL::COPIES;
   constexpr uint32_t HB = HL::BLOCK;
   __shared__ __attribute__((aligned(16))) uint32_t s_hist[HL::WORDS];
@@ -219,11 +219,10 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     for (uint32_t i = t; i < HL::WORDS / 4; i += HB) z[i] = make_uint4(0, 0, 0, 0);
   }
   for (uint32_t i = blockIdx.x * HB + t; i < clear_words; i += gridDim.x * HB) clear[i] = 0;
-  // the next sort's control block: its range-0 histograms and its tickets
+  // the next sort's control block: its histograms (every row) and its tickets
   if (clear_ctrl != nullptr) {
-    constexpr uint32_t H = GRS_CTRL_HIST_STRIDE, TK = GRS_MAX_PASSES * GRS_XCDS;
-    for (uint32_t i = blockIdx.x * HB + t; i < H + TK; i += gridDim.x * HB)
-      clear_ctrl[i < H ? i : GRS_CTRL_TICKETS + (i - H)] = 0;
+    constexpr uint32_t H = GRS_CTRL_HIST_WORDS, TK = GRS_MAX_PASSES * GRS_XCDS;
+    for (uint32_t i = blockIdx.x * HB + t; i < H + TK; i += gridDim.x * HB) clear_ctrl[i] = 0;
   }
   __syncthreads();
 
@@ -239,7 +238,7 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
   uint32_t* const base = s_hist + (t & (COPIES - 1));
   auto count = [&](K k) {
 #pragma unroll
-    for (int q = 0; q < MAXQ; ++q) {
+    for (int q = 0; q < QN; ++q) {
       uint32_t d;
       if constexpr (FULL) {
         if constexpr (sizeof(K) == 4) d = __builtin_amdgcn_ubfe(static_cast<uint32_t>(k), 8 * q, 8);
@@ -254,17 +253,7 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
 
   constexpr int VEC = 16 / sizeof(K);
   using V = uint4;
-  // this block's share: all keys (grid-stride), or its range's keys (range-stride)
-  uint32_t lo = 0, cnt_n = n, first = blockIdx.x, nblk = gridDim.x;
-  if (range_keys != 0) {
-    const uint32_t c = blockIdx.x % GRS_XCDS;
-    lo = min(n, c * range_keys);
-    cnt_n = min(n - lo, range_keys);
-    first = blockIdx.x / GRS_XCDS;
-    nblk = gridDim.x / GRS_XCDS;
-    g_hist += c * hist_stride;
-    keys += lo;
-  }
+  const uint32_t cnt_n = n, first = blockIdx.x, nblk = gridDim.x;
   const uint32_t nvec = (reinterpret_cast<uintptr_t>(keys) & 15u) ? 0u : cnt_n / VEC;
   const V* kv = reinterpret_cast<const V*>(keys);
   const uint32_t stride = nblk * HB;
@@ -315,9 +304,10 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     return c;
   };
   if constexpr (RB == 8) {
-    for (uint32_t i = t; i < static_cast<uint32_t>(passes * 256); i += HB) {
+    const uint32_t counted = static_cast<uint32_t>(min(passes, QN));
+    for (uint32_t i = t; i < counted * 256; i += HB) {
       const uint32_t c = total8(i / 256, i % 256);
-      if (c) atomicAdd(&g_hist[i], c);
+      if (c) atomicAdd(&g_hist[(i / 256) * GRS_HIST_PASS_STRIDE + i % 256], c);
     }
   } else {
     // 4-bit passes read their counts off the 8-bit super digits (see above)
@@ -336,13 +326,14 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
       if (i < static_cast<uint32_t>(supers * 256)) s_red[i] = tot[r];
     }
     __syncthreads();
+    static_assert(RB == 8 || QN == MAXQ, "4-bit passes: every super digit counted up front");
     for (uint32_t i = t; i < static_cast<uint32_t>(passes * 16); i += HB) {
       const uint32_t p = i / 16, d = i % 16, q = p / 2;
       const uint32_t* r8 = &s_red[q * 256];
       uint32_t c = 0;
 #pragma unroll
       for (int h = 0; h < 16; ++h) c += (p & 1u) ? r8[d * 16 + h] : r8[h * 16 + d];
-      if (c) atomicAdd(&g_hist[i], c);
+      if (c) atomicAdd(&g_hist[p * GRS_HIST_PASS_STRIDE + d], c);
     }
   }
 }

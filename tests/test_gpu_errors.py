@@ -44,11 +44,12 @@ def _input(gpu, n, key_bits, pairs, seed):
 
 
 def _expected(k, v):
-    ks = k.to(torch.int64) if k.dtype == torch.uint32 else k.view(torch.int64)
-    if k.dtype == torch.uint64:
-        ks = ks ^ (-(2**63))   # unsigned order on a signed sort
-    order = torch.sort(ks, stable=True).indices
-    return k[order].clone(), (v[order].clone() if v is not None else None)
+    """The stable sort of (k, v), computed on the host (numpy: torch cannot index u32)."""
+    import numpy as np
+
+    kh = k.cpu().numpy()
+    order = np.argsort(kh, kind="stable")
+    return kh[order], (v.cpu().numpy()[order] if v is not None else None)
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: f"{s[0]}{'p' if s[1] else ''}-rb{s[2]}-"
@@ -78,9 +79,9 @@ def test_timeout_surfaces_then_sorter_recovers(gpu, shape):
     ek, ev = _expected(k, v)
     s.sort(k, v)
     s.check_error()
-    assert torch.equal(k, ek)
+    assert (k.cpu().numpy() == ek).all()
     if pairs:
-        assert torch.equal(v, ev)
+        assert (v.cpu().numpy() == ev).all()
 
 
 def test_device_wide_check_reports_timeout(gpu):
@@ -100,7 +101,7 @@ def test_device_wide_check_reports_timeout(gpu):
     ek, _ = _expected(k, None)
     s.sort(k)
     s.check_error(device_wide=True)
-    assert torch.equal(k, ek)
+    assert (k.cpu().numpy() == ek).all()
 
 
 def test_python_parallel_sort_raises_then_recovers(gpu):
@@ -121,7 +122,7 @@ def test_python_parallel_sort_raises_then_recovers(gpu):
     ssbo.Upload(k.cpu())
     ps.Sort()
     ek, _ = _expected(k, None)
-    assert torch.equal(ssbo.Download().to(gpu), ek)
+    assert (ssbo.Download().numpy() == ek).all()
 
 
 def test_cpp_facade_demo_exits_nonzero_on_timeout(gpu):

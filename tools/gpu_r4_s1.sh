@@ -16,4 +16,8 @@ step() {  # step <name> <seconds> <cmd...>
 step r4s1_pytest 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step r4s1_emu28 240 python -u tools/lab2.py --n 268435456 --rounds 7 --variants v4:32:0:1024:36:1:272 --emu 1024:36:0:150000,1024:36:1:150000,1024:36:3:150000,1024:36:5:150000,1024:48:3:150000 --emu-handoff 1024:36:0:150000,1024:36:1:150000,1024:36:2:150000,1024:48:0:150000,1024:48:1:150000
 step r4s1_emu30 300 python -u tools/lab2.py --n 1073741824 --rounds 5 --variants v4:32:0:768:64:1:1040 --emu 1024:36:0:150000,1024:36:3:150000,1024:36:5:150000,1024:48:3:150000 --emu-handoff 1024:36:0:150000,1024:36:1:150000,1024:48:0:150000
+step r4s1_p4 240 python -u tools/lab2.py --n 268435456 --rounds 9 --check --variants p4:32:0:1024:36:1:272,p4:32:0:1024:36:1:336,v4:32:0:1024:36:1:272,p4:32:0:768:64:1:1040,p4:32:0:768:64:1:1104
+step r4s1_p4gw2 200 python -u tools/lab2.py --n 268435456 --rounds 9 --lib4 gw2 --variants p4:32:0:1024:36:1:272,p4:32:0:768:64:1:1040
+step r4s1_p4gw4 200 python -u tools/lab2.py --n 268435456 --rounds 9 --lib4 gw4 --variants p4:32:0:1024:36:1:272
+step r4s1_p4_30 300 python -u tools/lab2.py --n 1073741824 --rounds 5 --variants p4:32:0:768:64:1:1040,p4:32:0:768:64:1:1104,p4:64:0:768:44:1:1040,p4:64:0:768:44:1:1104
 step r4s1_bench 400 python -u bench.py

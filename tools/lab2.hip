@@ -178,6 +178,27 @@ __global__ __launch_bounds__(BLOCK) void scatter_emu_pairs(const uint32_t* __res
 // [floor32(D), D), from T - 1's slot line: every boundary line reaches memory once, whole,
 // from one CU.  VAR 0: as described; 1: no flag wait (timing of the traffic alone, wrong
 // data); 2: the slot lines are written by plain stores (no sc1) and no flag (traffic, wrong).
+// C2's memory pattern: the pass's loads and stores at 4-bit digits (16 runs per tile, every run
+// one key past alignment), no compute; lab2.py runs it 8 times back to back (the 8 passes of a
+// 2^24-key sort, ping-pong, MALL-resident) for the floor of the C2 passes.
+template <int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void scatter_emu16(const uint32_t* __restrict__ in,
+                                                       uint32_t* __restrict__ out, uint32_t n) {
+  constexpr uint32_t TILE = BLOCK * ITEMS, RUN = TILE / 16;
+  const uint32_t T = blockIdx.x;
+  if ((T + 1) * TILE > n) return;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t key[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) key[j] = in[T * TILE + w * 64 * ITEMS + j * 64 + lane];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * BLOCK + threadIdx.x;
+    uint32_t dst = (i / RUN) * (n / 16) + T * RUN + i % RUN + 1;
+    out[dst >= n ? 0u : dst] = key[k];
+  }
+}
+
 constexpr uint32_t kEmuRing = 2048;
 template <int BLOCK, int ITEMS, int VAR>
 __global__ __launch_bounds__(BLOCK) void scatter_emu_handoff(const uint32_t* __restrict__ in,
@@ -350,6 +371,25 @@ int lab2_emu(int block, int items, int mode, int lds, const void* in, void* out,
   void* args[] = {&i, &o, &n};
   if (hipLaunchKernel(k, dim3(tiles), dim3(block), args, lds, s) != hipSuccess) return -2;
   return 0;
+}
+
+// C2 memory-pattern emulation: `passes` launches of scatter_emu16, ping-pong between a and b
+int lab2_emu16(int block, int items, int passes, void* a, void* b, uint32_t n, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t tiles = n / (block * items);
+  for (int p = 0; p < passes; ++p) {
+    const uint32_t* i = static_cast<const uint32_t*>(p & 1 ? b : a);
+    uint32_t* o = static_cast<uint32_t*>(p & 1 ? a : b);
+    if (block == 1024 && items == 32)
+      hipLaunchKernelGGL((scatter_emu16<1024, 32>), dim3(tiles), dim3(1024), 0, s, i, o, n);
+    else if (block == 512 && items == 32)
+      hipLaunchKernelGGL((scatter_emu16<512, 32>), dim3(tiles), dim3(512), 0, s, i, o, n);
+    else if (block == 256 && items == 16)
+      hipLaunchKernelGGL((scatter_emu16<256, 16>), dim3(tiles), dim3(256), 0, s, i, o, n);
+    else
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // boundary-line hand-off emulation (scatter_emu_handoff): block, items, variant

@@ -30,11 +30,15 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--xcc", action="store_true", help="print the XCC id of each block (placement)")
     ap.add_argument("--lib", default="", help="load tools/liblab2_LIB.so (a build with other knobs)")
+    ap.add_argument("--lib4", default="", help="p4 variants from tools/liblab4_LIB4.so")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
     ap.add_argument("--emu-handoff", default="", help="block:items:var:lds,... boundary-line hand-off emulation")
+    ap.add_argument("--emu16", default="", help="block:items,... C2 memory pattern: 8 passes of 16 runs")
     ap.add_argument("--emu-pairs", default="", help="block:items:aos:lds,... pairs memory pattern (SoA vs AoS)")
     a = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, f"liblab2{'_' + a.lib if a.lib else ''}.so"))
+    l4 = os.path.join(HERE, f"liblab4{'_' + a.lib4 if a.lib4 else ''}.so")
+    L4 = ctypes.CDLL(l4) if os.path.exists(l4) else None
     vp = ctypes.c_void_p
     P = lambda t: vp(t.data_ptr())  # noqa: E731
     n = a.n
@@ -100,6 +104,8 @@ def main():
                               ctypes.c_uint32(rtiles))
         elif kind == "v4":
             rc = L.lab2_v4(kb, pairs, block, items, v[5], v[6], *args)
+        elif kind == "p4":   # the shipped kernel (tools/lab4.hip): p4:kb:pairs:block:items:minw:opt
+            rc = L4.lab4_v4(kb, pairs, block, items, v[5], v[6], *args)
         elif kind == "v6":   # v6:kb:pairs:block:items:minw:opt:grid
             rc = L.lab2_v6(kb, pairs, block, items, v[5], v[6], v[7], *args)
         else:
@@ -195,6 +201,20 @@ def main():
             med = statistics.median(ts)
             print(f"emu_handoff {e:16s} median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s "
                   f"err={int(herr[0].item())}", flush=True)
+    if a.emu16:
+        keys, out, _ = bufs[32]
+        for e in a.emu16.split(","):
+            b, it = (int(x) for x in e.split(":"))
+            ts = []
+            for _ in range(a.rounds):
+                e0.record()
+                assert L.lab2_emu16(b, it, 8, P(keys), P(out), ctypes.c_uint32(n), sp) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            med = statistics.median(ts)
+            print(f"emu16 {e:12s} 8 passes median {med:8.4f} ms = {med / 8 * 1e3:7.2f} us per pass  "
+                  f"{n * 8 * 8 / med / 1e6:8.1f} GB/s", flush=True)
     if a.emu_pairs:
         # 2^28-pair C3 shape unless --n says otherwise: SoA (two arrays) vs AoS (one 8-B array)
         npair = n
