@@ -64,7 +64,6 @@ OPTIONS = {
     "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
     "merge": (9, {"rounds": 0, "kway": 1}),
     "fault_tile": (10, {"off": -1}),   # test hook: tile v of every pass never publishes
-    "fold": (11, {"off": 0, "on": 1}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares

@@ -299,7 +299,6 @@ struct grs_sorter {
   int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
-  int fold_mode = 0;               // GRS_OPT_FOLD: 1 = each pass counts the next pass's digit
 };
 
 extern "C" {
@@ -450,10 +449,6 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value < 0 || value > 2) return bad();
       s->sharded_exchange = value;
       break;
-    case GRS_OPT_FOLD:
-      if (value < 0 || value > 1) return bad();
-      s->fold_mode = value;
-      break;
     case GRS_OPT_FAULT_TILE: {
       if (value < -1) return bad();
       // the pass's debug words after the error word (grs_pass.hpp PassDebug): fault tile + 1,
@@ -510,7 +505,6 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_EXCHANGE: *value = s->sharded_exchange; break;
     case GRS_OPT_MERGE: *value = s->merge_mode; break;
     case GRS_OPT_FAULT_TILE: *value = s->fault_tile; break;
-    case GRS_OPT_FOLD: *value = s->fold_mode; break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -631,8 +625,7 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
                        uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
                        uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream,
-                       uint32_t expect_tile = 0, uint32_t hist_rows = 1,
-                       grs::PassFold fold = grs::PassFold{nullptr, 0, 0u}) {
+                       uint32_t expect_tile = 0) {
   const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
   if (status_words_for(tiles, 1u << RB) > s->status_words)
     return set_err(GRS_ECAPACITY, "status buffer too small");
@@ -643,12 +636,12 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
     hipLaunchKernelGGL((grs::grs_onesweep_v6<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(grid), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev, hist_rows, fold);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
   } else {
     hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev, hist_rows, fold);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
   }
   GRS_HIP(hipGetLastError());
   return GRS_OK;
@@ -660,17 +653,16 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_rec(int kind, grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc,
                       uint32_t* vdst, uint32_t n, const grs::RadixDigit<K>& dig,
                       const uint32_t* hist, uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt,
-                      hipStream_t stream, uint32_t expect_tile, uint32_t hist_rows,
-                      grs::PassFold fold) {
+                      hipStream_t stream, uint32_t expect_tile) {
   using Dig = grs::RadixDigit<K>;
   constexpr bool R = sizeof(K) == 4 && PAIRS && RB == 8;
   constexpr uint32_t W = R ? 8192u : 0u, Rd = R ? 4096u : 0u, RS = R ? 16384u : 0u, WS = R ? 32768u : 0u;
   switch (R ? kind : 0) {
-    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, hist_rows, fold);
-    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, hist_rows, fold);
-    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, hist_rows, fold);
-    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, hist_rows, fold);
-    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, hist_rows, fold);
+    case 1: return launch_pass<K, PAIRS, RB, Tile, OPT | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
   }
 }
 
@@ -699,9 +691,6 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   const bool persist = !xl && !Big::TWO_ROUNDS && use_persistent(s, tiles, RB);
   const size_t words = status_words_for(tiles, RADIX);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
-  // histogram fold (GRS_OPT_FOLD, 8-bit digits): the upfront kernel counts pass 0's digit only;
-  // every other pass's digit is counted by the pass before it (grs_pass.hpp PassFold)
-  const bool fold = RB == 8 && s->fold_mode == 1 && passes > 1;
   uint32_t* st0 = s->status;
   uint32_t* st1 = s->status + s->status_words;
   uint32_t* const cb[2] = {s->ctrl, s->ctrl2};
@@ -730,11 +719,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     int grid = n <= (1u << 25) ? s->cus : slots;
     if (grid < need) grid = (need + slots - 1) / slots * slots;
     const bool full = begin_bit == 0 && end_bit == static_cast<int>(8 * sizeof(K));
-    constexpr int QALL = grs::Hist2Layout<K>::MAXQ;
-    auto kern = full ? grs::grs_upfront_hist2<K, RB, true, QALL> : grs::grs_upfront_hist2<K, RB, false, QALL>;
-    if constexpr (RB == 8) {
-      if (fold) kern = full ? grs::grs_upfront_hist2<K, RB, true, 1> : grs::grs_upfront_hist2<K, RB, false, 1>;
-    }
+    auto kern = full ? grs::grs_upfront_hist2<K, RB, true> : grs::grs_upfront_hist2<K, RB, false>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream,
                        src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
                        static_cast<uint32_t>(words), hist_next);
@@ -786,30 +771,21 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     uint32_t* st_nxt = (p & 1) ? st0 : st1;
     const Dig dig{shift, (1u << bits) - 1u};
     const uint32_t* ph = hist + p * GRS_HIST_PASS_STRIDE;
-    // histogram fold: pass p sums the rows pass p - 1 added into, and (but the last) adds the
-    // next pass's counts into that pass's rows
-    const uint32_t hrows = fold && p > 0 ? GRS_FOLD_ROWS : 1u;
-    grs::PassFold pfold{nullptr, 0, 0u};
-    if (fold && p + 1 < passes) {
-      const int nshift = begin_bit + (p + 1) * RB;
-      pfold = grs::PassFold{hist + (p + 1) * GRS_HIST_PASS_STRIDE, nshift,
-                            (1u << std::min(RB, end_bit - nshift)) - 1u};
-    }
     uint32_t* tk = tickets + p * GRS_XCDS;
     if (s->rank_mode != 0) {
-      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold)
-              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold);
+      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile)
+              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile);
     } else if (xl) {
       if constexpr (kXlType)
-        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold);
+        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
-        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold);
+        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else if (big && rec) {
-      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold);
+      r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else {
-      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold)
-              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, hrows, pfold);
+      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile)
+              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile);
     }
     if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;

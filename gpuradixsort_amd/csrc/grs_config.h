@@ -49,15 +49,12 @@
 #define GRS_XCDS 8
 
 // Layout of the per-sorter control block (uint32 words), zeroed once per sort call.
-//   [0, GRS_CTRL_HIST_WORDS)           digit histograms, [pass][row][256]: row 0 holds what the
-//                                      upfront histogram kernel counted; with the histogram
-//                                      fold, pass p - 1's tiles add pass p's digit counts into
-//                                      row (tile % GRS_FOLD_ROWS) and pass p sums the rows
+//   [0, GRS_CTRL_HIST_WORDS)           digit histograms, [pass][256] (the upfront kernel's)
 //   GRS_CTRL_TICKETS + pass * 8        per-pass tile ticket counter
-//   GRS_CTRL_ERROR                     nonzero = a bounded spin timed out
+//   GRS_CTRL_ERROR                     nonzero = a bounded spin timed out; [1], [2] the pass's
+//                                      debug words (grs_pass.hpp PassDebug)
 #define GRS_MAX_PASSES 16               // u64 keys at 4-bit digits
-#define GRS_FOLD_ROWS 16                // rows the fold's atomic adds are spread over
-#define GRS_HIST_PASS_STRIDE (GRS_FOLD_ROWS * 256)
+#define GRS_HIST_PASS_STRIDE 256
 #define GRS_CTRL_HIST_WORDS (GRS_MAX_PASSES * GRS_HIST_PASS_STRIDE)
 #define GRS_CTRL_TICKETS GRS_CTRL_HIST_WORDS
 #define GRS_CTRL_ERROR (GRS_CTRL_TICKETS + GRS_MAX_PASSES * GRS_XCDS)

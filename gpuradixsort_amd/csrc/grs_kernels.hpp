@@ -197,9 +197,8 @@ struct Hist2Layout {
 template <typename K>
 constexpr int kHist2GridShift = sizeof(K) == 4 ? 20 : 19;
 
-// QN: super digits counted (MAXQ, or 1 with the histogram fold, where each pass counts the
-// next pass's digit itself and this kernel only pass 0's).  Pass p's counts go to
-// g_hist[p * GRS_HIST_PASS_STRIDE + d] (row 0 of its rows).
+// QN: super digits counted (MAXQ: every pass's; fewer only in lab measurements).  Pass p's
+// counts go to g_hist[p * GRS_HIST_PASS_STRIDE + d].
 template <typename K, int RB, bool FULL, int QN = Hist2Layout<K>::MAXQ>
 __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,

@@ -66,16 +66,6 @@ struct PassDebug {
   }
 };
 
-// Histogram fold (run_sort, grs_capi.hip): pass p counts every key's digit of pass p + 1 in LDS
-// while it ranks, and adds the tile's counts into row (tile % GRS_FOLD_ROWS) of pass p + 1's
-// histogram rows (fire-and-forget atomics: pass p + 1 reads them after the kernel boundary),
-// so the upfront histogram kernel only counts pass 0's digit.  out == nullptr: no fold.
-struct PassFold {
-  uint32_t* out;       // pass p + 1's rows [GRS_FOLD_ROWS][256], or null
-  int shift;           // the next pass's digit: bits [shift, shift + popcount(mask))
-  uint32_t mask;
-};
-
 // Exclusive prefix of digit d over tiles [0, tile): own group's earlier tiles (< G words)
 // plus the group-level prefix (newest published group INCLUSIVE + complete accumulators
 // after it).  issue() sends the first round of loads, finish() consumes them.
@@ -168,7 +158,7 @@ struct Lb3 {
 };
 
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
-          bool IDX = false, int ROUNDS = 1, bool NEXT = false>
+          bool IDX = false, int ROUNDS = 1>
 struct V4Smem {
   static constexpr int RADIX = 1 << RB;
   static constexpr int WAVES = BLOCK / GRS_WAVE;
@@ -185,12 +175,10 @@ struct V4Smem {
   // indexed digits (partition): tile-local start of every digit, from which the store phase
   // reads off the digit of a reordered position (the key alone does not determine it)
   uint32_t lstart[IDX ? RADIX + 1 : 1];
-  // histogram fold: counts of the NEXT pass's digit over this tile's keys
-  uint32_t nh[NEXT ? RADIX : 1];
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
-                         (OPT & 1024) != 0 ? 2 : 1, !DigitF::kIndexed>;
+                         (OPT & 1024) != 0 ? 2 : 1>;
 
 // OPT bits of the shipped pass (grs_capi.hip picks them per shape):
 //   16   look-back issued after the reorder (default: before it, overlapped with nothing)
@@ -206,17 +194,6 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //   16384 / 32768: the records read / written are SPLIT over two buffers: records [0, n/2)
 //        in keys_in / keys_out and [n/2, n) in vals_in / vals_out (n even; the caller's two
 //        4n-byte arrays hold n records that way)
-
-// Pass total of digit t (t < radix): the sum of its histogram rows (1 row when the upfront
-// kernel counted the digit, GRS_FOLD_ROWS when the previous pass folded it).
-__device__ __forceinline__ uint32_t pass_total(const uint32_t* __restrict__ pass_hist,
-                                               uint32_t rows, uint32_t t, int radix) {
-  uint32_t gh = 0;
-  if (t < static_cast<uint32_t>(radix)) {
-    for (uint32_t r = 0; r < rows; ++r) gh += pass_hist[r * 256u + t];
-  }
-  return gh;
-}
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
@@ -282,14 +259,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
-    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, PassDebug dbg,
-    const PassFold& fold) {
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, PassDebug dbg) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr bool MATCH = (OPT & 512) != 0;
   constexpr bool LATE_LB = (OPT & 16) != 0 || PF;
-  constexpr bool NEXT = !DigitF::kIndexed;   // the fold can run (radix digits)
-  const bool folding = NEXT && fold.out != nullptr;
   constexpr int RADIX = SM::RADIX;
   constexpr int WAVES = SM::WAVES;
   constexpr int TILE = SM::TILE;
@@ -360,9 +334,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       r = atomicAdd(&sm.cnt[w * RADIX + d], 1u);
     }
     if constexpr (IDX) r |= d << 12;
-    if constexpr (NEXT) {
-      if (folding) atomicAdd(&sm.nh[static_cast<uint32_t>(key[j] >> fold.shift) & fold.mask], 1u);
-    }
     if (j & 1)
       rank[j / 2] |= r << 16;
     else
@@ -394,14 +365,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       st_status(status + static_cast<size_t>(tile) * RADIX + t, publish + 1u);
     gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
                                   (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if constexpr (NEXT) {
-      // the fold: this tile's counts of the next pass's digit (padding keys are all-ones, so
-      // they all fall on the largest next digit)
-      if (folding && t <= fold.mask) {
-        const uint32_t c = sm.nh[t] - (t == fold.mask ? pad : 0u);
-        if (c) atomicAdd(fold.out + (tile % GRS_FOLD_ROWS) * 256u + t, c);
-      }
-    }
   }
   if (w < static_cast<uint32_t>(DW)) {
     const uint32_t li = wave_scan_dpp(tile_cnt);
@@ -559,8 +522,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev, uint32_t hist_rows,
-    const PassFold fold) {
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
@@ -570,18 +532,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   uint32_t val[ITEMS];
   if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
-  if constexpr (!DigitF::kIndexed) {
-    for (uint32_t i = t; i < static_cast<uint32_t>(SM::RADIX); i += BLOCK) sm.nh[i] = 0;
-  }
   __syncthreads();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
   tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
-  const uint32_t gh = pass_total(pass_hist, hist_rows, t, SM::RADIX);
+  const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, key, val, keys_in, keys_out, vals_in,
                                                  vals_out, n, dg, gh, ticket, status, status_next,
-                                                 error_word, PassDebug::read(error_word), fold);
+                                                 error_word, PassDebug::read(error_word));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -602,17 +561,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev, uint32_t hist_rows,
-    const PassFold fold) {
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
   if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
-  if constexpr (!DigitF::kIndexed) {
-    for (uint32_t i = t; i < static_cast<uint32_t>(SM::RADIX); i += BLOCK) sm.nh[i] = 0;
-  }
-  const uint32_t gh = pass_total(pass_hist, hist_rows, t, SM::RADIX);
+  const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   const PassDebug dbg = PassDebug::read(error_word);
   __syncthreads();
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
@@ -624,13 +579,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   while (tile < tiles) {
     tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true>(
         sm, tile, key, val, keys_in, keys_out, vals_in, vals_out, n, dg, gh, ticket, status,
-        status_next, error_word, dbg, fold);
+        status_next, error_word, dbg);
     // every LDS read of the finished tile is done before the counters are reset
     lds_barrier();
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
-    if constexpr (!DigitF::kIndexed) {
-      for (uint32_t i = t; i < static_cast<uint32_t>(SM::RADIX); i += BLOCK) sm.nh[i] = 0;
-    }
     lds_barrier();
   }
 }

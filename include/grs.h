@@ -132,10 +132,6 @@ typedef enum grs_option {
   GRS_OPT_MERGE = 9,         /* presorted exchange, receive side: 0 (default) ceil(log2 k)
                                 2-way merge rounds over the k received runs, 1 one k-way merge
                                 pass (sample-delimited tiles merged in LDS; slower at 8 ranks) */
-  GRS_OPT_FOLD = 11,         /* 8-bit digits: 0 the upfront histogram kernel counts every pass's
-                                digit; 1 it counts pass 0's only and each pass counts the next
-                                pass's digit of the keys it ranks (LDS), folding the counts into
-                                the next pass's histogram rows */
   GRS_OPT_FAULT_TILE = 10    /* TEST HOOK: -1 (default) off; v >= 0: tile v of every pass never
                                 publishes its look-back tile words and spins give up after 2^12
                                 polls, so the later tiles of its look-back group time out: the

@@ -10,8 +10,7 @@
 extern "C" {
 
 // one pass of the shipped kernel: kb, pairs, block, items, minw, opt (same arguments as
-// lab2_v4; hist_stride / range_tiles are ignored).  opt bit 64 is lab-only: the histogram fold
-// on, its rows at err + 64 (the kernel's OPT gets opt & ~64)
+// lab2_v4; hist_stride / range_tiles are ignored)
 int lab4_v4(int kb, int pairs, int block, int items, int minw, int opt, const void* in, void* out,
             const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
             uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
@@ -23,16 +22,13 @@ int lab4_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
   case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000000L + O: {             \
     using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                               \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
-    hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, (O & ~64)>), dim3(tiles), dim3(B), \
+    hipLaunchKernelGGL((grs::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
                        0, s, (const KT*)in, (KT*)out, vin, vout, n,                            \
                        grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
-                       (const grs::RadixDigit<KT>*)nullptr, 1u,                                \
-                       grs::PassFold{(O & 64) ? err + 64 : nullptr, shift + 8, 255u});         \
+                       (const grs::RadixDigit<KT>*)nullptr);                                   \
   } break;
-    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 36, 1, 336)
-    V(32, 0, 768, 64, 1, 1040) V(32, 0, 768, 64, 1, 1104)
-    V(64, 0, 768, 44, 1, 1040) V(64, 0, 768, 44, 1, 1104)
-    V(32, 1, 768, 40, 1, 1040) V(32, 1, 768, 40, 1, 1104)
+    V(32, 0, 1024, 36, 1, 272) V(32, 0, 768, 64, 1, 1040) V(64, 0, 768, 44, 1, 1040)
+    V(32, 1, 768, 40, 1, 1040)
 #undef V
     default:
       return -1;
