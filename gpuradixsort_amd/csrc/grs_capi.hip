@@ -1092,17 +1092,22 @@ grs_status grs_copy_u32(const uint32_t* d_src, uint32_t* d_dst, size_t n, void* 
   return GRS_OK;
 }
 
-grs_status grs_gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
-                              size_t record_bytes, void* stream) {
+static grs_status gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
+                                 size_t record_bytes, void* stream, uint32_t idx_max) {
   if (n == 0) return GRS_OK;
   if (!d_src || !d_dst || !d_idx || record_bytes == 0 || record_bytes > 0xFFFFFFFFull)
     return set_err(GRS_EINVAL, "grs_gather_records: bad argument");
   hipLaunchKernelGGL(grs::grs_gather_records, dim3(grid_for(n * ((record_bytes + 3) / 4), 256)),
                      dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), d_idx,
-                     static_cast<uint64_t>(n), static_cast<uint32_t>(record_bytes));
+                     static_cast<uint64_t>(n), static_cast<uint32_t>(record_bytes), idx_max);
   GRS_HIP(hipGetLastError());
   return GRS_OK;
+}
+
+grs_status grs_gather_records(const void* d_src, void* d_dst, const uint32_t* d_idx, size_t n,
+                              size_t record_bytes, void* stream) {
+  return gather_records(d_src, d_dst, d_idx, n, record_bytes, stream, 0xFFFFFFFFu);
 }
 
 grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t seed,
@@ -2220,7 +2225,8 @@ grs_status grs_sort_records_by_keys(grs_sorter* s, void* d_records, size_t n, si
   grs_status r = records_scratch(s, record_bytes, &keys, &idx, &copy, d_keys, d_idx);
   // the caller's keys / indices may live in the scratch (grs_records_key_buffers) or anywhere
   if (r == GRS_OK) r = grs_sort(s, d_keys, d_idx, n, stream);                     // stable pairs
-  if (r == GRS_OK) r = grs_gather_records(d_records, copy, d_idx, n, record_bytes, stream);  // K5
+  if (r == GRS_OK) r = gather_records(d_records, copy, d_idx, n, record_bytes, stream,
+                                      static_cast<uint32_t>(n - 1));  // K5
   if (r == GRS_OK && hipMemcpyAsync(d_records, copy, n * record_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     r = set_err(GRS_EHIP, "grs_sort_records_by_keys: copy back");
   if (prev != s->device) (void)hipSetDevice(prev);
@@ -2263,7 +2269,8 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
     if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_records: launch");
   }
   if (r == GRS_OK) r = grs_sort(s, keys, idx, n, stream);                        // stable pairs
-  if (r == GRS_OK) r = grs_gather_records(d_records, copy, idx, n, record_bytes, stream);  // K5
+  if (r == GRS_OK) r = gather_records(d_records, copy, idx, n, record_bytes, stream,
+                                      static_cast<uint32_t>(n - 1));  // K5
   if (r == GRS_OK && hipMemcpyAsync(d_records, copy, n * record_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     r = set_err(GRS_EHIP, "grs_sort_records: copy back");                          // copy-back
   if (prev != s->device) (void)hipSetDevice(prev);

@@ -447,10 +447,13 @@ __global__ void grs_copy_u32(const uint32_t* __restrict__ src, uint32_t* __restr
     dst[i] = src[i];
 }
 
-// K5 generalised (SortOriginalData.comp:27-51): dst[i] = src[idx[i]] for records of
-// `rb` bytes.  Records that are a multiple of 4 bytes move as dwords.
+// K5 generalised (SortOriginalData.comp:27-51): dst[i] = src[min(idx[i], idx_max)] for records
+// of `rb` bytes.  Records that are a multiple of 4 bytes move as dwords.  idx_max: the records
+// sort passes n - 1, so indices left unwritten by a sort that timed out never read past the
+// records; the public gather passes 0xFFFFFFFF (the caller's indices, unchecked).
 __global__ void grs_gather_records(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                   const uint32_t* __restrict__ idx, uint64_t n, uint32_t rb) {
+                                   const uint32_t* __restrict__ idx, uint64_t n, uint32_t rb,
+                                   uint32_t idx_max) {
   const uint64_t total = n * rb;
   if ((rb & 3u) == 0) {
     const uint32_t wpr = rb >> 2;
@@ -459,13 +462,13 @@ __global__ void grs_gather_records(const uint8_t* __restrict__ src, uint8_t* __r
     for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < n * wpr;
          e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
       const uint64_t r = e / wpr, c = e - r * wpr;
-      d[e] = s[static_cast<uint64_t>(idx[r]) * wpr + c];
+      d[e] = s[static_cast<uint64_t>(min(idx[r], idx_max)) * wpr + c];
     }
   } else {
     for (uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
       const uint64_t r = e / rb, c = e - r * rb;
-      dst[e] = src[static_cast<uint64_t>(idx[r]) * rb + c];
+      dst[e] = src[static_cast<uint64_t>(min(idx[r], idx_max)) * rb + c];
     }
   }
 }
@@ -737,7 +740,8 @@ __global__ void grs_segment_ids(const uint32_t* __restrict__ perm,
   }
 }
 
-// out_keys[j] = keys[pos[j]]; out_vals[j] = vals[perm[pos[j]]] (vals may be null).
+// out_keys[j] = keys[pos[j]]; out_vals[j] = vals[perm[pos[j]]] (vals may be null).  Both
+// indices are clamped to n - 1: after a sort that timed out they may be stale words.
 template <typename K>
 __global__ void grs_segment_gather(const K* __restrict__ keys, K* __restrict__ out_keys,
                                    const uint32_t* __restrict__ pos,
@@ -746,9 +750,10 @@ __global__ void grs_segment_gather(const K* __restrict__ keys, K* __restrict__ o
                                    uint32_t* __restrict__ out_vals, uint64_t n) {
   for (uint64_t j = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; j < n;
        j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint32_t p = pos[j];
+    const uint32_t last = static_cast<uint32_t>(n - 1);
+    const uint32_t p = min(pos[j], last);
     out_keys[j] = keys[p];
-    if (vals) out_vals[j] = vals[perm[p]];
+    if (vals) out_vals[j] = vals[min(perm[p], last)];
   }
 }
 

@@ -98,7 +98,8 @@ struct Lb3 {
   }
   // gold: the value this tile's add to its group accumulator returned; publish: its count.
   // A spin that exceeds `limit` polls sets the error word and counts the word as 0: prefixes
-  // can then only come out SMALLER than the true ones, so every store stays inside [0, n).
+  // can then only come out SMALLER than the true ones (onesweep_tile clamps the runs to
+  // [0, n) for the passes after such a one).
   __device__ __forceinline__ uint32_t finish(const uint32_t* status, const uint32_t* gacc,
                                              uint32_t* ginc, uint32_t tile, uint32_t tiles,
                                              uint32_t d, uint32_t gold, uint32_t publish,
@@ -432,7 +433,15 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   if (t < static_cast<uint32_t>(RADIX)) {
     const uint32_t prefix =
         lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word, dbg.spin_limit);
-    sm.base[t] = gstart + prefix - lstart;
+    uint32_t start = gstart + prefix;
+    if constexpr (!IDX) {
+      // A timed-out look-back only underestimates this pass's prefixes, but the next pass of
+      // the same sort then reads keys whose digits no longer match the upfront histogram, and
+      // a run could pass n.  Keep every run inside [0, n) (a no-op on consistent counts).
+      const uint32_t room = n - publish;
+      start = gstart > room ? room : gstart + min(prefix, room - gstart);
+    }
+    sm.base[t] = start - lstart;
   }
   lds_barrier();  // B4
 

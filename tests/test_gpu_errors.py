@@ -10,6 +10,7 @@ look-back tile words, so the later tiles of its look-back group hit the bound.
 import os
 import subprocess
 
+import numpy as np
 import pytest
 import torch
 
@@ -45,8 +46,6 @@ def _input(gpu, n, key_bits, pairs, seed):
 
 def _expected(k, v):
     """The stable sort of (k, v), computed on the host (numpy: torch cannot index u32)."""
-    import numpy as np
-
     kh = k.cpu().numpy()
     order = np.argsort(kh, kind="stable")
     return kh[order], (v.cpu().numpy()[order] if v is not None else None)
@@ -62,13 +61,35 @@ def test_timeout_surfaces_then_sorter_recovers(gpu, shape):
     n = 1 << 22
     s = grs.RadixSorter(n, key_bits=key_bits, pairs=pairs, radix_bits=rb, options=opts)
     assert s.get_option("fault_tile") == -1
+    # all-ones keys first: the sorter's scratch then holds the largest digit everywhere, so
+    # the slots a timed-out pass leaves unwritten hand the later passes more keys of the last
+    # digit than the upfront histogram counted (runs past n without the pass's clamp)
+    k, v = _input(gpu, n, key_bits, pairs, 10)
+    k.view(torch.int32 if key_bits == 32 else torch.int64).fill_(-1)
+    s.sort(k, v)
+    s.check_error()
     s.set_option("fault_tile", 0)
     assert s.get_option("fault_tile") == 0
-    k, v = _input(gpu, n, key_bits, pairs, 11)
+    # the keys (and values) sit at the front of larger buffers whose tails must stay untouched
+    guard = 1 << 16
+    kbuf = torch.empty(n + guard, dtype=torch.uint32 if key_bits == 32 else torch.uint64,
+                       device=gpu)
+    grs.fill_splitmix(kbuf, 11)
+    ktail = kbuf[n:].clone()
+    k = kbuf[:n]
+    v = vbuf = None
+    if pairs:
+        vbuf = torch.empty(n + guard, dtype=torch.uint32, device=gpu)
+        grs.iota_u32(vbuf)
+        v = vbuf[:n]
     s.sort(k, v)
     with pytest.raises(GrsError) as e:
         s.check_error()
     assert e.value.status == ETIMEOUT
+    assert (kbuf[n:].cpu().numpy() == ktail.cpu().numpy()).all(), "a timed-out sort wrote past n"
+    if pairs:
+        assert (vbuf[n:].cpu().numpy() == np.arange(n, n + guard)).all(), \
+            "a timed-out sort wrote values past n"
     # the error word is sticky until read: the check above cleared it
     s.check_error()
 

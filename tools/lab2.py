@@ -62,7 +62,7 @@ def main():
     vout = torch.empty_like(vin)
     ticket = torch.zeros(64, dtype=torch.uint32, device=dev)   
     max_tiles = n // 4096 + 64
-    err = torch.zeros(64 + 8 * max_tiles + 64, dtype=torch.uint32, device=dev)
+    err = torch.zeros(64 + 12 * max_tiles + 64, dtype=torch.uint32, device=dev)
     err[63] = a.rot
     st = torch.zeros(3 * max_tiles * 256, dtype=torch.uint32, device=dev)
     st2 = torch.zeros_like(st)
@@ -267,7 +267,7 @@ def main():
         run(v)
         torch.cuda.synchronize()
         tiles = (n + v[3] * v[4] - 1) // (v[3] * v[4])
-        a_ = err[64:64 + 8 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 8).astype("float64")
+        a_ = err[64:64 + 12 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 12).astype("float64")
         m = a_[:, :6].mean(0)
         print(f"   ticket known at {a_[:, 6].mean():.0f} cycles (p90 {np.percentile(a_[:, 6], 90):.0f})", flush=True)
         d = np.diff(np.concatenate([[0.0], m]))
@@ -276,6 +276,10 @@ def main():
         print(f"stamps {v}: " + ", ".join(f"{nm}={x:.0f}" for nm, x in zip(names, d))
               + f"  total={m[5]:.0f}  (p90 reorder+lb {np.percentile(a_[:, 4] - a_[:, 3], 90):.0f})",
               flush=True)
+        r_end, lb_end = a_[:, 8], a_[:, 9]
+        print(f"   reorder ends at {r_end.mean():.0f}, look-back (thread 0) at {lb_end.mean():.0f} "
+              f"cycles: look-back wait after the reorder {(lb_end - r_end).mean():.0f} "
+              f"(p90 {np.percentile(lb_end - r_end, 90):.0f})", flush=True)
         starts = a_[:, 7] * 256.0
         span = (starts.max() - starts.min())
         print(f"   tiles={tiles} start spread {span:.0f} cycles", flush=True)

@@ -525,7 +525,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   do {                                                                                     \
     if constexpr ((OPT & 8) != 0) {                                                        \
       if (t == 0)                                                                          \
-        error_word[64 + static_cast<size_t>(tile) * 8 + (k)] =                             \
+        error_word[64 + static_cast<size_t>(tile) * 12 + (k)] =                             \
             static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);                 \
     }                                                                                      \
   } while (0)
@@ -742,6 +742,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         rank[j / 2] = (rank[j / 2] & 0xFFFF0000u) | pos;
     }
   }
+  V4_STAMP(8);   // this wave's reorder issued (stamped by thread 0's wave)
   if constexpr ((OPT & 16) != 0 || PF) {
     if constexpr (WIDE) {
       if (wd < static_cast<uint32_t>(RADIX)) lbw.issue(status, gacc, ginc, tile, wd, wj, g0);
@@ -787,6 +788,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       prefix = lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word);
     }
     sm.base[t] = gstart + roff + prefix - lstart;
+    V4_STAMP(9);   // thread 0's look-back finished
     if constexpr ((OPT & 33554432) != 0) {
       sm.rbeg[t] = gstart + roff + prefix;
       sm.rend[t] = gstart + roff + prefix + publish;
@@ -961,7 +963,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   if constexpr ((OPT & 8) != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     V4_STAMP(5);
-    if (t == 0) error_word[64 + static_cast<size_t>(tile) * 8 + 7] = static_cast<uint32_t>(t_begin >> 8);
+    if (t == 0) error_word[64 + static_cast<size_t>(tile) * 12 + 7] = static_cast<uint32_t>(t_begin >> 8);
   }
 #undef V4_STAMP
   return next;
@@ -1023,7 +1025,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   }
   if constexpr ((OPT & 8) != 0) {
     if (t == 0)
-      error_word[64 + static_cast<size_t>(tile) * 8 + 6] =
+      error_word[64 + static_cast<size_t>(tile) * 12 + 6] =
           static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_begin);
   }
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
