@@ -442,7 +442,7 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       s->sharded_general = value == 1;
       break;
     case GRS_OPT_SHARDED_SEND:
-      if (value < 0 || value > 1) return bad();
+      if (value < 0 || value > 2) return bad();
       s->sharded_send = value;
       break;
     case GRS_OPT_EXCHANGE:

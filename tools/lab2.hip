@@ -311,6 +311,44 @@ __global__ void xcc_probe(uint32_t* out) {
   if (threadIdx.x == 0) out[blockIdx.x] = grs_lab::xcc_id();
 }
 
+
+// Replay of a pass's memory traffic (round 4): the input is PRE-REORDERED (each tile's keys
+// already stably grouped by digit, as the real pass holds them in LDS after its reorder) and
+// table[tile][d] = global destination of tile position 0 of digit d (the real pass's base[]).
+// A workgroup takes a ticket, loads its tile (ITEMS keys per thread, positions k*BLOCK + t)
+// and stores key i to table[d] + i: exactly the real pass's load lines and store addresses,
+// in its store order, without the ranking, reorder or look-back.  Its time is the floor of
+// that access pattern.
+template <int BLOCK, int ITEMS, int RB>
+__global__ __launch_bounds__(BLOCK) void replay_pass(const uint32_t* __restrict__ pre,
+                                                     uint32_t* __restrict__ out,
+                                                     const uint32_t* __restrict__ table, uint32_t n,
+                                                     int shift, uint32_t* __restrict__ ticket) {
+  constexpr int R = 1 << RB;
+  constexpr uint32_t TILE = BLOCK * ITEMS;
+  __shared__ uint32_t tb[R];
+  __shared__ uint32_t tk;
+  if (threadIdx.x == 0) tk = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t tile = tk;
+  for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(R); i += BLOCK)
+    tb[i] = table[static_cast<size_t>(tile) * R + i];
+  const uint32_t base = tile * TILE;
+  const uint32_t valid = min(TILE, n - base);
+  uint32_t key[ITEMS];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * BLOCK + threadIdx.x;
+    key[k] = i < valid ? pre[base + i] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const uint32_t i = k * BLOCK + threadIdx.x;
+    if (i < valid) out[tb[(key[k] >> shift) & (R - 1)] + i] = key[k];
+  }
+}
+
 extern "C" {
 
 int lab2_xcc(uint32_t* out, int blocks, void* stream) {
@@ -534,6 +572,7 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     V(32, 0, 1024, 36, 1, 277086480) V(32, 0, 1024, 36, 1, 277086488) V(32, 0, 768, 64, 1, 277087248)
     V(32, 0, 1024, 36, 1, 8388880) V(32, 0, 1024, 36, 1, 8388888) V(32, 0, 768, 64, 1, 8389648)
     V(32, 0, 768, 64, 1, 8389656)
+    V(32, 0, 1024, 36, 1, 526608) V(32, 0, 1024, 36, 1, 526616)
 #undef V
     default:
       return -1;
@@ -630,4 +669,20 @@ int lab2_stream(int kind, int unroll, int grid, const void* in, void* out, uint6
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+
+// replay of one pass's memory traffic: block, items, radix bits (see replay_pass)
+int lab2_replay(int block, int items, int rb, const uint32_t* pre, uint32_t* out,
+                const uint32_t* table, uint32_t n, int shift, uint32_t* ticket, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t tiles = (n + block * items - 1) / (block * items);
+#define RP(B, I, RB_)                                                                        \
+  if (block == B && items == I && rb == RB_) {                                               \
+    hipLaunchKernelGGL((replay_pass<B, I, RB_>), dim3(tiles), dim3(B), 0, s, pre, out, table, n, \
+                       shift, ticket);                                                       \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                         \
+  }
+  RP(1024, 36, 8) RP(768, 64, 8) RP(1024, 32, 4) RP(1024, 48, 8) RP(1024, 16, 8)
+#undef RP
+  return -1;
+}
 }  // extern "C"

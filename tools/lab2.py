@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--lib4", default="", help="p4 variants from tools/liblab4_LIB4.so")
     ap.add_argument("--emu", default="", help="block:items:mode:lds,... pass memory-pattern emulation")
     ap.add_argument("--emu-handoff", default="", help="block:items:var:lds,... boundary-line hand-off emulation")
+    ap.add_argument("--replay", default="", help="block:items:rb,... the pass's exact loads and stores, no ranking")
     ap.add_argument("--emu16", default="", help="block:items,... C2 memory pattern: 8 passes of 16 runs")
     ap.add_argument("--emu-pairs", default="", help="block:items:aos:lds,... pairs memory pattern (SoA vs AoS)")
     a = ap.parse_args()
@@ -201,6 +202,41 @@ def main():
             med = statistics.median(ts)
             print(f"emu_handoff {e:16s} median {med:8.4f} ms  {n * 8 / med / 1e6:8.1f} GB/s "
                   f"err={int(herr[0].item())}", flush=True)
+    if a.replay:
+        keys, out, _ = bufs[32]
+        k64 = keys.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        for e in a.replay.split(","):
+            b, it, rb = (int(x) for x in e.split(":"))
+            R, T = 1 << rb, b * it
+            tiles = (n + T - 1) // T
+            pos = torch.arange(n, dtype=torch.int64, device=dev)
+            comp = (pos // T) * R + (k64 & (R - 1))
+            srt, perm = torch.sort(comp, stable=True)
+            pre = keys.view(torch.int32)[perm].view(torch.uint32).contiguous()
+            cnt = torch.bincount(comp, minlength=tiles * R).view(tiles, R)
+            lstart = torch.cumsum(cnt, 1) - cnt                       # tile-local digit starts
+            tpre = torch.cumsum(cnt, 0) - cnt                         # earlier tiles, per digit
+            tot = cnt.sum(0)
+            gbase = torch.cumsum(tot, 0) - tot
+            table = (gbase[None, :] + tpre - lstart).to(torch.int32).view(torch.uint32).contiguous()
+            del pos, comp, srt, perm, cnt, lstart, tpre
+            ts = []
+            for _ in range(a.rounds):
+                ticket.zero_()
+                torch.cuda.synchronize()
+                e0.record()
+                assert L.lab2_replay(b, it, rb, P(pre), P(out), P(table), ctypes.c_uint32(n), 0,
+                                     P(ticket), sp) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            ref = torch.sort(k64 & (R - 1), stable=True)[1]
+            ok = torch.equal(out.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, k64[ref])
+            med = statistics.median(ts)
+            print(f"replay {e:12s} median {med:8.4f} ms  min {min(ts):8.4f}  {n * 8 / med / 1e6:8.1f} GB/s "
+                  f"({n * 8 / med / 8e9:.3f} of 8 TB/s)  output {'= one stable digit pass' if ok else 'WRONG'}",
+                  flush=True)
+            del pre, table
     if a.emu16:
         keys, out, _ = bufs[32]
         for e in a.emu16.split(","):
@@ -280,9 +316,40 @@ def main():
         print(f"   reorder ends at {r_end.mean():.0f}, look-back (thread 0) at {lb_end.mean():.0f} "
               f"cycles: look-back wait after the reorder {(lb_end - r_end).mean():.0f} "
               f"(p90 {np.percentile(lb_end - r_end, 90):.0f})", flush=True)
-        starts = a_[:, 7] * 256.0
-        span = (starts.max() - starts.min())
-        print(f"   tiles={tiles} start spread {span:.0f} cycles", flush=True)
+        # per CU: its tiles in start order, and the gap from one tile's drained stores (every
+        # wave) to the next tile's first instruction on the same CU
+        raw = err[64:64 + 12 * tiles].view(torch.int32).cpu().numpy().reshape(tiles, 12)
+        # absolute (s_memtime >> 8) words: unwrap the 32-bit values around their median
+        ref = int(np.median(raw[:, 7].astype(np.uint32)))
+        unwrap = lambda x: ((x.astype(np.uint32).astype(np.int64) - ref + (1 << 31)) % (1 << 32)) - (1 << 31)  # noqa: E731
+        st_ = unwrap(raw[:, 7])
+        en_ = unwrap(raw[:, 10])
+        cu = raw[:, 11].astype(np.uint32)
+        gaps, busy, cus = [], [], 0
+        for c in np.unique(cu):
+            idx = np.where(cu == c)[0]
+            o = idx[np.argsort(st_[idx])]
+            s_, e_ = st_[o], en_[o]
+            cus += 1
+            if len(o) > 1:
+                gaps.extend(((s_[1:] - e_[:-1]) * 256).tolist())
+            busy.append(((e_ - s_).sum(), e_.max() - s_.min()))
+        g = np.array(gaps, dtype=np.float64)
+        b = np.array(busy, dtype=np.float64)
+        print(f"   tiles={tiles} on {cus} CUs; per-CU gap between tiles mean {g.mean():.0f} "
+              f"p50 {np.median(g):.0f} p90 {np.percentile(g, 90):.0f} cycles; CU busy "
+              f"{b[:, 0].sum() / b[:, 1].sum():.3f} of its span; tile mean "
+              f"{(en_ - st_).mean() * 256:.0f}", flush=True)
+        if v[0] in ("v6", "r6"):   # persistent: every workgroup's entry and exit
+            grid = min(tiles, v[7] if v[7] > 0 else 256)
+            wg = err[64 + 12 * tiles:64 + 12 * tiles + 2 * grid].view(torch.int32).cpu().numpy()
+            wg = unwrap(wg).reshape(grid, 2) * 256
+            t0, t1 = wg[:, 0].min(), wg[:, 1].max()
+            print(f"   workgroups: entry spread {wg[:, 0].max() - t0:.0f}, exit spread "
+                  f"{t1 - wg[:, 1].min():.0f}, kernel span {t1 - t0:.0f} cycles; first tile "
+                  f"starts {(st_ * 256).min() - t0:.0f} after the first entry, mean wg "
+                  f"{(wg[:, 1] - wg[:, 0]).mean():.0f} (tiles {b[:, 0].sum() * 256 / cus:.0f} per CU)",
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -802,7 +802,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         sm.jsplit = cstart + ((D + (LTILE - lstart)) - (D & ~63u)) / 64u;
     }
   }
-  if constexpr (PF && ROUNDS == 1 && !PF_LATE && PF_SPLIT && !NOPF) {
+  // OPT 2048 (with PF_SPLIT): the digit waves' share of the prefetch goes behind their stores
+  // instead, so B4 does not wait for its issue
+  if constexpr (PF && ROUNDS == 1 && !PF_LATE && PF_SPLIT && !NOPF && (OPT & 2048) == 0) {
     if (next < tiles && w < static_cast<uint32_t>(DW))
       tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
   }
@@ -955,6 +957,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       }
     }
   }
+  if constexpr (PF && ROUNDS == 1 && !PF_LATE && PF_SPLIT && !NOPF && (OPT & 2048) != 0) {
+    if (next < tiles && w < static_cast<uint32_t>(DW))
+      tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, next, t);
+  }
   if constexpr (PF && NOPF) next = __builtin_amdgcn_readfirstlane(sm.next);
   if constexpr (PF && ROUNDS == 1 && PF_LATE && !NOPF) {   // the next tile's loads behind the stores
     next = __builtin_amdgcn_readfirstlane(sm.next);
@@ -964,6 +970,16 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     V4_STAMP(5);
     if (t == 0) error_word[64 + static_cast<size_t>(tile) * 12 + 7] = static_cast<uint32_t>(t_begin >> 8);
+    // slot 10: every wave's stores drained (absolute, >> 8); slot 11: the CU (XCC, SE, SH, CU)
+    asm volatile("s_barrier" ::: "memory");
+    if (t == 0) {
+      uint32_t hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      error_word[64 + static_cast<size_t>(tile) * 12 + 10] =
+          static_cast<uint32_t>(__builtin_amdgcn_s_memtime() >> 8);
+      error_word[64 + static_cast<size_t>(tile) * 12 + 11] = ((xcc & 0xFu) << 16) | ((hw >> 8) & 0xFFu);
+    }
   }
 #undef V4_STAMP
   return next;
@@ -1061,6 +1077,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   __shared__ SM sm;
   constexpr bool XR = (OPT & 1048576) != 0;
   const uint32_t t = threadIdx.x;
+  const uint64_t t_entry = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
   if (t == 0)
     sm.ticket = XR ? draw_ticket_xr(ticket, (n + SM::TILE - 1) / SM::TILE, range_tiles)
                    : atomicAdd(ticket, 1u);
@@ -1087,6 +1104,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
       if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);
     }
     lds_barrier();
+  }
+  // stamps: this workgroup's entry and exit (absolute, >> 8) after the tiles' 12 words each
+  if constexpr ((OPT & 8) != 0) {
+    if (t == 0) {
+      uint32_t* wg = error_word + 64 + static_cast<size_t>(tiles) * 12 + 2 * blockIdx.x;
+      wg[0] = static_cast<uint32_t>(t_entry >> 8);
+      wg[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() >> 8);
+    }
   }
 }
 
