@@ -1174,11 +1174,14 @@ grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, in
   return GRS_OK;
 }
 
-// Scan scratch: [0] error word (kept for the ABI; reduce-then-scan never spins), [1..3]
-// pad, then one uint32 prefix per 16K-item tile.
-static constexpr size_t kScanTile = GRS_SCAN_BLOCK * GRS_SCAN_ITEMS;
+// Scan scratch: [0] error word (set when a look-back spin gives up), [1] ticket, [2..3] pad,
+// then one 64-bit look-back status word per tile.  Tiles of 8K items below 2^22 items, 32K from
+// there (more tiles in flight at small n, fewer look-backs at large n; tools/ab_scan.py).
+static constexpr size_t kScanTileSmall = (GRS_SCAN_OP_BLOCK / GRS_WAVE) * 8 * 4 * GRS_WAVE;
+static constexpr size_t kScanTileLarge = (GRS_SCAN_OP_BLOCK / GRS_WAVE) * 32 * 4 * GRS_WAVE;
+static constexpr size_t kScanLargeMin = size_t(1) << 22;
 
-size_t grs_scan_scratch_bytes(size_t n) { return 16 + 4 * ((n + kScanTile - 1) / kScanTile); }
+size_t grs_scan_scratch_bytes(size_t n) { return 16 + 8 * ((n + kScanTileSmall - 1) / kScanTileSmall); }
 
 grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
                                   uint32_t* d_total, void* d_scratch, size_t scratch_bytes,
@@ -1195,19 +1198,20 @@ grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t 
     return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: scratch too small");
   if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15u)
     return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: d_in and d_out must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(d_scratch) & 7u)
+    return set_err(GRS_EINVAL, "grs_exclusive_scan_u32: scratch must be 8-byte aligned");
   uint32_t* ctl = static_cast<uint32_t*>(d_scratch);
-  uint32_t* sums = ctl + 4;
-  const uint32_t tiles = static_cast<uint32_t>((n + kScanTile - 1) / kScanTile);
+  const bool large = n >= kScanLargeMin;
+  const size_t tile = large ? kScanTileLarge : kScanTileSmall;
+  const uint32_t tiles = static_cast<uint32_t>((n + tile - 1) / tile);
   const uint32_t n32 = static_cast<uint32_t>(n);
-  GRS_HIP(hipMemsetAsync(ctl, 0, 16, st));
-  hipLaunchKernelGGL(grs::grs_scan_reduce, dim3(tiles), dim3(GRS_SCAN_BLOCK), 0, st, d_in, n32,
-                     sums);
-  GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(grs::grs_scan_spine, dim3(1), dim3(GRS_SCAN_SPINE_BLOCK), 0, st, sums, tiles,
-                     d_total);
-  GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL(grs::grs_scan_downsweep, dim3(tiles), dim3(GRS_SCAN_BLOCK), 0, st, d_in,
-                     d_out, n32, sums);
+  GRS_HIP(hipMemsetAsync(ctl, 0, 16 + 8 * static_cast<size_t>(tiles), st));
+  if (large)
+    hipLaunchKernelGGL(grs::grs_scan_onepass<32>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, st, d_in,
+                       d_out, n32, ctl, d_total);
+  else
+    hipLaunchKernelGGL(grs::grs_scan_onepass<8>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, st, d_in,
+                       d_out, n32, ctl, d_total);
   GRS_HIP(hipGetLastError());
   return GRS_OK;
 }
@@ -1294,6 +1298,49 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_segmented: n exceeds capacity");
   if (n == 0) return GRS_OK;
   if (!d_keys) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL keys");
+  // short segments (the longest <= GRS_SEG_SMALL_MAX): one workgroup per segment in LDS.
+  // Reading the longest length back costs one stream synchronisation; it is skipped where
+  // the average segment already exceeds the bound.
+  if (static_cast<uint64_t>(num_segments) * GRS_SEG_SMALL_MAX >= n) {
+    int prev = 0;
+    GRS_HIP(hipGetDevice(&prev));
+    if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint32_t* dmax = s->ctrl + GRS_CTRL_ERROR + 4;
+    grs_status r = GRS_OK;
+    bool small = false;
+    if (hipMemsetAsync(dmax, 0, 4, st) != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: memset");
+    if (r == GRS_OK) {
+      hipLaunchKernelGGL(grs::grs_segment_maxlen, dim3(std::min<size_t>(grid_for(num_segments, 256), 1024)),
+                         dim3(256), 0, st, d_offsets, static_cast<uint32_t>(num_segments), dmax);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(s->h_err, dmax, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        r = set_err(GRS_EHIP, "grs_sort_segmented: longest segment");
+      else
+        small = *s->h_err <= GRS_SEG_SMALL_MAX;
+    }
+    if (r == GRS_OK && small) {
+      const uint32_t longest = *s->h_err;
+      auto go = [&](auto kt, auto smax) {
+        using KT = decltype(kt);
+        hipLaunchKernelGGL((grs::grs_segment_bitonic<KT, decltype(smax)::value>), dim3(num_segments),
+                           dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
+                           d_offsets);
+      };
+      auto pick = [&](auto kt) {
+        if (longest <= 512) go(kt, std::integral_constant<uint32_t, 512>{});
+        else if (longest <= 1024) go(kt, std::integral_constant<uint32_t, 1024>{});
+        else if (longest <= 2048) go(kt, std::integral_constant<uint32_t, 2048>{});
+        else go(kt, std::integral_constant<uint32_t, GRS_SEG_SMALL_MAX>{});
+      };
+      if (s->key_type == GRS_KEY_U32) pick(uint32_t{});
+      else pick(uint64_t{});
+      if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+    }
+    if (prev != s->device) (void)hipSetDevice(prev);
+    if (r != GRS_OK || small) return r;
+  }
   if (s->key_type == GRS_KEY_U32) return sort_segmented_u32(s, d_keys, d_vals, n, d_offsets,
                                                             num_segments, stream);
   int prev = 0;

@@ -142,6 +142,17 @@ __device__ __forceinline__ void st_status(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Inclusive wave64 scan of a u32 by DPP (row_shr 1/2/4/8, row_bcast 15/31): 6 VALU, no LDS.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 // Workgroup barrier that drains LDS only: __syncthreads() also waits for every outstanding
 // global load (vmcnt(0)), which would drain prefetches that are meant to stay in flight.
 __device__ __forceinline__ void lds_barrier() {
@@ -568,154 +579,244 @@ __global__ void grs_extract_keys(const uint8_t* __restrict__ rec, uint64_t n, ui
 
 // ----------------------------------------------------------------------------------------
 // stand-alone device-wide exclusive scan of uint32 (the reference's K3a + K3b,
-// ParallelPrefixScan.comp:41-196), reduce-then-scan
+// ParallelPrefixScan.comp:41-196).  The reference scans 1024-item groups with a Blelloch tree
+// in shared memory (K3a), then the <= 1024 group totals in one work group (K3b); sums wrap
+// mod 2^32.  Here: one launch.
 // ----------------------------------------------------------------------------------------
 //
-// The reference scans 1024-item groups with a Blelloch tree in shared memory (K3a), then the
-// <= 1024 group totals in one work group (K3b); sums wrap mod 2^32.  Here the groups are
-// 16K-item tiles and there are three launches:
-//   grs_scan_reduce     tile sums (one read of the input)
-//   grs_scan_spine      exclusive scan of the tile sums in one workgroup (+ the total)
-//   grs_scan_downsweep  re-read each tile, scan it, add its tile prefix, write it
-// 12 B of HBM traffic per item.  (Measured against single-pass decoupled look-back variants
-// of 8 B/item, flat and two-level: the look-back chain made those 1.6-2.3x slower, DESIGN.md
-// §3.5.)  In place (in == out) is allowed: only the downsweep writes, a tile after reading it.
-#define GRS_SCAN_BLOCK 512
-#define GRS_SCAN_ITEMS 32
-#define GRS_SCAN_SPINE_BLOCK 1024
+// Single-pass scan (decoupled look-back): one read and one write of the items, 8 B/item.
+// A workgroup takes a ticket (tiles start in id order: a tile only waits on started tiles);
+// each wave scans its own contiguous 4K items row by row (a row = 64 lanes x 4 consecutive
+// items, one 16-byte load per lane: 1 KB per wave-instruction), a DPP wave scan per row plus the
+// running row carry, and keeps the prefixes in registers.  The tile's sum is published as
+// (AGG, sum) in one 64-bit status word, wave 0 looks back (scan_lookback), publishes
+// (INC, prefix + sum), and every wave adds its offset and stores.  Flag and value travel in one
+// word, so no ordering between two stores is needed.  Sums wrap mod 2^32.  In place (in == out)
+// is allowed: a tile writes only its own range, after reading it.  Scratch (ctl): [0] error
+// word, [1] ticket, [2..3] pad, then one 64-bit status word per tile, all zero at the call.
+// Measured at 2^28 (tools/ab_scan.py): 0.445 ms with 32 rows per wave (32K-item tiles), 0.48
+// with 16; an LDS-transposed variant 0.513; the previous reduce-then-scan (three launches, 12 B
+// of traffic per item) 0.61.
+__device__ __forceinline__ unsigned long long ld_status64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-__global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_reduce(const uint32_t* __restrict__ in,
-                                                                 uint32_t n,
-                                                                 uint32_t* __restrict__ tile_sums) {
-  constexpr int B = GRS_SCAN_BLOCK, I = GRS_SCAN_ITEMS, TILE = B * I, W = B / GRS_WAVE;
-  __shared__ uint32_t s_wsum[W];
-  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-  const uint32_t base = blockIdx.x * TILE;
-  uint32_t sum = 0;
-  if (base + TILE <= n) {
-    const uint4* v = reinterpret_cast<const uint4*>(in + base);
+#define GRS_SCAN_OP_BLOCK 256
+
+// One wave's look-back over 64 predecessors per round (lane l reads tile j - l): the nearest
+// published inclusive prefix plus every sum after it, or 64 sums and the next 64.  Returns the
+// exclusive prefix of `tile` (underestimated after a timeout, which sets ctl[0]).  (A window
+// of 4 x 64 per round measured 0.74 against 0.48 ms at 2^28: the steady state finds an
+// inclusive prefix a few tiles back, and the wider rounds only add latency; tools/ab_scan.py.)
+__device__ __forceinline__ uint32_t scan_lookback(const unsigned long long* status, uint32_t tile,
+                                                  uint32_t lane, uint32_t* ctl) {
+  constexpr unsigned long long INC = 2ull << 32;
+  int32_t j = static_cast<int32_t>(tile) - 1;   // newest predecessor not yet summed
+  uint32_t excl = 0, spins = 0;
+  for (;;) {
+    const int32_t idx = j - static_cast<int32_t>(lane);
+    const unsigned long long sw = idx >= 0 ? ld_status64(status + idx) : INC;   // before tile 0: 0
+    const uint32_t flag = static_cast<uint32_t>(sw >> 32), val = static_cast<uint32_t>(sw);
+    const uint64_t incm = __builtin_amdgcn_ballot_w64(flag == 2u);
+    const uint64_t zm = __builtin_amdgcn_ballot_w64(flag == 0u);
+    // lanes 0..first (nearest inclusive, or the whole window) must all be published
+    const uint32_t first = incm ? static_cast<uint32_t>(__builtin_ctzll(incm)) : GRS_WAVE - 1;
+    const uint64_t upto = first == GRS_WAVE - 1 ? ~0ull : (2ull << first) - 1ull;
+    if ((zm & upto) == 0) {
+      uint32_t v = lane <= first ? val : 0u;
 #pragma unroll
-    for (int k = 0; k < I / 4; ++k) {
-      const uint4 x = v[k * B + t];
-      sum += x.x + x.y + x.z + x.w;
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, GRS_WAVE);
+      excl += v;
+      if (incm) return excl;
+      j -= GRS_WAVE;
+      continue;
     }
-  } else {
-    for (uint32_t i = base + t; i < n; i += B) sum += in[i];
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, GRS_WAVE);
-  if (lane == 0) s_wsum[w] = sum;
-  __syncthreads();
-  if (t == 0) {
-    uint32_t tot = 0;
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww) tot += s_wsum[ww];
-    tile_sums[blockIdx.x] = tot;
+    if (++spins > static_cast<uint32_t>(GRS_SPIN_LIMIT)) {   // prefix underestimated
+      if (lane == 0) atomicOr(ctl, 1u);
+      return excl;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
 }
 
-// One workgroup: tile_sums[0..m) -> exclusive prefix in place; *total = sum (nullable).
-__global__ __launch_bounds__(GRS_SCAN_SPINE_BLOCK) void grs_scan_spine(uint32_t* __restrict__ sums,
-                                                                      uint32_t m,
-                                                                      uint32_t* __restrict__ total) {
-  constexpr int B = GRS_SCAN_SPINE_BLOCK, W = B / GRS_WAVE;
-  __shared__ uint32_t s_wsum[W];
-  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < m; base += B) {
-    const uint32_t i = base + t;
-    const uint32_t x = i < m ? sums[i] : 0u;
-    uint32_t incl = x;
-#pragma unroll
-    for (int o = 1; o < GRS_WAVE; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
-      if (lane >= static_cast<uint32_t>(o)) incl += y;
-    }
-    if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, blk = 0;
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww) {
-      const uint32_t ws = s_wsum[ww];
-      if (static_cast<uint32_t>(ww) < w) wbase += ws;
-      blk += ws;
-    }
-    if (i < m) sums[i] = carry + wbase + incl - x;
-    carry += blk;
-    __syncthreads();   // s_wsum is rewritten by the next chunk
-  }
-  if (t == 0 && total != nullptr) *total = carry;
-}
-
-__global__ __launch_bounds__(GRS_SCAN_BLOCK) void grs_scan_downsweep(
+template <int R>
+__global__ __launch_bounds__(GRS_SCAN_OP_BLOCK) void grs_scan_onepass(
     const uint32_t* in, uint32_t* out, uint32_t n,   // may alias (in place)
-    const uint32_t* __restrict__ tile_prefix) {
-  constexpr int B = GRS_SCAN_BLOCK, I = GRS_SCAN_ITEMS, TILE = B * I, W = B / GRS_WAVE;
-  // items pass through LDS with one pad word per 32 (position i -> i + i / 32): the coalesced
-  // stripes (item k*B + t) and the per-thread runs (items t*I .. t*I + I-1) are both
-  // bank-conflict-free
-  __shared__ uint32_t s_tile[TILE + TILE / 32];
+    uint32_t* __restrict__ ctl, uint32_t* __restrict__ total) {
+  constexpr int B = GRS_SCAN_OP_BLOCK, W = B / GRS_WAVE;
+  constexpr uint32_t ROW = 4 * GRS_WAVE, CHUNK = R * ROW, TILE = W * CHUNK;
+  constexpr unsigned long long AGG = 1ull << 32, INC = 2ull << 32;
   __shared__ uint32_t s_wsum[W];
+  __shared__ uint32_t s_tk, s_prefix;
+  unsigned long long* const status = reinterpret_cast<unsigned long long*>(ctl + 4);
   const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-  const uint32_t base = blockIdx.x * TILE;
-  auto pad = [](uint32_t i) { return i + (i >> 5); };
-  const bool full = base + TILE <= n;
-  if (full) {   // 16-byte loads: chunk k*B + t = items 4(k*B + t) .. +3
-    const uint4* v = reinterpret_cast<const uint4*>(in + base);
+  if (t == 0) s_tk = atomicAdd(ctl + 1, 1u);
+  __syncthreads();
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(s_tk);
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  const uint32_t base = tile * TILE;
+  const uint32_t valid = n - base;   // tile-local bound (base + TILE may pass 2^32)
+  const uint32_t wbase = w * CHUNK;  // this wave's first item, tile-local
+  uint4 q[R];
+  if (valid >= TILE) {
+    const uint4* v = reinterpret_cast<const uint4*>(in + base + wbase);
 #pragma unroll
-    for (int k = 0; k < I / 4; ++k) {
-      const uint4 q = v[k * B + t];
-      const uint32_t o = pad(4 * (k * B + t));   // 4 words never straddle a pad
-      s_tile[o] = q.x;
-      s_tile[o + 1] = q.y;
-      s_tile[o + 2] = q.z;
-      s_tile[o + 3] = q.w;
-    }
+    for (int r = 0; r < R; ++r) q[r] = v[r * GRS_WAVE + lane];
   } else {
 #pragma unroll
-    for (int k = 0; k < I; ++k) {
-      const uint32_t i = base + k * B + t;
-      s_tile[pad(k * B + t)] = i < n ? in[i] : 0u;
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = wbase + r * ROW + 4 * lane;
+      const uint32_t* p = in + base + i;
+      q[r].x = i < valid ? p[0] : 0u;
+      q[r].y = i + 1 < valid ? p[1] : 0u;
+      q[r].z = i + 2 < valid ? p[2] : 0u;
+      q[r].w = i + 3 < valid ? p[3] : 0u;
+    }
+  }
+  // rows -> exclusive prefixes within the wave's chunk, in place
+  uint32_t carry = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t a = q[r].x, b = a + q[r].y, c = b + q[r].z, d = c + q[r].w;
+    const uint32_t incl = wave_scan_dpp(d);
+    const uint32_t e = carry + incl - d;
+    q[r] = make_uint4(e, e + a, e + b, e + c);
+    carry += __builtin_amdgcn_readlane(incl, GRS_WAVE - 1);
+  }
+  if (lane == 0) s_wsum[w] = carry;
+  __syncthreads();
+  uint32_t agg = 0, wpre = 0;
+#pragma unroll
+  for (int ww = 0; ww < W; ++ww) {
+    const uint32_t ws = s_wsum[ww];
+    wpre += static_cast<uint32_t>(ww) < w ? ws : 0u;
+    agg += ws;
+  }
+  if (w == 0) {
+    uint32_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0) st_status64(status, INC | agg);
+    } else {
+      if (lane == 0) st_status64(status + tile, AGG | agg);
+      excl = scan_lookback(status, tile, lane, ctl);
+      if (lane == 0) st_status64(status + tile, INC | static_cast<unsigned long long>(excl + agg));
+    }
+    if (lane == 0) {
+      s_prefix = excl;
+      if (tile == tiles - 1 && total != nullptr) *total = excl + agg;
     }
   }
   __syncthreads();
-  uint32_t x[I], sum = 0;
+  const uint32_t off = s_prefix + wpre;
+  if (valid >= TILE) {
+    uint4* v = reinterpret_cast<uint4*>(out + base + wbase);
 #pragma unroll
-  for (int k = 0; k < I; ++k) {
-    x[k] = s_tile[pad(t * I + k)];
-    sum += x[k];
-  }
-  uint32_t incl = sum;
-#pragma unroll
-  for (int o = 1; o < GRS_WAVE; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, GRS_WAVE);
-    if (lane >= static_cast<uint32_t>(o)) incl += y;
-  }
-  if (lane == GRS_WAVE - 1) s_wsum[w] = incl;
-  __syncthreads();   // also: every thread's reads of s_tile are done
-  uint32_t run = tile_prefix[blockIdx.x] + incl - sum;
-#pragma unroll
-  for (int ww = 0; ww < W; ++ww)
-    if (static_cast<uint32_t>(ww) < w) run += s_wsum[ww];
-#pragma unroll
-  for (int k = 0; k < I; ++k) {
-    const uint32_t xi = x[k];
-    s_tile[pad(t * I + k)] = run;
-    run += xi;
-  }
-  __syncthreads();
-  if (full) {
-    uint4* v = reinterpret_cast<uint4*>(out + base);
-#pragma unroll
-    for (int k = 0; k < I / 4; ++k) {
-      const uint32_t o = pad(4 * (k * B + t));
-      v[k * B + t] = make_uint4(s_tile[o], s_tile[o + 1], s_tile[o + 2], s_tile[o + 3]);
-    }
+    for (int r = 0; r < R; ++r)
+      v[r * GRS_WAVE + lane] = make_uint4(q[r].x + off, q[r].y + off, q[r].z + off, q[r].w + off);
   } else {
 #pragma unroll
-    for (int k = 0; k < I; ++k) {
-      const uint32_t i = base + k * B + t;
-      if (i < n) out[i] = s_tile[pad(k * B + t)];
+    for (int r = 0; r < R; ++r) {
+      const uint32_t i = wbase + r * ROW + 4 * lane;
+      uint32_t* p = out + base + i;
+      if (i < valid) p[0] = q[r].x + off;
+      if (i + 1 < valid) p[1] = q[r].y + off;
+      if (i + 2 < valid) p[2] = q[r].z + off;
+      if (i + 3 < valid) p[3] = q[r].w + off;
+    }
+  }
+}
+
+// Segmented sort of short segments: one workgroup per segment sorts it
+// in LDS -- one read and one write of the keys (and payload) instead of the two radix sorts
+// and the gather of the general path.  A bitonic network over (key, position in the segment),
+// so equal keys keep their input order; the payload follows through the position.  Segments
+// of at most GRS_SEG_SMALL_MAX items (the host checks the longest first).
+#define GRS_SEG_SMALL_MAX 4096
+#define GRS_SEG_SMALL_BLOCK 256
+
+// The longest segment's length -> *out (atomicMax; *out zeroed by the caller).
+__global__ void grs_segment_maxlen(const uint32_t* __restrict__ offsets, uint32_t nseg,
+                                   uint32_t* __restrict__ out) {
+  uint32_t m = 0;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x)
+    m = max(m, offsets[s + 1] - offsets[s]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(m, o, GRS_WAVE)));
+  if ((threadIdx.x & (GRS_WAVE - 1)) == 0 && m != 0) atomicMax(out, m);
+}
+
+// SMAX: the LDS arrays' size (a power of two >= the longest segment, chosen by the host):
+// shorter segments leave room for more workgroups per CU.
+template <typename K, uint32_t SMAX>
+__global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_bitonic(
+    K* __restrict__ keys, uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets) {
+  static_assert(SMAX <= GRS_SEG_SMALL_MAX && (SMAX & (SMAX - 1)) == 0, "power-of-two bound");
+  constexpr uint32_t B = GRS_SEG_SMALL_BLOCK;
+  constexpr bool U64 = sizeof(K) == 8;
+  // u32 keys: (key << 32) | position, one 64-bit compare; u64 keys: key, then position
+  __shared__ uint64_t sk[SMAX];
+  __shared__ uint32_t si[U64 ? SMAX : 1];
+  __shared__ uint32_t sv[SMAX];
+  const uint32_t t = threadIdx.x;
+  const uint32_t lo = offsets[blockIdx.x];
+  const uint32_t len = offsets[blockIdx.x + 1] - lo;
+  if (len <= 1 || len > SMAX) return;   // (longer segments never reach this kernel)
+  uint32_t p = 2;
+  while (p < len) p <<= 1;
+  for (uint32_t i = t; i < p; i += B) {
+    if (i < len) {
+      const K k = keys[lo + i];
+      if constexpr (U64) {
+        sk[i] = k;
+        si[i] = i;
+      } else {
+        sk[i] = (static_cast<uint64_t>(k) << 32) | i;
+      }
+      if (vals != nullptr) sv[i] = vals[lo + i];
+    } else {   // padding sorts after every item
+      sk[i] = ~0ull;
+      if constexpr (U64) si[i] = ~0u;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= p; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = t; i < p / 2; i += B) {
+        const uint32_t a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), b = a + j;
+        const bool up = (a & k) == 0;
+        const uint64_t x = sk[a], y = sk[b];
+        bool gt;
+        uint32_t xi = 0, yi = 0;
+        if constexpr (U64) {
+          xi = si[a];
+          yi = si[b];
+          gt = x > y || (x == y && xi > yi);
+        } else {
+          gt = x > y;
+        }
+        if (gt == up) {
+          sk[a] = y;
+          sk[b] = x;
+          if constexpr (U64) {
+            si[a] = yi;
+            si[b] = xi;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = t; i < len; i += B) {
+    const uint64_t x = sk[i];
+    if constexpr (U64) {
+      keys[lo + i] = static_cast<K>(x);
+      if (vals != nullptr) vals[lo + i] = sv[si[i]];
+    } else {
+      keys[lo + i] = static_cast<K>(x >> 32);
+      if (vals != nullptr) vals[lo + i] = sv[static_cast<uint32_t>(x)];
     }
   }
 }

@@ -32,17 +32,6 @@
 
 namespace grs {
 
-// Inclusive wave64 scan of a u32 by DPP (row_shr 1/2/4/8, row_bcast 15/31): 6 VALU, no LDS.
-__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return v;
-}
-
 // Look-back status of one pass (uint32 words, all zero at pass start):
 //   tile words   [tiles][R]   count + 1 of the tile's digit (0 = not published yet)
 //   group accs   [groups][R]  (arrivals << 24) | sum of the group's tile counts

@@ -381,10 +381,12 @@ grs_status grs_sort_records_by_keys(grs_sorter* s, void* d_records, size_t n, si
                                     void* d_keys, uint32_t* d_idx, void* stream);
 
 /* Stand-alone device-wide exclusive prefix sum of uint32 (sums wrap mod 2^32), the
- * reference's K3a + K3b (ParallelPrefixScan.comp:41-196, ParallelSort.cpp:253-274) as one
- * reduce-then-scan (three launches).  d_out may equal d_in; both 16-byte aligned.  d_total (nullable) receives the sum of all
- * items (the reference's totalNumberOfOnes, PrefixScanBuffer.comp:37).  Scratch: device
- * memory of grs_scan_scratch_bytes(n) bytes, owned by the caller, one call at a time. */
+ * reference's K3a + K3b (ParallelPrefixScan.comp:41-196, ParallelSort.cpp:253-274) in one
+ * pass with a decoupled look-back (8 B of HBM traffic per item).  d_out may equal d_in; both
+ * 16-byte aligned.
+ * d_total (nullable) receives the sum of all items (the reference's totalNumberOfOnes,
+ * PrefixScanBuffer.comp:37).  Scratch: device memory of grs_scan_scratch_bytes(n) bytes,
+ * 8-byte aligned, owned by the caller, one call at a time. */
 #define GRS_SCAN_MAX_N 0xFFFFF000u
 size_t grs_scan_scratch_bytes(size_t n);
 grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
@@ -396,8 +398,11 @@ grs_status grs_scan_check_error(const void* d_scratch, void* stream);
 /* Segmented (batched) stable sort: every segment [off[s], off[s+1]) of d_keys[0..n) is
  * sorted on its own, with d_vals (nullable) permuted alike; d_offsets: num_segments + 1
  * non-decreasing DEVICE words, off[0] = 0, off[num_segments] = n.  Needs a sorter created
- * with a payload (it carries the input index); two sorts (keys, then segment ids) and one
- * gather; scratch of 12 + key-size bytes per item is allocated on first use and kept. */
+ * with a payload.  Where no segment is longer than 4096 items, one workgroup per segment
+ * sorts it in LDS (one read and one write of the data); finding the longest segment costs one
+ * synchronisation of `stream` (skipped when n / num_segments > 4096).  Otherwise two sorts
+ * (keys, then segment ids; for u32 keys one sort of (segment, key)) and a gather; scratch of
+ * 12 + key-size bytes per item is allocated on first use and kept. */
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
                               const uint32_t* d_offsets, int num_segments, void* stream);
 

@@ -147,7 +147,7 @@ def random_offsets(n, nseg, rng, empty=True):
 
 @pytest.mark.parametrize("kb", [32, 64])
 @pytest.mark.parametrize("n,nseg", [(1, 1), (1000, 1), (100_003, 7), (300_000, 4096),
-                                    (1 << 20, 100_000)])
+                                    (1 << 20, 100_000), (300_000, 200)])
 def test_segmented_sort(gpu, kb, n, nseg):
     import gpuradixsort_amd as grs
 
@@ -171,6 +171,34 @@ def test_segmented_sort(gpu, kb, n, nseg):
     s.sort_segmented(k2, o)
     torch.cuda.synchronize()
     assert np.array_equal(k2.cpu().numpy().view(dt), want_k)
+    s.close()
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+@pytest.mark.parametrize("lengths", [[4096] * 5, [4095, 1, 2, 3, 4096, 0, 17], [4096, 4097, 5]],
+                         ids=["all_4096", "ragged", "one_4097"])
+def test_segmented_sort_short_segment_bound(gpu, kb, lengths):
+    """Segments at the LDS path's bound (4096 items: a full bitonic network), ragged and empty
+    ones, and one item past the bound (the general path takes the whole call)."""
+    import gpuradixsort_amd as grs
+
+    rng = np.random.default_rng(sum(lengths) + kb)
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.uint32)
+    n = int(off[-1])
+    dt = np.uint32 if kb == 32 else np.uint64
+    keys = rng.integers(0, 64, n, dtype=dt)              # heavy ties
+    keys[::5] = np.iinfo(dt).max                         # the largest key beside the padding
+    vals = np.arange(n, dtype=np.uint32)
+    want_k, want_v = oracle.segmented_sort_np(keys, off, vals)
+    s = grs.RadixSorter(n, key_bits=kb, pairs=True)
+    k = torch.from_numpy(keys.view(np.int32 if kb == 32 else np.int64).copy()).to(gpu)
+    v = torch.from_numpy(vals.view(np.int32).copy()).to(gpu)
+    o = torch.from_numpy(off.view(np.int32)).to(gpu)
+    s.sort_segmented(k, o, v)
+    torch.cuda.synchronize()
+    s.check_error()
+    assert np.array_equal(k.cpu().numpy().view(dt), want_k)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), want_v)
     s.close()
 
 

@@ -319,7 +319,7 @@ __global__ void xcc_probe(uint32_t* out) {
 // and stores key i to table[d] + i: exactly the real pass's load lines and store addresses,
 // in its store order, without the ranking, reorder or look-back.  Its time is the floor of
 // that access pattern.
-template <int BLOCK, int ITEMS, int RB>
+template <int BLOCK, int ITEMS, int RB, bool X8>
 __global__ __launch_bounds__(BLOCK) void replay_pass(const uint32_t* __restrict__ pre,
                                                      uint32_t* __restrict__ out,
                                                      const uint32_t* __restrict__ table, uint32_t n,
@@ -328,7 +328,8 @@ __global__ __launch_bounds__(BLOCK) void replay_pass(const uint32_t* __restrict_
   constexpr uint32_t TILE = BLOCK * ITEMS;
   __shared__ uint32_t tb[R];
   __shared__ uint32_t tk;
-  if (threadIdx.x == 0) tk = atomicAdd(ticket, 1u);
+  if (threadIdx.x == 0)
+    tk = X8 ? grs_lab::draw_ticket_x8(ticket, (n + TILE - 1) / TILE) : atomicAdd(ticket, 1u);
   __syncthreads();
   const uint32_t tile = tk;
   for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(R); i += BLOCK)
@@ -533,6 +534,8 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 1024, 36, 1, 16777488) V(32, 0, 1024, 36, 1, 33554704) V(32, 0, 768, 64, 1, 16778256)
     V(32, 0, 768, 64, 1, 33555472) V(32, 1, 768, 40, 1, 16778256) V(32, 1, 768, 40, 1, 33555472)
     V(64, 0, 768, 44, 1, 16778256) V(64, 0, 768, 44, 1, 33555472)
+    V(32, 0, 1024, 36, 1, 134217984 + 16) V(32, 0, 1024, 36, 1, 134217984 + 24)
+    V(32, 0, 768, 64, 1, 134217728 + 1040) V(32, 0, 768, 64, 1, 134217728 + 1048)
     V(32, 0, 1024, 36, 1, 4194576) V(32, 0, 1024, 36, 1, 4194584) V(32, 0, 768, 64, 1, 4195344)
     V(32, 0, 768, 64, 1, 4195352) V(32, 1, 768, 40, 1, 4195344) V(64, 0, 768, 44, 1, 4195344)
 #undef V
@@ -602,6 +605,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
     V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
     V(1024, 32, 1, 524288) V(1024, 32, 1, 524296) V(512, 32, 2, 524288) V(512, 32, 2, 8)
     V(1024, 32, 1, 64) V(1024, 32, 1, 72) V(1024, 32, 1, 16777216) V(1024, 32, 1, 33554432)
+    V(1024, 32, 1, 134217728) V(1024, 32, 1, 134217736)
     V(1024, 32, 1, 67108864) V(1024, 32, 1, 67108872) V(1024, 32, 1, 67108880)
 #undef V
     default:
@@ -671,18 +675,40 @@ int lab2_stream(int kind, int unroll, int grid, const void* in, void* out, uint6
 
 
 // replay of one pass's memory traffic: block, items, radix bits (see replay_pass)
-int lab2_replay(int block, int items, int rb, const uint32_t* pre, uint32_t* out,
+int lab2_replay(int block, int items, int rb, int x8, const uint32_t* pre, uint32_t* out,
                 const uint32_t* table, uint32_t n, int shift, uint32_t* ticket, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint32_t tiles = (n + block * items - 1) / (block * items);
 #define RP(B, I, RB_)                                                                        \
   if (block == B && items == I && rb == RB_) {                                               \
-    hipLaunchKernelGGL((replay_pass<B, I, RB_>), dim3(tiles), dim3(B), 0, s, pre, out, table, n, \
-                       shift, ticket);                                                       \
+    if (x8)                                                                                  \
+      hipLaunchKernelGGL((replay_pass<B, I, RB_, true>), dim3(tiles), dim3(B), 0, s, pre, out, \
+                         table, n, shift, ticket);                                           \
+    else                                                                                     \
+      hipLaunchKernelGGL((replay_pass<B, I, RB_, false>), dim3(tiles), dim3(B), 0, s, pre, out, \
+                         table, n, shift, ticket);                                           \
     return hipGetLastError() == hipSuccess ? 0 : -2;                                         \
   }
   RP(1024, 36, 8) RP(768, 64, 8) RP(1024, 32, 4) RP(1024, 48, 8) RP(1024, 16, 8)
 #undef RP
   return -1;
+}
+
+// single-pass scan (grs_scan_onepass<rows>) beside the library's scan (tools/ab_scan.py)
+int lab2_scan2(int rows, const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* ctl,
+               uint32_t* total, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t TILE = GRS_SCAN_OP_BLOCK / 64 * rows * 256;
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  if (hipMemsetAsync(ctl, 0, 16 + 8 * static_cast<size_t>(tiles), s) != hipSuccess) return -2;
+  if (rows == 16)
+    hipLaunchKernelGGL(grs::grs_scan_onepass<16>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total);
+  else if (rows == 8)
+    hipLaunchKernelGGL(grs::grs_scan_onepass<8>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total);
+  else if (rows == 32)
+    hipLaunchKernelGGL(grs::grs_scan_onepass<32>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total);
+  else
+    return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 }  // extern "C"

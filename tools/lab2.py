@@ -206,7 +206,9 @@ def main():
         keys, out, _ = bufs[32]
         k64 = keys.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
         for e in a.replay.split(","):
-            b, it, rb = (int(x) for x in e.split(":"))
+            f = [int(x) for x in e.split(":")]
+            b, it, rb = f[:3]
+            x8 = f[3] if len(f) > 3 else 0
             R, T = 1 << rb, b * it
             tiles = (n + T - 1) // T
             pos = torch.arange(n, dtype=torch.int64, device=dev)
@@ -225,7 +227,7 @@ def main():
                 ticket.zero_()
                 torch.cuda.synchronize()
                 e0.record()
-                assert L.lab2_replay(b, it, rb, P(pre), P(out), P(table), ctypes.c_uint32(n), 0,
+                assert L.lab2_replay(b, it, rb, x8, P(pre), P(out), P(table), ctypes.c_uint32(n), 0,
                                      P(ticket), sp) == 0
                 e1.record()
                 torch.cuda.synchronize()
