@@ -748,75 +748,120 @@ __global__ void grs_segment_maxlen(const uint32_t* __restrict__ offsets, uint32_
   if ((threadIdx.x & (GRS_WAVE - 1)) == 0 && m != 0) atomicMax(out, m);
 }
 
-// SMAX: the LDS arrays' size (a power of two >= the longest segment, chosen by the host):
-// shorter segments leave room for more workgroups per CU.
+// SMAX: a power of two >= the longest segment, chosen by the host (shorter bounds leave room
+// for more workgroups per CU).  Thread t holds positions t*E .. t*E + E - 1 (E = SMAX / 256) in
+// registers; a compare-exchange at distance j runs in registers (j < E), across the wave by
+// lane shuffles (j < 64 E), and through LDS with one barrier only beyond that (3 of 55 stages
+// at 1024 items).  Padding positions hold the largest (key, position) and sort last.
 template <typename K, uint32_t SMAX>
 __global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_bitonic(
     K* __restrict__ keys, uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets) {
-  static_assert(SMAX <= GRS_SEG_SMALL_MAX && (SMAX & (SMAX - 1)) == 0, "power-of-two bound");
   constexpr uint32_t B = GRS_SEG_SMALL_BLOCK;
+  static_assert(SMAX <= GRS_SEG_SMALL_MAX && SMAX >= 2 * B && (SMAX & (SMAX - 1)) == 0,
+                "power-of-two bound of at least two items per thread");
+  constexpr uint32_t E = SMAX / B;
   constexpr bool U64 = sizeof(K) == 8;
-  // u32 keys: (key << 32) | position, one 64-bit compare; u64 keys: key, then position
-  __shared__ uint64_t sk[SMAX];
-  __shared__ uint32_t si[U64 ? SMAX : 1];
-  __shared__ uint32_t sv[SMAX];
+  __shared__ uint64_t xk[2][SMAX];                       // cross-wave exchange, double-buffered
+  __shared__ uint32_t xi[U64 ? 2 : 1][U64 ? SMAX : 1];   // u64 keys: their positions
+  __shared__ uint32_t sv[SMAX];                          // the payload, by input position
   const uint32_t t = threadIdx.x;
   const uint32_t lo = offsets[blockIdx.x];
   const uint32_t len = offsets[blockIdx.x + 1] - lo;
   if (len <= 1 || len > SMAX) return;   // (longer segments never reach this kernel)
   uint32_t p = 2;
   while (p < len) p <<= 1;
-  for (uint32_t i = t; i < p; i += B) {
-    if (i < len) {
-      const K k = keys[lo + i];
-      if constexpr (U64) {
-        sk[i] = k;
-        si[i] = i;
-      } else {
-        sk[i] = (static_cast<uint64_t>(k) << 32) | i;
-      }
-      if (vals != nullptr) sv[i] = vals[lo + i];
-    } else {   // padding sorts after every item
-      sk[i] = ~0ull;
-      if constexpr (U64) si[i] = ~0u;
+  // u32 keys: x = (key << 32) | position (one 64-bit order); u64 keys: x = key, ix = position
+  uint64_t x[E];
+  uint32_t ix[E];
+#pragma unroll
+  for (uint32_t e = 0; e < E; ++e) {
+    const uint32_t a = t * E + e;
+    if (a < len) {
+      const K kk = keys[lo + a];
+      x[e] = U64 ? static_cast<uint64_t>(kk) : (static_cast<uint64_t>(kk) << 32) | a;
+      ix[e] = a;
+      if (vals != nullptr) sv[a] = vals[lo + a];
+    } else {
+      x[e] = ~0ull;
+      ix[e] = ~0u;
     }
   }
-  __syncthreads();
+  // (x, ix) > (y, iy) in the sort order
+  auto greater = [](uint64_t xa, uint32_t ia, uint64_t xb, uint32_t ib) {
+    if constexpr (U64) return xa > xb || (xa == xb && ia > ib);
+    else return xa > xb;
+  };
+  uint32_t buf = 0;
   for (uint32_t k = 2; k <= p; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = t; i < p / 2; i += B) {
-        const uint32_t a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), b = a + j;
-        const bool up = (a & k) == 0;
-        const uint64_t x = sk[a], y = sk[b];
-        bool gt;
-        uint32_t xi = 0, yi = 0;
-        if constexpr (U64) {
-          xi = si[a];
-          yi = si[b];
-          gt = x > y || (x == y && xi > yi);
-        } else {
-          gt = x > y;
+      if (j < E) {   // both positions in this thread's registers
+#pragma unroll
+        for (uint32_t e = 0; e < E; ++e) {
+          const uint32_t f = e | j;
+          if ((e & j) == 0 && f < E) {
+            const bool up = ((t * E + e) & k) == 0;
+            if (greater(x[e], ix[e], x[f], ix[f]) == up) {
+              const uint64_t tx = x[e];
+              x[e] = x[f];
+              x[f] = tx;
+              const uint32_t ti = ix[e];
+              ix[e] = ix[f];
+              ix[f] = ti;
+            }
+          }
         }
-        if (gt == up) {
-          sk[a] = y;
-          sk[b] = x;
-          if constexpr (U64) {
-            si[a] = yi;
-            si[b] = xi;
+      } else {
+        uint64_t y[E];
+        uint32_t iy[E];
+        if (j < GRS_WAVE * E) {   // the partner is lane (lane ^ j / E) of this wave
+          const int m = static_cast<int>(j / E);
+#pragma unroll
+          for (uint32_t e = 0; e < E; ++e) {
+            const uint32_t ylo = __shfl_xor(static_cast<uint32_t>(x[e]), m, GRS_WAVE);
+            const uint32_t yhi = __shfl_xor(static_cast<uint32_t>(x[e] >> 32), m, GRS_WAVE);
+            y[e] = (static_cast<uint64_t>(yhi) << 32) | ylo;
+            iy[e] = U64 ? static_cast<uint32_t>(__shfl_xor(ix[e], m, GRS_WAVE)) : 0u;
+          }
+        } else {   // another wave's: through LDS
+#pragma unroll
+          for (uint32_t e = 0; e < E; ++e) {
+            xk[buf][t * E + e] = x[e];
+            if constexpr (U64) xi[buf][t * E + e] = ix[e];
+          }
+          __syncthreads();
+#pragma unroll
+          for (uint32_t e = 0; e < E; ++e) {
+            y[e] = xk[buf][(t * E + e) ^ j];
+            if constexpr (U64) iy[e] = xi[buf][(t * E + e) ^ j];
+            else iy[e] = 0u;
+          }
+          buf ^= 1u;   // the next LDS stage writes the other buffer (a barrier lies between)
+        }
+#pragma unroll
+        for (uint32_t e = 0; e < E; ++e) {
+          const uint32_t a = t * E + e;
+          const bool up = (a & k) == 0, lower = (a & j) == 0;
+          // the lower position of an ascending pair keeps the smaller item, and so on
+          if (greater(x[e], ix[e], y[e], iy[e]) == (lower == up)) {
+            x[e] = y[e];
+            ix[e] = iy[e];
           }
         }
       }
-      __syncthreads();
     }
   }
-  for (uint32_t i = t; i < len; i += B) {
-    const uint64_t x = sk[i];
-    if constexpr (U64) {
-      keys[lo + i] = static_cast<K>(x);
-      if (vals != nullptr) vals[lo + i] = sv[si[i]];
-    } else {
-      keys[lo + i] = static_cast<K>(x >> 32);
-      if (vals != nullptr) vals[lo + i] = sv[static_cast<uint32_t>(x)];
+  __syncthreads();   // the payload rows (sv) are read across threads below
+#pragma unroll
+  for (uint32_t e = 0; e < E; ++e) {
+    const uint32_t a = t * E + e;
+    if (a < len) {
+      if constexpr (U64) {
+        keys[lo + a] = static_cast<K>(x[e]);
+        if (vals != nullptr) vals[lo + a] = sv[ix[e]];
+      } else {
+        keys[lo + a] = static_cast<K>(x[e] >> 32);
+        if (vals != nullptr) vals[lo + a] = sv[static_cast<uint32_t>(x[e])];
+      }
     }
   }
 }

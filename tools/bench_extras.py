@@ -41,7 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 28)
     ap.add_argument("--reps", type=int, default=10)
-    a = ap.parse_args()
+    a, _ = ap.parse_known_args()
     dev = torch.device("cuda", 0)
     n = a.n
     L = grs.lib()
@@ -91,18 +91,18 @@ def main():
                       "note": "restore copy of the keys subtracted"}), flush=True)
 
 
-def partition(n, g=8):
+def partition(n, g=8, options=None):
     """grs_partition (the multi-GPU exchange's local step): 2^27 u32 keys into g buckets by
     g - 1 splitters at uniform quantiles; 8 B/key algorithmic (read + write)."""
     dev = torch.device("cuda", 0)
-    s = grs.RadixSorter(n, key_bits=32)
+    s = grs.RadixSorter(n, key_bits=32, options=options or {})
     k = torch.empty(n, dtype=torch.int32, device=dev)
     grs.fill_splitmix(k, 4)
     out = torch.empty_like(k)
     counts = torch.zeros(16, dtype=torch.int32, device=dev)
     sp = [(i * (1 << 32)) // g for i in range(1, g)]
     ms = timed(lambda: s.partition(k, out, sp, counts), 10)
-    print(json.dumps({"op": f"partition_u32_{g}_buckets", "n": n, "ms": round(ms, 4),
+    print(json.dumps({"op": f"partition_u32_{g}_buckets", "options": options or {}, "n": n, "ms": round(ms, 4),
                       "GB/s": round(n * 8 / ms / 1e6, 1), "frac": round(n * 8 / ms / 1e6 / PEAK, 4),
                       "note": "histogram + one onesweep pass with a splitter digit"}), flush=True)
 
@@ -130,4 +130,8 @@ def host_sort(n):
 if __name__ == "__main__":
     main()
     partition(1 << 27)
+    if "--partition-ab" in sys.argv:
+        partition(1 << 27, options={"rank": "match"})
+        partition(1 << 27, g=4)
+        partition(1 << 27, g=4, options={"rank": "match"})
     host_sort(1 << 27)
