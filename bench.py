@@ -139,6 +139,14 @@ def cpu_baseline(n_sample: int, key_bits: int, pairs: bool, seed: int) -> dict:
 CAL_WORDS = 1 << 27   # calibration copy: 512 MiB read + 512 MiB written
 
 
+def config_seed(cid):
+    """SURVEY.md §8(d)'s seed, 0x6A09E667F3BCC908 + config id; the north-star leg (id 6, C3's n
+    and key width) also differs in bit 48 so that its keys are not C3's multiset (the same rule
+    as oracle.config_seed, restated: bench.py's timed legs do not import the oracle)."""
+    s = 0x6A09E667F3BCC908 + cid + ((1 << 48) if cid == 6 else 0)
+    return s & ((1 << 64) - 1)
+
+
 def pmc_probe(a, options):
     """Child run under rocprofv3 --pmc (see measure_traffic): one warm sort, one measured sort
     of the same workload, two calibration copies of known bytes."""
@@ -148,7 +156,7 @@ def pmc_probe(a, options):
     n = a.n or n_cfg
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    seed = (0x6A09E667F3BCC908 + cid) & ((1 << 64) - 1)
+    seed = config_seed(cid)
     k = torch.empty(n, dtype=torch.uint32 if kb == 32 else torch.uint64, device=dev)
     v = torch.empty(n, dtype=torch.uint32, device=dev) if pairs else None
     s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb, options=options)
@@ -242,7 +250,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         n_cfg = a.n
     strong = config == "c4"
     n_local = n_cfg // world if strong else n_cfg
-    seed = (0x6A09E667F3BCC908 + cid) & ((1 << 64) - 1)
+    seed = config_seed(cid)
     kdt = torch.uint32 if kb == 32 else torch.uint64
     step_bytes = n_local * (kb // 8 + (4 if pairs else 0))
     pool = max(1, min(warmup + steps, int(a.pool_gib * 2**30 // step_bytes)))

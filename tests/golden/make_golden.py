@@ -76,7 +76,8 @@ CONFIGS = {
     "c4_1b_u32": (4, 1 << 30, 32, False),
     "c5_256m_u64": (5, 1 << 28, 64, False),
     # the north star's own 1-GPU config (BASELINE.json north_star: 256 M uniform-random
-    # uint32 keys, keys only); config id 6 = its own seed
+    # uint32 keys, keys only); config id 6 = its own seed (oracle.config_seed: bit 48 set, so
+    # its keys are not C3's multiset)
     "ns_256m_u32": (6, 1 << 28, 32, False),
 }
 SMALL = ("c1_64k_u32", "c1_64k_u32_pairs", "c2_16m_u32")
