@@ -689,7 +689,8 @@ int lab2_replay(int block, int items, int rb, int x8, const uint32_t* pre, uint3
                          table, n, shift, ticket);                                           \
     return hipGetLastError() == hipSuccess ? 0 : -2;                                         \
   }
-  RP(1024, 36, 8) RP(768, 64, 8) RP(1024, 32, 4) RP(1024, 48, 8) RP(1024, 16, 8)
+  RP(1024, 36, 8) RP(768, 64, 8) RP(1024, 32, 4) RP(1024, 48, 8) RP(1024, 16, 8) RP(1024, 40, 8)
+  RP(768, 56, 8) RP(768, 60, 8)
 #undef RP
   return -1;
 }
