@@ -1322,11 +1322,20 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
     }
     if (r == GRS_OK && small) {
       const uint32_t longest = *s->h_err;
+      // block radix sort in LDS; the bitonic network where the lane order of LDS atomics is
+      // not relied on (the device probe failed, or GRS_OPT_RANK = 1)
+      const bool radix = s->rank_mode == 0;
       auto go = [&](auto kt, auto smax) {
         using KT = decltype(kt);
-        hipLaunchKernelGGL((grs::grs_segment_bitonic<KT, decltype(smax)::value>), dim3(num_segments),
-                           dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
-                           d_offsets);
+        constexpr uint32_t SM = decltype(smax)::value;
+        if (radix)
+          hipLaunchKernelGGL((grs::grs_segment_radix<KT, SM>), dim3(num_segments),
+                             dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
+                             d_offsets);
+        else
+          hipLaunchKernelGGL((grs::grs_segment_bitonic<KT, SM>), dim3(num_segments),
+                             dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
+                             d_offsets);
       };
       auto pick = [&](auto kt) {
         if (longest <= 512) go(kt, std::integral_constant<uint32_t, 512>{});

@@ -174,12 +174,16 @@ def test_segmented_sort(gpu, kb, n, nseg):
     s.close()
 
 
+@pytest.mark.parametrize("rank", ["probe", "match"])
 @pytest.mark.parametrize("kb", [32, 64])
-@pytest.mark.parametrize("lengths", [[4096] * 5, [4095, 1, 2, 3, 4096, 0, 17], [4096, 4097, 5]],
-                         ids=["all_4096", "ragged", "one_4097"])
-def test_segmented_sort_short_segment_bound(gpu, kb, lengths):
-    """Segments at the LDS path's bound (4096 items: a full bitonic network), ragged and empty
-    ones, and one item past the bound (the general path takes the whole call)."""
+@pytest.mark.parametrize("lengths", [[4096] * 5, [4095, 1, 2, 3, 4096, 0, 17], [4096, 4097, 5],
+                                     [300, 1000, 513, 2, 0, 1024, 511]],
+                         ids=["all_4096", "ragged", "one_4097", "mixed_bounds"])
+def test_segmented_sort_short_segment_bound(gpu, kb, lengths, rank):
+    """Segments at the LDS path's bound (4096 items), ragged and empty ones, lengths around the
+    512 / 1024 / 2048 LDS sizes, and one item past the bound (the general path takes the whole
+    call); rank "probe" = the block radix sort (lane-ordered LDS atomics, probed), "match" = the
+    bitonic fallback."""
     import gpuradixsort_amd as grs
 
     rng = np.random.default_rng(sum(lengths) + kb)
@@ -190,7 +194,7 @@ def test_segmented_sort_short_segment_bound(gpu, kb, lengths):
     keys[::5] = np.iinfo(dt).max                         # the largest key beside the padding
     vals = np.arange(n, dtype=np.uint32)
     want_k, want_v = oracle.segmented_sort_np(keys, off, vals)
-    s = grs.RadixSorter(n, key_bits=kb, pairs=True)
+    s = grs.RadixSorter(n, key_bits=kb, pairs=True, options={"rank": rank})
     k = torch.from_numpy(keys.view(np.int32 if kb == 32 else np.int64).copy()).to(gpu)
     v = torch.from_numpy(vals.view(np.int32).copy()).to(gpu)
     o = torch.from_numpy(off.view(np.int32)).to(gpu)
