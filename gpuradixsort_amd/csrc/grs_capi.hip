@@ -1298,10 +1298,15 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   if (n > s->capacity) return set_err(GRS_ECAPACITY, "grs_sort_segmented: n exceeds capacity");
   if (n == 0) return GRS_OK;
   if (!d_keys) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL keys");
-  // short segments (the longest <= GRS_SEG_SMALL_MAX): one workgroup per segment in LDS.
-  // Reading the longest length back costs one stream synchronisation; it is skipped where
-  // the average segment already exceeds the bound.
-  if (static_cast<uint64_t>(num_segments) * GRS_SEG_SMALL_MAX >= n) {
+  // short segments: one workgroup per segment in LDS, the block radix sort up to 16384 (u32
+  // keys) / 8192 (u64 keys) items, or the bitonic fallback up to 4096 where the lane order of
+  // LDS atomics is not relied on (the device probe failed, or GRS_OPT_RANK = 1).  Reading the
+  // longest length back costs one stream synchronisation; it is skipped where the average
+  // segment already exceeds the bound.
+  const bool radix = s->rank_mode == 0;
+  const uint32_t small_max = !radix ? GRS_SEG_SMALL_MAX
+                             : s->key_type == GRS_KEY_U32 ? GRS_SEG_RADIX_MAX32 : GRS_SEG_RADIX_MAX64;
+  if (static_cast<uint64_t>(num_segments) * small_max >= n) {
     int prev = 0;
     GRS_HIP(hipGetDevice(&prev));
     if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
@@ -1318,30 +1323,34 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
           hipStreamSynchronize(st) != hipSuccess)
         r = set_err(GRS_EHIP, "grs_sort_segmented: longest segment");
       else
-        small = *s->h_err <= GRS_SEG_SMALL_MAX;
+        small = *s->h_err <= small_max;
     }
     if (r == GRS_OK && small) {
       const uint32_t longest = *s->h_err;
-      // block radix sort in LDS; the bitonic network where the lane order of LDS atomics is
-      // not relied on (the device probe failed, or GRS_OPT_RANK = 1)
-      const bool radix = s->rank_mode == 0;
-      auto go = [&](auto kt, auto smax) {
+      auto go = [&](auto kt, auto smax, auto block) {
         using KT = decltype(kt);
-        constexpr uint32_t SM = decltype(smax)::value;
-        if (radix)
-          hipLaunchKernelGGL((grs::grs_segment_radix<KT, SM>), dim3(num_segments),
-                             dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
-                             d_offsets);
-        else
-          hipLaunchKernelGGL((grs::grs_segment_bitonic<KT, SM>), dim3(num_segments),
-                             dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
-                             d_offsets);
+        constexpr uint32_t SM = decltype(smax)::value, BL = decltype(block)::value;
+        if constexpr (SM <= (sizeof(KT) == 4 ? GRS_SEG_RADIX_MAX32 : GRS_SEG_RADIX_MAX64)) {
+          if (radix)
+            hipLaunchKernelGGL((grs::grs_segment_radix<KT, SM, BL>), dim3(num_segments), dim3(BL),
+                               0, st, static_cast<KT*>(d_keys), d_vals, d_offsets);
+        }
+        if constexpr (SM <= GRS_SEG_SMALL_MAX) {
+          if (!radix)
+            hipLaunchKernelGGL((grs::grs_segment_bitonic<KT, SM>), dim3(num_segments),
+                               dim3(GRS_SEG_SMALL_BLOCK), 0, st, static_cast<KT*>(d_keys), d_vals,
+                               d_offsets);
+        }
       };
+      using B256 = std::integral_constant<uint32_t, 256>;
+      using B1024 = std::integral_constant<uint32_t, 1024>;
       auto pick = [&](auto kt) {
-        if (longest <= 512) go(kt, std::integral_constant<uint32_t, 512>{});
-        else if (longest <= 1024) go(kt, std::integral_constant<uint32_t, 1024>{});
-        else if (longest <= 2048) go(kt, std::integral_constant<uint32_t, 2048>{});
-        else go(kt, std::integral_constant<uint32_t, GRS_SEG_SMALL_MAX>{});
+        if (longest <= 512) go(kt, std::integral_constant<uint32_t, 512>{}, B256{});
+        else if (longest <= 1024) go(kt, std::integral_constant<uint32_t, 1024>{}, B256{});
+        else if (longest <= 2048) go(kt, std::integral_constant<uint32_t, 2048>{}, B256{});
+        else if (longest <= 4096) go(kt, std::integral_constant<uint32_t, 4096>{}, B256{});
+        else if (longest <= 8192) go(kt, std::integral_constant<uint32_t, 8192>{}, B1024{});
+        else go(kt, std::integral_constant<uint32_t, 16384>{}, B1024{});
       };
       if (s->key_type == GRS_KEY_U32) pick(uint32_t{});
       else pick(uint64_t{});

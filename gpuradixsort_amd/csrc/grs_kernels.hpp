@@ -869,39 +869,40 @@ __global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_bitonic(
 // The same short segments by a block LSD radix sort in LDS (the default; the bitonic kernel
 // above is the fallback when the device probe of the lane-ordered LDS atomics fails, §6.3):
 // 8-bit digits, sizeof(K) passes.  Items are held wave-striped (item j of lane l of wave w is
-// segment position w * 64 * I + j * 64 + l, I = SMAX / 256), so the returning LDS add on the
-// wave's digit counter ranks them stably, as the sort pass does; per pass one add, one scan
-// of the 4 x 256 counters and one scatter through LDS.  The payload follows the input position.
-template <typename K, uint32_t SMAX>
-__global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_radix(
+// segment position w * 64 * I + j * 64 + l, I = SMAX / BLOCK), so the returning LDS add on the
+// wave's digit counter ranks them stably, as the sort pass does; per pass one add, one scan of
+// the W x 256 counters and one scatter of keys (and payload) through LDS.  BLOCK 256 up to
+// 4096 items, 1024 threads beyond (u32 keys to 16384, u64 keys to 8192: the LDS holds the
+// keys, the payload and 16 x 256 counters).
+#define GRS_SEG_RADIX_MAX32 16384
+#define GRS_SEG_RADIX_MAX64 8192
+template <typename K, uint32_t SMAX, uint32_t BLOCK>
+__global__ __launch_bounds__(BLOCK) void grs_segment_radix(
     K* __restrict__ keys, uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets) {
-  constexpr uint32_t B = GRS_SEG_SMALL_BLOCK, W = B / GRS_WAVE;
-  static_assert(SMAX <= GRS_SEG_SMALL_MAX && SMAX >= 2 * B && (SMAX & (SMAX - 1)) == 0,
-                "power-of-two bound of at least two items per thread");
-  static_assert(B == 256, "one thread per 8-bit digit in the counter scan");
-  constexpr uint32_t I = SMAX / B;
+  constexpr uint32_t W = BLOCK / GRS_WAVE, I = SMAX / BLOCK;
+  static_assert((BLOCK == 256 || BLOCK == 1024) && I >= 2 && (SMAX & (SMAX - 1)) == 0,
+                "256 or 1024 threads, a power-of-two bound of at least two items per thread");
+  static_assert(SMAX <= (sizeof(K) == 4 ? GRS_SEG_RADIX_MAX32 : GRS_SEG_RADIX_MAX64), "LDS");
   __shared__ K sk[SMAX];
-  __shared__ uint16_t sp[SMAX];
   __shared__ uint32_t sv[SMAX];
   __shared__ uint32_t cnt[W * 256];
-  __shared__ uint32_t wtot[W];
+  __shared__ uint32_t wtot[4];
   const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
   const uint32_t lo = offsets[blockIdx.x];
   const uint32_t len = offsets[blockIdx.x + 1] - lo;
   if (len <= 1 || len > SMAX) return;   // (longer segments never reach this kernel)
+  const bool pay = vals != nullptr;
   K k[I];
-  uint32_t p[I];
+  uint32_t v[I];
 #pragma unroll
   for (uint32_t j = 0; j < I; ++j) {
     const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
     k[j] = i < len ? keys[lo + i] : K(0);
-    p[j] = i;
-    if (vals != nullptr && i < len) sv[i] = vals[lo + i];
+    v[j] = pay && i < len ? vals[lo + i] : 0u;
   }
   for (int pass = 0; pass < static_cast<int>(sizeof(K)); ++pass) {
     const int shift = 8 * pass;
-#pragma unroll
-    for (uint32_t c = t; c < W * 256; c += B) cnt[c] = 0;
+    for (uint32_t c = t; c < W * 256; c += BLOCK) cnt[c] = 0;
     __syncthreads();
     uint32_t r[I];
 #pragma unroll
@@ -911,19 +912,22 @@ __global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_radix(
       r[j] = i < len ? atomicAdd(&cnt[w * 256 + d], 1u) : 0u;
     }
     __syncthreads();
-    {   // thread t = digit t: wave offsets, then the digit's start over all digits
-      uint32_t c[W], tot = 0;
+    // threads 0..255, one per digit: wave offsets, then the digit's start over all digits
+    uint32_t c[W], tot = 0, incl = 0;
+    if (t < 256) {
 #pragma unroll
       for (uint32_t ww = 0; ww < W; ++ww) {
         c[ww] = cnt[ww * 256 + t];
         tot += c[ww];
       }
-      const uint32_t incl = wave_scan_dpp(tot);
+      incl = wave_scan_dpp(tot);
       if (lane == GRS_WAVE - 1) wtot[w] = incl;
-      __syncthreads();
+    }
+    __syncthreads();
+    if (t < 256) {
       uint32_t base = incl - tot;
 #pragma unroll
-      for (uint32_t ww = 0; ww < W; ++ww) base += ww < w ? wtot[ww] : 0u;
+      for (uint32_t ww = 0; ww < 4; ++ww) base += ww < w ? wtot[ww] : 0u;
 #pragma unroll
       for (uint32_t ww = 0; ww < W; ++ww) {
         cnt[ww * 256 + t] = base;
@@ -938,7 +942,7 @@ __global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_radix(
         const uint32_t d = static_cast<uint32_t>(k[j] >> shift) & 255u;
         const uint32_t dst = cnt[w * 256 + d] + r[j];
         sk[dst] = k[j];
-        sp[dst] = static_cast<uint16_t>(p[j]);
+        if (pay) sv[dst] = v[j];
       }
     }
     __syncthreads();
@@ -947,7 +951,7 @@ __global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_radix(
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
       if (i < len) {
         k[j] = sk[i];
-        p[j] = sp[i];
+        if (pay) v[j] = sv[i];
       }
     }
     // (the next pass's counter reset and scatter are behind its first barrier)
@@ -957,7 +961,7 @@ __global__ __launch_bounds__(GRS_SEG_SMALL_BLOCK) void grs_segment_radix(
     const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
     if (i < len) {
       keys[lo + i] = k[j];
-      if (vals != nullptr) vals[lo + i] = sv[p[j]];
+      if (pay) vals[lo + i] = v[j];
     }
   }
 }

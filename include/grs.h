@@ -398,9 +398,10 @@ grs_status grs_scan_check_error(const void* d_scratch, void* stream);
 /* Segmented (batched) stable sort: every segment [off[s], off[s+1]) of d_keys[0..n) is
  * sorted on its own, with d_vals (nullable) permuted alike; d_offsets: num_segments + 1
  * non-decreasing DEVICE words, off[0] = 0, off[num_segments] = n.  Needs a sorter created
- * with a payload.  Where no segment is longer than 4096 items, one workgroup per segment
- * sorts it in LDS (one read and one write of the data); finding the longest segment costs one
- * synchronisation of `stream` (skipped when n / num_segments > 4096).  Otherwise two sorts
+ * with a payload.  Where no segment is longer than 16384 items (u32 keys; 8192 for u64 keys,
+ * 4096 where the LDS lane-order probe failed), one workgroup per segment sorts it in LDS (one
+ * read and one write of the data); finding the longest segment costs one synchronisation of
+ * `stream` (skipped when the average segment is already longer).  Otherwise two sorts
  * (keys, then segment ids; for u32 keys one sort of (segment, key)) and a gather; scratch of
  * 12 + key-size bytes per item is allocated on first use and kept. */
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,

@@ -177,13 +177,14 @@ def test_segmented_sort(gpu, kb, n, nseg):
 @pytest.mark.parametrize("rank", ["probe", "match"])
 @pytest.mark.parametrize("kb", [32, 64])
 @pytest.mark.parametrize("lengths", [[4096] * 5, [4095, 1, 2, 3, 4096, 0, 17], [4096, 4097, 5],
-                                     [300, 1000, 513, 2, 0, 1024, 511]],
-                         ids=["all_4096", "ragged", "one_4097", "mixed_bounds"])
+                                     [300, 1000, 513, 2, 0, 1024, 511],
+                                     [16384, 9000, 8192, 1, 8193], [16385, 3]],
+                         ids=["all_4096", "ragged", "one_4097", "mixed_bounds", "to_16k", "one_16385"])
 def test_segmented_sort_short_segment_bound(gpu, kb, lengths, rank):
-    """Segments at the LDS path's bound (4096 items), ragged and empty ones, lengths around the
-    512 / 1024 / 2048 LDS sizes, and one item past the bound (the general path takes the whole
-    call); rank "probe" = the block radix sort (lane-ordered LDS atomics, probed), "match" = the
-    bitonic fallback."""
+    """Segments at the LDS paths' bounds (4096 items for the bitonic fallback, 16384 / 8192 for the
+    block radix sort of u32 / u64 keys), ragged and empty ones, lengths around every LDS size,
+    and one item past a bound (the general path takes the whole call); rank "probe" = the block
+    radix sort (lane-ordered LDS atomics, probed), "match" = the bitonic fallback."""
     import gpuradixsort_amd as grs
 
     rng = np.random.default_rng(sum(lengths) + kb)

@@ -5,8 +5,8 @@ Prints one JSON line per operation with its algorithmic bytes per item, GB/s and
 of the 8 TB/s HBM peak:
   scan            grs_exclusive_scan_u32, 2^28 items: 8 B/item (read + write)
   key_transform   grs_key_transform f32, 2^28 items: 8 B/item
-  segmented_sort  grs_sort_segmented u32 key + u32 payload, 2^26 items in 2^16 segments
-                  (Gkeys/s; two sorts + a gather by construction)
+  segmented_sort  grs_sort_segmented u32 key + u32 payload, 2^26 items in 2^16, 2^12 and 2^6
+                  segments (Gkeys/s; the first two sorted in LDS, the last by the general path)
 """
 import argparse
 import json
@@ -73,22 +73,24 @@ def main():
     del x, y, f
 
     m = 1 << 26
-    segs = 1 << 16
     s = grs.RadixSorter(m, key_bits=32, pairs=True)
     k0 = torch.empty(m, dtype=torch.int32, device=dev)
     grs.fill_splitmix(k0, 2)
     k = torch.empty_like(k0)
     v = torch.empty_like(k0)
-    off = torch.arange(0, m + 1, m // segs, dtype=torch.int32, device=dev)
-
-    def seg():
-        k.copy_(k0)
-        s.sort_segmented(k, off, v)
     ms_copy = timed(lambda: k.copy_(k0), a.reps)
-    ms = timed(seg, a.reps) - ms_copy
-    print(json.dumps({"op": "sort_segmented_u32_pairs", "n": m, "segments": segs,
-                      "ms": round(ms, 4), "Gkeys/s": round(m / ms / 1e6, 2),
-                      "note": "restore copy of the keys subtracted"}), flush=True)
+    # 1K-item segments (256-thread LDS sort), 16K-item segments (1024-thread LDS sort), and
+    # 64 segments of 1M items (the general path)
+    for segs in (1 << 16, 1 << 12, 1 << 6):
+        off = torch.arange(0, m + 1, m // segs, dtype=torch.int32, device=dev)
+
+        def seg():
+            k.copy_(k0)
+            s.sort_segmented(k, off, v)
+        ms = timed(seg, a.reps) - ms_copy
+        print(json.dumps({"op": "sort_segmented_u32_pairs", "n": m, "segments": segs,
+                          "ms": round(ms, 4), "Gkeys/s": round(m / ms / 1e6, 2),
+                          "note": "restore copy of the keys subtracted"}), flush=True)
 
 
 def partition(n, g=8, options=None):

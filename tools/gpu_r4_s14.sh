@@ -2,5 +2,5 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 
-timeout -k 10 300 python -u -m pytest tests/test_gpu_extras.py -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4s16_extras_tests.txt 2>&1 && timeout -k 10 200 python -u tools/bench_extras.py > gpurun_out/r4s16_bench_extras.txt 2>&1
-rc=$?; tail -3 gpurun_out/r4s16_extras_tests.txt; grep op gpurun_out/r4s16_bench_extras.txt; exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_gpu_extras.py -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4s17_extras_tests.txt 2>&1 && timeout -k 10 200 python -u tools/bench_extras.py > gpurun_out/r4s17_bench_extras.txt 2>&1
+rc=$?; tail -3 gpurun_out/r4s17_extras_tests.txt; grep op gpurun_out/r4s17_bench_extras.txt; exit $rc
