@@ -56,8 +56,9 @@ def test_scan_vs_reference_restatement(gpu, n):
         assert total == wtot
 
 
-@pytest.mark.parametrize("n", [(1 << 24) + 5, 100_000_007])
+@pytest.mark.parametrize("n", [(1 << 22) - 1, 1 << 22, (1 << 24) + 5, 100_000_007])
 def test_scan_large_in_place(gpu, n):
+    """In place, around and above the switch from 8K- to 32K-item tiles (2^22 items)."""
     rng = np.random.default_rng(7)
     a = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     want, wtot = cumsum_excl(a)
