@@ -594,10 +594,23 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
   case ((B * 1000L + I) * 10 + M) * 100000000L + O: {                                          \
     const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
     const uint32_t g = std::min<uint32_t>(tiles, grid);                                        \
-    hipLaunchKernelGGL((grs_lab::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),         \
-                       dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
-                       grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
-                       (const grs::RadixDigit<uint32_t>*)nullptr, hist_stride, range_tiles);   \
+    if ((O & 2) != 0) {   /* static tiles: a cooperative launch (every workgroup resident) */   \
+      const uint32_t* a_in = (const uint32_t*)in; uint32_t* a_out = (uint32_t*)out;           \
+      const uint32_t* a_vin = nullptr; uint32_t* a_vout = nullptr; uint32_t a_n = n;          \
+      grs::RadixDigit<uint32_t> a_dig{0, 15u};                                                 \
+      const grs::RadixDigit<uint32_t>* a_dd = nullptr;                                         \
+      void* args[] = {&a_in, &a_out, &a_vin, &a_vout, &a_n, &a_dig, &hist, &ticket, &st, &st2, \
+                      &err, &a_dd, &hist_stride, &range_tiles};                                \
+      if (hipLaunchCooperativeKernel(                                                          \
+              reinterpret_cast<const void*>(&grs_lab::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), \
+              dim3(g), dim3(B), args, 0, s) != hipSuccess)                                     \
+        return -3;                                                                             \
+    } else {                                                                                   \
+      hipLaunchKernelGGL((grs_lab::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),       \
+                         dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
+                         grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,        \
+                         (const grs::RadixDigit<uint32_t>*)nullptr, hist_stride, range_tiles); \
+    }                                                                                          \
   } break;
     V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
     V(1024, 32, 1, 8) V(1024, 32, 1, 512) V(1024, 32, 1, 520) V(1024, 32, 1, 528)
@@ -605,7 +618,7 @@ int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in
     V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
     V(1024, 32, 1, 524288) V(1024, 32, 1, 524296) V(512, 32, 2, 524288) V(512, 32, 2, 8)
     V(1024, 32, 1, 64) V(1024, 32, 1, 72) V(1024, 32, 1, 16777216) V(1024, 32, 1, 33554432)
-    V(1024, 32, 1, 134217728) V(1024, 32, 1, 134217736)
+    V(1024, 32, 1, 134217728) V(1024, 32, 1, 134217736) V(1024, 32, 1, 2) V(1024, 32, 1, 10)
     V(1024, 32, 1, 67108864) V(1024, 32, 1, 67108872) V(1024, 32, 1, 67108880)
 #undef V
     default:

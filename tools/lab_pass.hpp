@@ -611,7 +611,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   V4_STAMP(0);
   if constexpr (PF) {
     if (t == 0)
-      sm.next = XR ? draw_ticket_xr(ticket, tiles, range_tiles)
+      sm.next = (OPT & 2) != 0 ? tile + gridDim.x
+              : XR ? draw_ticket_xr(ticket, tiles, range_tiles)
               : (OPT & 134217728) != 0 ? draw_ticket_x8(ticket, tiles) : atomicAdd(ticket, 1u);  // read after B2
   }
   // this tile's (and its group's) words of the next pass's status buffer
@@ -1097,8 +1098,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   constexpr bool XR = (OPT & 1048576) != 0;
   const uint32_t t = threadIdx.x;
   const uint64_t t_entry = (OPT & 8) ? __builtin_amdgcn_s_memtime() : 0;
+  // OPT 2: static tiles (blockIdx.x, then + gridDim.x): no ticket round trip, valid only with
+  // every workgroup resident (a cooperative launch)
   if (t == 0)
-    sm.ticket = XR ? draw_ticket_xr(ticket, (n + SM::TILE - 1) / SM::TILE, range_tiles)
+    sm.ticket = (OPT & 2) != 0 ? blockIdx.x
+              : XR ? draw_ticket_xr(ticket, (n + SM::TILE - 1) / SM::TILE, range_tiles)
               : (OPT & 134217728) != 0 ? draw_ticket_x8(ticket, (n + SM::TILE - 1) / SM::TILE)
                                        : atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
