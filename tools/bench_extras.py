@@ -93,6 +93,32 @@ def main():
                           "note": "restore copy of the keys subtracted"}), flush=True)
 
 
+def record_sort(n=1 << 24, rb=28):
+    """grs_sort_records (the reference's intended use, ParallelSort.h:13-31):
+    n 28-byte particles (position float3 at offset 0) sorted by the 30-bit Morton code of their
+    position: key extraction, stable (key, index) sort, record gather, copy-back."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    rec0 = torch.empty((n, rb), dtype=torch.uint8, device=dev)
+    pos = torch.rand((n, 3), generator=g, device=dev) * 2 - 1
+    rec0[:, :12] = pos.view(torch.uint8).view(n, 12)
+    rec0[:, 12:] = 0
+    rec = torch.empty_like(rec0)
+    rs = grs.RecordSort(n)
+    ms_copy = timed(lambda: rec.copy_(rec0), 10)
+
+    def go():
+        rec.copy_(rec0)
+        rs.sort(rec, morton=(0, (-1.0, -1.0, -1.0), (1.0, 1.0, 1.0)))
+    ms = timed(go, 10) - ms_copy
+    print(json.dumps({"op": f"sort_records_morton_{rb}B", "n": n, "ms": round(ms, 4),
+                      "Mrecords/s": round(n / ms / 1e3, 1),
+                      "record_GB/s": round(n * rb * 2 / ms / 1e6, 1),
+                      "note": "extraction + (key, index) sort + gather + copy-back; restore copy subtracted"}),
+          flush=True)
+
+
 def partition(n, g=8, options=None):
     """grs_partition (the multi-GPU exchange's local step): 2^27 u32 keys into g buckets by
     g - 1 splitters at uniform quantiles; 8 B/key algorithmic (read + write)."""
@@ -131,6 +157,7 @@ def host_sort(n):
 
 if __name__ == "__main__":
     main()
+    record_sort()
     partition(1 << 27)
     if "--partition-ab" in sys.argv:
         partition(1 << 27, options={"rank": "match"})
