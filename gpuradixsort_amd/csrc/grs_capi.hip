@@ -711,9 +711,10 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = false;
   {
-    // grs_upfront_hist2: 2 blocks of 512 per CU; a multiple of the resident slots so the
-    // grid-stride loop ends evenly, and > n >> kHist2GridShift blocks (16-bit counters)
-    const int slots = 2 * s->cus;
+    // grs_upfront_hist2: 2 blocks of 512 per CU (u64 keys: 1 of 1024); a multiple of the
+    // resident slots so the grid-stride loop ends evenly, and > n >> kHist2GridShift blocks
+    // (16-bit counters)
+    const int slots = grs::Hist2Layout<K>::PER_CU * s->cus;
     const int need = static_cast<int>(n >> grs::kHist2GridShift<K>) + 1;
     // (one block per CU up to 2^25 keys: two measured slower at C2, 24.8 vs 21.5 us)
     int grid = n <= (1u << 25) ? s->cus : slots;

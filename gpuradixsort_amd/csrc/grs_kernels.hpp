@@ -187,23 +187,26 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 // its 0.91 ms.  Here the 16-bit half is chosen by the POSITION's parity instead: super digits 2p and 2p+1 share the word
 // of (pair p, digit value d), so the add value is a compile-time 1 or 0x10000 and a digit
 // costs v_bfe_u32 + v_lshl_add_u32 (+ the ds_add_u32, whose pair offset is an immediate).
-// Copy c of each counter sits in bank c (COPIES = 32 for u32 keys: every 32-lane LDS group
-// conflict-free; 16 for u64 keys, 2-way at most).  64 KB per 512-thread block, 2 blocks per
-// CU.  A copy counts at most (512 / COPIES) * VEC * ceil(n / VEC / (grid * 512)) keys per
-// counter, which the launch keeps below 2^16 (grid > n >> kHist2GridShift).
+// Copy c of each counter sits in bank c (COPIES = 32: every 32-lane LDS group conflict-free).
+// u32 keys: 64 KB per 512-thread block, 2 blocks per CU; u64 keys: 128 KB per 1024-thread
+// block, 1 per CU.  A copy counts at most (BLOCK / COPIES) * VEC * ceil(n / VEC / (grid *
+// BLOCK)) keys per counter, which the launch keeps below 2^16 (grid > n >> kHist2GridShift).
 // FULL: the bit range is the whole key (begin_bit 0, every super digit 8 bits wide), so the
 // field offsets are immediates; otherwise they are SGPR operands (one 64-bit shift more for
 // u64 keys).  Super digits past the range are counted into digit 0 of their position and
 // never read.  A used position shares its word with an unused one only as the low half
 // (supers odd); the unused high half's overflow carries out of bit 31, so it cannot corrupt
 // the used count.
+// u64 keys (round 4): 32 copies too, so no 2-way bank conflicts, in 128 KB of LDS for one
+// 1024-thread block per CU (was 16 copies in 64 KB, two 512-thread blocks).
 template <typename K>
 struct Hist2Layout {
   static constexpr int MAXQ = static_cast<int>(sizeof(K));   // super digits per key
   static constexpr int PAIRS = MAXQ / 2;
-  static constexpr int COPIES = 16384 / (PAIRS * 256);         // u32: 32, u64: 16
-  static constexpr int WORDS = PAIRS * 256 * COPIES;           // 16384 words = 64 KB
-  static constexpr int BLOCK = 512;
+  static constexpr int COPIES = 32;
+  static constexpr int WORDS = PAIRS * 256 * COPIES;           // u32 64 KB, u64 128 KB
+  static constexpr int BLOCK = sizeof(K) == 4 ? 512 : 1024;    // 32 threads per copy
+  static constexpr int PER_CU = sizeof(K) == 4 ? 2 : 1;        // resident blocks per CU
 };
 template <typename K>
 constexpr int kHist2GridShift = sizeof(K) == 4 ? 20 : 19;
