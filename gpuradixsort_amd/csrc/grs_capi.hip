@@ -1227,6 +1227,49 @@ grs_status grs_scan_check_error(const void* d_scratch, void* stream) {
   return e ? set_err(GRS_ETIMEOUT, "a scan look-back spin exceeded its bound") : GRS_OK;
 }
 
+// At most 16 segments, some longer than the LDS path takes: each segment is sorted on its own by
+// the sorter (its keys and payload are contiguous: sub-range pointers), 16 B of traffic per
+// pair per pass and no gather.  (A whole-array key sort + one partition pass by segment
+// measured 2.97 ms for 4 x 2^24 pairs: its payload gather reads 4 B per 128-B line.)  The
+// offsets are read back once (one stream synchronisation).  Keys-only calls carry a scratch
+// rider.
+static grs_status sort_segmented_few(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
+                                     const uint32_t* d_offsets, int num_segments, void* stream) {
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  grs_status r = GRS_OK;
+  uint32_t off[GRS_MAX_SPLITTERS + 2] = {};
+  if (hipMemcpyAsync(off, d_offsets, (num_segments + 1) * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_sort_segmented: offsets");
+  if (r == GRS_OK && !d_vals && s->seg_bytes < n * 4) {   // the keys-only rider
+    if (s->seg_buf) (void)hipFree(s->seg_buf);
+    s->seg_buf = nullptr;
+    s->seg_bytes = 0;
+    if (hipMalloc(&s->seg_buf, n * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      r = set_err(GRS_ENOMEM, "grs_sort_segmented: scratch allocation failed");
+    } else {
+      s->seg_bytes = n * 4;
+    }
+  }
+  for (int g = 0; g < num_segments && r == GRS_OK; ++g) {
+    const uint32_t lo = off[g], hi = off[g + 1];
+    if (hi <= lo + 1) continue;
+    if (hi > n) {
+      r = set_err(GRS_EINVAL, "grs_sort_segmented: offsets past n");
+      break;
+    }
+    uint32_t* v = d_vals ? d_vals + lo : static_cast<uint32_t*>(s->seg_buf) + lo;
+    r = grs_sort(s, static_cast<char*>(d_keys) + static_cast<size_t>(lo) * kb, v, hi - lo, stream);
+  }
+  if (prev != s->device) (void)hipSetDevice(prev);
+  return r;
+}
+
 // u32 keys: one sort of u64 keys (segment << 32 | key) by bits [0, 32 + ceil(log2 S)), the
 // payload riding along; no random gathers (grs_segment_marks / _compose / _split).
 // Scratch (seg_buf): comp u64[n] | marks u32[n] | marks_excl u32[n] | scan scratch.
@@ -1360,6 +1403,8 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
     if (prev != s->device) (void)hipSetDevice(prev);
     if (r != GRS_OK || small) return r;
   }
+  if (num_segments <= GRS_MAX_SPLITTERS + 1)
+    return sort_segmented_few(s, d_keys, d_vals, n, d_offsets, num_segments, stream);
   if (s->key_type == GRS_KEY_U32) return sort_segmented_u32(s, d_keys, d_vals, n, d_offsets,
                                                             num_segments, stream);
   int prev = 0;

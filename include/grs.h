@@ -401,9 +401,10 @@ grs_status grs_scan_check_error(const void* d_scratch, void* stream);
  * with a payload.  Where no segment is longer than 16384 items (u32 keys; 8192 for u64 keys,
  * 4096 where the LDS lane-order probe failed), one workgroup per segment sorts it in LDS (one
  * read and one write of the data); finding the longest segment costs one synchronisation of
- * `stream` (skipped when the average segment is already longer).  Otherwise two sorts
- * (keys, then segment ids; for u32 keys one sort of (segment, key)) and a gather; scratch of
- * 12 + key-size bytes per item is allocated on first use and kept. */
+ * `stream` (skipped when the average segment is already longer).  Otherwise, with at most 16
+ * segments, each segment is sorted on its own (the offsets are read back: one synchronisation);
+ * with more, two sorts (keys, then segment ids; for u32 keys one sort of (segment, key)) and a
+ * gather; scratch of 12 + key-size bytes per item is allocated on first use and kept. */
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
                               const uint32_t* d_offsets, int num_segments, void* stream);
 

@@ -79,9 +79,10 @@ def main():
     k = torch.empty_like(k0)
     v = torch.empty_like(k0)
     ms_copy = timed(lambda: k.copy_(k0), a.reps)
-    # 1K-item segments (256-thread LDS sort), 16K-item segments (1024-thread LDS sort), and
-    # 64 segments of 1M items (the general path)
-    for segs in (1 << 16, 1 << 12, 1 << 6):
+    # 1K-item segments (256-thread LDS sort), 16K-item segments (1024-thread LDS sort), 64
+    # segments of 1M items (the composite (segment, key) sort) and 4 of 16M (key sort + one
+    # partition pass by segment)
+    for segs in (1 << 16, 1 << 12, 1 << 6, 4):
         off = torch.arange(0, m + 1, m // segs, dtype=torch.int32, device=dev)
 
         def seg():
