@@ -538,6 +538,7 @@ int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const vo
     V(32, 0, 768, 64, 1, 134217728 + 1040) V(32, 0, 768, 64, 1, 134217728 + 1048)
     V(32, 0, 1024, 36, 1, 4194576) V(32, 0, 1024, 36, 1, 4194584) V(32, 0, 768, 64, 1, 4195344)
     V(32, 0, 768, 64, 1, 4195352) V(32, 1, 768, 40, 1, 4195344) V(64, 0, 768, 44, 1, 4195344)
+    V(32, 0, 1024, 36, 1, 276) V(32, 0, 1024, 36, 1, 284)
 #undef V
     default:
       return -1;
@@ -576,6 +577,7 @@ int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid
     V(32, 0, 1024, 36, 1, 8388880) V(32, 0, 1024, 36, 1, 8388888) V(32, 0, 768, 64, 1, 8389648)
     V(32, 0, 768, 64, 1, 8389656)
     V(32, 0, 1024, 36, 1, 526608) V(32, 0, 1024, 36, 1, 526616)
+    V(32, 0, 1024, 36, 1, 260) V(32, 0, 1024, 36, 1, 268)
 #undef V
     default:
       return -1;

@@ -64,7 +64,29 @@ __host__ __device__ constexpr size_t lb3_status_words(size_t tiles, size_t radix
 // after it).  issue() sends the first round of loads, finish() consumes them.
 // GW: groups polled per round.  The two-round (XL) tiles use 4: the window's registers are
 // live across the reorder there, beside the tile's keys and positions.
-template <int RADIX, int GW = GRS_LB_GWIN, bool OWNACC = false>
+// OPT 4: one wave's 64 status words (a uniform 64-word row) into its lanes through scalar
+// loads with glc (coherent across XCDs, tools/smem_probe.hip): a re-poll that does not queue
+// behind the wave's outstanding vector loads (vmcnt retires in order)
+typedef uint32_t lab_u32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ uint32_t smem_row_lane(const uint32_t* row) {
+  lab_u32x16 v[4];
+  asm volatile(
+      "s_load_dwordx16 %0, %4, 0x0 glc\n\t"
+      "s_load_dwordx16 %1, %4, 0x40 glc\n\t"
+      "s_load_dwordx16 %2, %4, 0x80 glc\n\t"
+      "s_load_dwordx16 %3, %4, 0xc0 glc\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=s"(v[0]), "=s"(v[1]), "=s"(v[2]), "=s"(v[3]) : "s"(row) : "memory");
+  uint32_t out = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(out) : "s"(v[q][i]), "i"(16 * q + i));
+  return out;
+}
+
+template <int RADIX, int GW = GRS_LB_GWIN, bool OWNACC = false, bool SC = false>
 struct Lb3 {
   static constexpr int G = GRS_LB_GROUP;
   uint32_t tw[G - 1];
@@ -107,14 +129,28 @@ struct Lb3 {
 #pragma unroll
     for (int k = 0; k < G - 1; ++k) {
       uint32_t v = tw[k];
-      while (v == 0u) {
-        if (++spins > GRS_SPIN_LIMIT) {
-          atomicOr(error_word, 1u);
-          v = 1u;
-          break;
+      if constexpr (SC) {   // the whole wave re-polls its row until every lane's word is in
+        const uint32_t* row = status + static_cast<size_t>(first + k) * RADIX +
+                              (__builtin_amdgcn_readfirstlane(d) & ~63u);
+        while (__builtin_amdgcn_ballot_w64(v == 0u) != 0) {
+          if (++spins > GRS_SPIN_LIMIT) {
+            if (v == 0u) atomicOr(error_word, 1u);
+            v = v == 0u ? 1u : v;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          v = smem_row_lane(row);
         }
-        __builtin_amdgcn_s_sleep(1);
-        v = ld_status(status + static_cast<size_t>(first + k) * RADIX + d);
+      } else {
+        while (v == 0u) {
+          if (++spins > GRS_SPIN_LIMIT) {
+            atomicOr(error_word, 1u);
+            v = 1u;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          v = ld_status(status + static_cast<size_t>(first + k) * RADIX + d);
+        }
       }
       own += v - 1u;
     }
@@ -321,6 +357,8 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
                          (OPT & 67108864) != 0 ? 4 : 1>;
 
 // OPT bits (lab ablations; the library uses OPT = 0):
+//   4  the look-back's re-polls of its own group's tile words through scalar loads
+//      (smem_row_lane; the digit threads are whole waves at 8-bit digits)
 //   8  stamps: s_memtime at phase ends into error_word[64 + tile*8 + k]
 //   16 look-back issued after the reorder (no overlap)
 //   32 contiguous stores (dst = tile position; wrong output)      64 no look-back (estimate)
@@ -696,7 +734,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
 
   static_assert((OPT & 1073741824) == 0 || ((OPT & 2097152) == 0 && (OPT & 536870912) == 0),
                 "accumulator read-back: the one-thread-per-digit look-back, add at B1");
-  Lb3<RADIX, (ROUNDS > 1 ? GRS_LB_GWIN_XL : GRS_LB_GWIN), (OPT & 1073741824) != 0> lb;
+  Lb3<RADIX, (ROUNDS > 1 ? GRS_LB_GWIN_XL : GRS_LB_GWIN), (OPT & 1073741824) != 0, (OPT & 4) != 0> lb;
   LbWide<RADIX, WIDE ? LW : 2> lbw;
   const uint32_t wd = t / LW, wj = t & (LW - 1);   // wide look-back: digit and lane in its group
   if (t < static_cast<uint32_t>(RADIX)) {
