@@ -843,7 +843,16 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
                               count + 1, stream));
     GRS_HIP(hipMemsetAsync(s->status, 0, words * 4, stream));
   } else {
-    const int grid = std::max(1, std::min<int>(2048, (n + 4095) / 4096));
+    // one resident wave of workgroups (grid-stride loop): 2048 blocks at 6 per CU (76 VGPRs)
+    // ran as 1536 + 512, a second, mostly empty round (tools/prof_partition.py)
+    static const int per_cu = [] {
+      int b = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, grs::grs_digit_hist<K, Dig>, GRS_HIST_BLOCK,
+                                                       0) != hipSuccess || b < 1)
+        b = 4;
+      return b;
+    }();
+    const int grid = std::max(1, std::min<int>(per_cu * std::max(1, s->cus), (n + 4095) / 4096));
     hipLaunchKernelGGL((grs::grs_digit_hist<K, Dig>), dim3(grid), dim3(GRS_HIST_BLOCK), 0, stream,
                        keys, n, dig, dig_dev, hist, s->status, static_cast<uint32_t>(words));
     GRS_HIP(hipGetLastError());
