@@ -272,8 +272,9 @@ struct grs_sorter {
   // grs_sort_sharded scratch (first use): samples, gathered samples, count matrix, digit
   void* shard_buf = nullptr;
   size_t shard_bytes = 0;
-  void* rec_buf = nullptr;         // grs_sort_records scratch: keys | index | record copy
+  void* rec_buf = nullptr;         // record sorts: per-call keys | index | record copy
   size_t rec_bytes = 0;
+  void* rec_kbuf = nullptr;        // grs_records_key_buffers: keys | index for the capacity
   uint32_t* shard_host = nullptr;  // pinned: the G x G count matrix read back once per call
   void* xbuf = nullptr;            // grs_sort_sharded send buffer: G regions of n_local items
   size_t xbuf_bytes = 0;
@@ -337,6 +338,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->host_stage) (void)hipFree(s->host_stage);
   if (s->shard_buf) (void)hipFree(s->shard_buf);
   if (s->rec_buf) (void)hipFree(s->rec_buf);
+  if (s->rec_kbuf) (void)hipFree(s->rec_kbuf);
   if (s->shard_host) (void)hipHostFree(s->shard_host);
   if (s->xbuf) (void)hipFree(s->xbuf);
   if (s->xrbuf) (void)hipFree(s->xrbuf);
@@ -1193,9 +1195,14 @@ static constexpr size_t kScanLargeMin = size_t(1) << 22;
 
 size_t grs_scan_scratch_bytes(size_t n) { return 16 + 8 * ((n + kScanTileSmall - 1) / kScanTileSmall); }
 
-grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
-                                  uint32_t* d_total, void* d_scratch, size_t scratch_bytes,
-                                  void* stream) {
+}  // extern "C"
+
+// The one-pass scan.  err2 (nullable): a sorter's error word that a look-back timeout also
+// sets, so the internal callers (segmented sort, presorted exchange) surface GRS_ETIMEOUT
+// through grs_check_error / grs_stream_check_error like the sort passes.
+static grs_status scan_u32_impl(const uint32_t* d_in, uint32_t* d_out, size_t n, uint32_t* d_total,
+                                void* d_scratch, size_t scratch_bytes, void* stream,
+                                uint32_t* err2) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n > GRS_SCAN_MAX_N) return set_err(GRS_ECAPACITY, "grs_exclusive_scan_u32: n too large");
   if (n == 0) {
@@ -1218,12 +1225,20 @@ grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t 
   GRS_HIP(hipMemsetAsync(ctl, 0, 16 + 8 * static_cast<size_t>(tiles), st));
   if (large)
     hipLaunchKernelGGL(grs::grs_scan_onepass<32>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, st, d_in,
-                       d_out, n32, ctl, d_total);
+                       d_out, n32, ctl, d_total, err2);
   else
     hipLaunchKernelGGL(grs::grs_scan_onepass<8>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, st, d_in,
-                       d_out, n32, ctl, d_total);
+                       d_out, n32, ctl, d_total, err2);
   GRS_HIP(hipGetLastError());
   return GRS_OK;
+}
+
+extern "C" {
+
+grs_status grs_exclusive_scan_u32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                  uint32_t* d_total, void* d_scratch, size_t scratch_bytes,
+                                  void* stream) {
+  return scan_u32_impl(d_in, d_out, n, d_total, d_scratch, scratch_bytes, stream, nullptr);
 }
 
 grs_status grs_scan_check_error(const void* d_scratch, void* stream) {
@@ -1323,7 +1338,8 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
                        marks);
     if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
   }
-  if (r == GRS_OK) r = grs_exclusive_scan_u32(marks, excl, n, nullptr, scan_scratch, scan_bytes, stream);
+  if (r == GRS_OK)
+    r = scan_u32_impl(marks, excl, n, nullptr, scan_scratch, scan_bytes, stream, s->ctrl + GRS_CTRL_ERROR);
   if (r == GRS_OK) {
     hipLaunchKernelGGL(grs::grs_segment_compose, dim3(grid_for(n, 256)), dim3(256), 0, st,
                        static_cast<const uint32_t*>(d_keys), marks, excl, comp,
@@ -1332,6 +1348,11 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
   }
   // payload: the caller's values, or the marks buffer as a don't-care rider
   if (r == GRS_OK) r = grs_sort_bits(s->seg64, comp, d_vals ? d_vals : marks, n, 0, 32 + segbits, stream);
+  if (r == GRS_OK) {   // the inner sorter's look-back timeouts surface through this sorter's checks
+    hipLaunchKernelGGL(grs::grs_fold_error, dim3(1), dim3(64), 0, st, s->seg64->ctrl + GRS_CTRL_ERROR,
+                       s->ctrl + GRS_CTRL_ERROR);
+    if (hipGetLastError() != hipSuccess) r = set_err(GRS_EHIP, "grs_sort_segmented: launch");
+  }
   if (r == GRS_OK) {
     hipLaunchKernelGGL(grs::grs_segment_split, dim3(grid_for(n, 256)), dim3(256), 0, st, comp,
                        static_cast<uint32_t*>(d_keys), static_cast<uint64_t>(n));
@@ -1568,6 +1589,47 @@ grs_status xmark(grs_sorter* s, int k, hipStream_t st) {
   return GRS_OK;
 }
 
+// Pinned words of grs_sort_sharded's host read-back: G rows of at most 2G + 3 words.
+constexpr size_t kShardHostWords = 16 * (2 * 16 + 3) + 16;
+
+// The agreement before an exchange.  Each rank appends three words to the row it all-gathers
+// (its counts / sizes): its sticky error word and its receive capacity min(out_cap, capacity)
+// as two words.  Every rank then reads every row and takes the SAME decision -- a timeout or a
+// too-small receive side on any rank aborts all of them before any data moves (a rank that
+// returned alone would leave its peers waiting in the grouped send / recv for ever).
+grs_status append_verdict(grs_sorter* s, uint32_t* tail, size_t cap, hipStream_t st) {
+  GRS_HIP(hipMemcpyAsync(tail, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToDevice, st));
+  GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(tail + 1),
+                            static_cast<int>(static_cast<uint32_t>(cap)), 1, st));
+  GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(tail + 2),
+                            static_cast<int>(static_cast<uint32_t>(static_cast<uint64_t>(cap) >> 32)), 1, st));
+  return GRS_OK;
+}
+
+// rows: g rows of w words, the verdict in the last three; recv[r] = what rank r would receive.
+// GRS_OK, or the status every rank returns (the sticky error word is cleared on a timeout).
+grs_status read_verdict(grs_sorter* s, const uint32_t* rows, int g, int w, const uint64_t* recv,
+                        int me, hipStream_t st) {
+  bool err = false;
+  int short_rank = -1;
+  for (int r = 0; r < g; ++r) {
+    const uint32_t* v = rows + static_cast<size_t>(r) * w + (w - 3);
+    err |= v[0] != 0u;
+    const uint64_t cap = v[1] | (static_cast<uint64_t>(v[2]) << 32);
+    if (recv[r] > cap && (short_rank < 0 || r == me)) short_rank = r;
+  }
+  if (err) {
+    GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
+    return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a look-back spin exceeded its bound (on this "
+                                 "rank or a peer; every rank aborts before the exchange)");
+  }
+  if (short_rank >= 0)
+    return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run of rank " +
+                                      std::to_string(short_rank) + " (" + std::to_string(recv[short_rank]) +
+                                      " items) exceeds its out_capacity or sorter capacity");
+  return GRS_OK;
+}
+
 template <typename K, bool PAIRS, int N>
 grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uint32_t n, K* out_k,
                          uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
@@ -1577,8 +1639,9 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   // scratch: sk[S] | sp[S] | ak[G*S] | ap[G*S] | cnt[16] | mat[G*G] | digit, 256-B aligned parts
   auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
   const size_t gs = static_cast<size_t>(g) * S;
-  const size_t need = al(S * sizeof(K)) + al(S * 4) + al(gs * sizeof(K)) + al(gs * 4) + al(64) +
-                      al(static_cast<size_t>(g) * g * 4) + al(sizeof(Dig));
+  const int W = g + 3;   // words per rank in the count all-gather: counts + verdict
+  const size_t need = al(S * sizeof(K)) + al(S * 4) + al(gs * sizeof(K)) + al(gs * 4) + al(4 * W) +
+                      al(static_cast<size_t>(g) * W * 4) + al(sizeof(Dig));
   if (s->shard_bytes < need) {
     if (s->shard_buf) (void)hipFree(s->shard_buf);
     s->shard_buf = nullptr;
@@ -1589,7 +1652,7 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
     }
     s->shard_bytes = need;
   }
-  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), (16 * 32 + 4) * 4,
+  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), kShardHostWords * 4,
                                       hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     return set_err(GRS_ENOMEM, "grs_sort_sharded: pinned allocation failed");
@@ -1599,8 +1662,8 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   uint32_t* sp = reinterpret_cast<uint32_t*>(b);     b += al(S * 4);
   K* ak = reinterpret_cast<K*>(b);                   b += al(gs * sizeof(K));
   uint32_t* ap = reinterpret_cast<uint32_t*>(b);     b += al(gs * 4);
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(b);    b += al(64);
-  uint32_t* mat = reinterpret_cast<uint32_t*>(b);    b += al(static_cast<size_t>(g) * g * 4);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(b);    b += al(4 * W);
+  uint32_t* mat = reinterpret_cast<uint32_t*>(b);    b += al(static_cast<size_t>(g) * W * 4);
   Dig* dig = reinterpret_cast<Dig*>(b);
 
   if (xmark(s, 0, st) != GRS_OK) return GRS_EHIP;
@@ -1627,12 +1690,19 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   //    same.  Contiguous buckets are also the path when G * region reaches 2^32.
   //    (GRS_OPT_SHARDED_SEND = 2, a test hook: regions of n / (2G), so that full buckets spill
   //    and the redo path runs even on one rank)
-  const uint32_t region =
-      n == 0 ? 0u
-      : s->sharded_send == 2
-          ? std::max<uint32_t>(1u, n / (2u * static_cast<uint32_t>(g)))
-          : static_cast<uint32_t>(std::min<uint64_t>(n, static_cast<uint64_t>(n) * 5 / 4 / g + 65536));
-  bool regions = n > 0 && static_cast<uint64_t>(g) * region < (1ull << 32) && s->sharded_send != 1;
+  //    Every rank computes every rank's region from that rank's n (its row sum of the count
+  //    matrix), so all of them know whether any rank spilled (the options must agree).
+  auto region_of = [&](uint64_t nr) -> uint32_t {
+    return nr == 0 ? 0u
+         : s->sharded_send == 2
+             ? std::max<uint32_t>(1u, static_cast<uint32_t>(nr / (2u * static_cast<uint32_t>(g))))
+             : static_cast<uint32_t>(std::min<uint64_t>(nr, nr * 5 / 4 / g + 65536));
+  };
+  auto regions_of = [&](uint64_t nr) {
+    return nr > 0 && static_cast<uint64_t>(g) * region_of(nr) < (1ull << 32) && s->sharded_send != 1;
+  };
+  const uint32_t region = region_of(n);
+  bool regions = regions_of(n);
   K* send_k = static_cast<K*>(s->alt_keys);
   uint32_t* send_v = s->alt_vals;
   const size_t xitems = static_cast<size_t>(g - 1) * region + n;   // region-mode buffer items
@@ -1658,19 +1728,33 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   } else {
     GRS_HIP(hipMemsetAsync(cnt, 0, static_cast<size_t>(g) * 4, st));
   }
-  // 5-6. count matrix to every rank, then the one host synchronisation (counts + error word)
-  GRS_RCCL(ncclAllGather(cnt, mat, g, ncclUint32, comm, st));
-  GRS_HIP(hipMemcpyAsync(s->shard_host, mat, static_cast<size_t>(g) * g * 4, hipMemcpyDeviceToHost, st));
-  GRS_HIP(hipMemcpyAsync(s->shard_host + g * g, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st));
+  // 5-6. count matrix + every rank's verdict to every rank, then the one host synchronisation
+  if (append_verdict(s, cnt + g, std::min<size_t>(out_cap, s->capacity), st) != GRS_OK) return GRS_EHIP;
+  GRS_RCCL(ncclAllGather(cnt, mat, W, ncclUint32, comm, st));
+  GRS_HIP(hipMemcpyAsync(s->shard_host, mat, static_cast<size_t>(g) * W * 4, hipMemcpyDeviceToHost, st));
   GRS_HIP(hipStreamSynchronize(st));
-  if (s->shard_host[g * g] != 0) {
-    GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
-    return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a partition look-back spin exceeded its bound");
+  uint32_t* const h = s->shard_host;
+  uint64_t recv_tot[16] = {};
+  for (int r = 0; r < g; ++r)
+    for (int p = 0; p < g; ++p) recv_tot[p] += h[static_cast<size_t>(r) * W + p];
+  {
+    const grs_status v = read_verdict(s, h, g, W, recv_tot, me, st);
+    if (v != GRS_OK) return v;
   }
+  // the verdict words read, compact the rows into the G x G count matrix (row r moves down)
+  for (int r = 0; r < g; ++r)
+    for (int p = 0; p < g; ++p) h[r * g + p] = h[static_cast<size_t>(r) * W + p];
   uint64_t soff[16], roff[16], total = 0;
-  shard_plan(s->shard_host, g, me, soff, roff, &total);
-  bool spilled = false;
-  for (int p = 0; regions && p < g; ++p) spilled |= s->shard_host[me * g + p] > region;
+  shard_plan(h, g, me, soff, roff, &total);
+  bool spilled = false, spilled_any = false;
+  for (int r = 0; r < g; ++r) {
+    uint64_t nr = 0;
+    for (int p = 0; p < g; ++p) nr += h[r * g + p];
+    bool sp = false;
+    for (int p = 0; regions_of(nr) && p < g; ++p) sp |= h[r * g + p] > region_of(nr);
+    spilled_any |= sp;
+    if (r == me) spilled = sp;
+  }
   if (spilled) {   // a bucket outgrew its region: contiguous buckets instead (same counts)
     s->x_region_redo++;
     regions = false;
@@ -1679,20 +1763,24 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
     const grs_status r = run_partition_n<K, PAIRS, N>(s, keys, vals, send_k, send_v, n, Dig{}, dig,
                                                       g - 1, cnt, st, 0u);
     if (r != GRS_OK) return r;
-    // the redone partition's look-back must not have timed out before its buckets are sent
-    // (one more synchronisation, on this rare path only)
-    GRS_HIP(hipMemcpyAsync(s->shard_host + g * g, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st));
+  }
+  if (spilled_any) {
+    // the redone partitions' look-backs must not have timed out before their buckets are sent:
+    // every rank all-gathers its error word once more (this rare path only) and all decide alike
+    GRS_HIP(hipMemcpyAsync(cnt, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToDevice, st));
+    GRS_RCCL(ncclAllGather(cnt, mat, 1, ncclUint32, comm, st));
+    GRS_HIP(hipMemcpyAsync(h + g * g, mat, static_cast<size_t>(g) * 4, hipMemcpyDeviceToHost, st));
     GRS_HIP(hipStreamSynchronize(st));
-    if (s->shard_host[g * g] != 0) {
+    bool err = false;
+    for (int r = 0; r < g; ++r) err |= h[g * g + r] != 0u;
+    if (err) {
       GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
-      return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a partition look-back spin exceeded its bound");
+      return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a partition look-back spin exceeded its bound "
+                                   "(on this rank or a peer)");
     }
   }
   if (regions)
     for (int p = 0; p < g; ++p) soff[p] = static_cast<uint64_t>(p) * region;
-  if (total > out_cap || total > s->capacity)
-    return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
-                                      " items) exceeds out_capacity or the sorter capacity");
   // 7. exchange: keys and payload in one group; the self part is a device copy
   if (xmark(s, 1, st) != GRS_OK) return GRS_EHIP;
   GRS_RCCL(ncclGroupStart());
@@ -1798,13 +1886,12 @@ grs_status codec_encode(grs_sorter* s, const uint32_t* sorted, uint32_t n,
                      static_cast<uint32_t>(g), nb, cs.blk_words, cs.blk_meta);
   GRS_HIP(hipGetLastError());
   GRS_HIP(hipMemsetAsync(cs.blk_words + nb, 0, 4, st));
-  grs_status r = grs_exclusive_scan_u32(cs.blk_words, cs.blk_woff, nb + 1, nullptr, cs.scan,
-                                        cs.scan_bytes, st);
+  grs_status r = scan_u32_impl(cs.blk_words, cs.blk_woff, nb + 1, nullptr, cs.scan, cs.scan_bytes,
+                               st, s->ctrl + GRS_CTRL_ERROR);
   if (r != GRS_OK) return r;
   hipLaunchKernelGGL(grs::grs_codec_pack, grid, dim3(256), 0, st, sorted, cs.plan,
                      static_cast<uint32_t>(g), nb, cs.blk_meta, cs.blk_woff, send, cs.sizes);
   GRS_HIP(hipGetLastError());
-  (void)s;
   return GRS_OK;
 }
 
@@ -1907,10 +1994,12 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   const uint32_t S = static_cast<uint32_t>(grs_shard_samples_per_rank(g));
   auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
   const size_t gs = static_cast<size_t>(g) * S;
-  const size_t need = al(S * 4) + al(S * 4) + al(gs * 4) + al(gs * 4) + al(4 * 2 * g * g) + al(sizeof(Dig));
+  const int W = 2 * g + 3;   // words per rank in the size all-gather: (keys, words) + verdict
+  const size_t need = al(S * 4) + al(S * 4) + al(gs * 4) + al(gs * 4) + al(4 * static_cast<size_t>(g) * W) +
+                      al(4 * W) + al(sizeof(Dig));
   grs_status r = grow_buf(&s->shard_buf, &s->shard_bytes, need, "grs_sort_sharded: scratch");
   if (r != GRS_OK) return r;
-  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), (16 * 32 + 4) * 4,
+  if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), kShardHostWords * 4,
                                       hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     return set_err(GRS_ENOMEM, "grs_sort_sharded: pinned allocation failed");
@@ -1920,7 +2009,8 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   uint32_t* sp = reinterpret_cast<uint32_t*>(b);  b += al(S * 4);
   uint32_t* ak = reinterpret_cast<uint32_t*>(b);  b += al(gs * 4);
   uint32_t* ap = reinterpret_cast<uint32_t*>(b);  b += al(gs * 4);
-  uint32_t* mat = reinterpret_cast<uint32_t*>(b); b += al(4 * 2 * g * g);
+  uint32_t* mat = reinterpret_cast<uint32_t*>(b); b += al(4 * static_cast<size_t>(g) * W);
+  uint32_t* row = reinterpret_cast<uint32_t*>(b); b += al(4 * W);
   Dig* dig = reinterpret_cast<Dig*>(b);
   CodecScratch cs;
   if ((r = codec_scratch(s, n, s->capacity, g, &cs)) != GRS_OK) return r;
@@ -1946,16 +2036,23 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   GRS_HIP(hipGetLastError());
   // 4. bounds + encode
   if ((r = codec_encode<N>(s, out_k, n, dig, g, send, cs, st)) != GRS_OK) return r;
-  // 5. (keys, words) of every bucket of every rank, then the one host synchronisation
-  GRS_RCCL(ncclAllGather(cs.sizes, mat, 2 * g, ncclUint32, comm, st));
-  GRS_HIP(hipMemcpyAsync(s->shard_host, mat, 4 * 2 * g * g, hipMemcpyDeviceToHost, st));
-  GRS_HIP(hipMemcpyAsync(s->shard_host + 2 * g * g, s->ctrl + GRS_CTRL_ERROR, 4, hipMemcpyDeviceToHost, st));
+  // 5. (keys, words) of every bucket of every rank + every rank's verdict, then the one host
+  //    synchronisation
+  GRS_HIP(hipMemcpyAsync(row, cs.sizes, 4 * 2 * static_cast<size_t>(g), hipMemcpyDeviceToDevice, st));
+  if ((r = append_verdict(s, row + 2 * g, std::min<size_t>(out_cap, s->capacity), st)) != GRS_OK) return r;
+  GRS_RCCL(ncclAllGather(row, mat, W, ncclUint32, comm, st));
+  GRS_HIP(hipMemcpyAsync(s->shard_host, mat, 4 * static_cast<size_t>(g) * W, hipMemcpyDeviceToHost, st));
   GRS_HIP(hipStreamSynchronize(st));
-  const uint32_t* h = s->shard_host;
-  if (h[2 * g * g] != 0) {
-    GRS_HIP(hipMemsetAsync(s->ctrl + GRS_CTRL_ERROR, 0, 4, st));
-    return set_err(GRS_ETIMEOUT, "grs_sort_sharded: a look-back spin of the local sort exceeded its bound");
+  uint32_t* const h = s->shard_host;
+  {
+    uint64_t recv_tot[grs::kMaxRanks] = {};
+    for (int q = 0; q < g; ++q)
+      for (int p = 0; p < g; ++p) recv_tot[p] += h[static_cast<size_t>(q) * W + 2 * p];
+    if ((r = read_verdict(s, h, g, W, recv_tot, me, st)) != GRS_OK) return r;
   }
+  // compact the rows into the G x 2G matrix
+  for (int q = 0; q < g; ++q)
+    for (int p = 0; p < 2 * g; ++p) h[q * 2 * g + p] = h[static_cast<size_t>(q) * W + p];
   uint64_t soff[grs::kMaxRanks], roff[grs::kMaxRanks], total = 0, so = 0, ro = 0;
   uint32_t lens[grs::kMaxRanks];
   for (int p = 0; p < g; ++p) {
@@ -1966,9 +2063,6 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
     lens[p] = h[p * 2 * g + 2 * me];
     total += lens[p];
   }
-  if (total > out_cap || total > s->capacity)
-    return set_err(GRS_ECAPACITY, "grs_sort_sharded: the received run (" + std::to_string(total) +
-                                      " items) exceeds out_capacity or the sorter capacity");
   if ((r = grow_buf(&s->xrbuf, &s->xrbuf_bytes, std::max<size_t>(4 * ro, 4), "grs_sort_sharded: receive buffer")) != GRS_OK)
     return r;
   uint32_t* recv = static_cast<uint32_t*>(s->xrbuf);
@@ -2272,41 +2366,40 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
   return GRS_OK;
 }
 
-// The record sort's scratch (first use, grown on demand): keys | indices | record copy, laid
-// out for the sorter's CAPACITY, never for one call's n: the key and index buffers that
-// grs_records_key_buffers hands out sit at the same place whatever n a later call sorts (a
-// layout by n would put a smaller call's record copy over the caller's indices).  Growing
-// (a larger record size) frees the buffer, so it is refused while `held` (the caller's keys or
-// indices of this call) points into it.
-static grs_status records_scratch(grs_sorter* s, size_t record_bytes, void** keys, uint32_t** idx,
-                                  void** copy, const void* held0 = nullptr,
-                                  const void* held1 = nullptr) {
+// The record sort's scratch, two allocations so a small call never pays for the capacity:
+//  - rec_kbuf: the key and index buffers grs_records_key_buffers hands out, laid out for the
+//    sorter's CAPACITY (the same place whatever n a later call sorts) and independent of the
+//    record size, allocated on first use and never moved;
+//  - rec_buf: grown on demand to one call's needs -- grs_sort_records' own keys | indices |
+//    record copy, or grs_sort_records_by_keys' record copy.  It never aliases rec_kbuf, so the
+//    buffers a caller holds stay valid whatever record size a later call uses.
+static grs_status records_key_scratch(grs_sorter* s, void** keys, uint32_t** idx) {
   const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(s->capacity, 1);
-  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
-  const size_t need = al(cap * kb) + al(cap * 4) + al(cap * record_bytes);
-  if (s->rec_bytes < need) {
-    auto inside = [&](const void* p) {
-      const char* b = static_cast<const char*>(s->rec_buf);
-      return p && b && static_cast<const char*>(p) >= b && static_cast<const char*>(p) < b + s->rec_bytes;
-    };
-    if (inside(held0) || inside(held1))
-      return set_err(GRS_EINVAL, "grs_sort_records_by_keys: the record scratch must grow for this "
-                                 "record size while the key buffers passed live in it (call "
-                                 "grs_records_key_buffers with this record size first)");
-    if (s->rec_buf) (void)hipFree(s->rec_buf);
-    s->rec_buf = nullptr;
-    s->rec_bytes = 0;
-    if (hipMalloc(&s->rec_buf, need) != hipSuccess) {
+  const size_t koff = (cap * kb + 255) & ~static_cast<size_t>(255);
+  if (!s->rec_kbuf) {
+    if (hipMalloc(&s->rec_kbuf, koff + cap * 4) != hipSuccess) {
       (void)hipGetLastError();
-      return set_err(GRS_ENOMEM, "grs_sort_records: scratch allocation failed");
+      s->rec_kbuf = nullptr;
+      return set_err(GRS_ENOMEM, "grs_records_key_buffers: scratch allocation failed");
     }
-    s->rec_bytes = need;
   }
-  char* b = static_cast<char*>(s->rec_buf);
-  *keys = b;
-  *idx = reinterpret_cast<uint32_t*>(b + al(cap * kb));
-  *copy = b + al(cap * kb) + al(cap * 4);
+  *keys = s->rec_kbuf;
+  *idx = reinterpret_cast<uint32_t*>(static_cast<char*>(s->rec_kbuf) + koff);
+  return GRS_OK;
+}
+
+// rec_buf of at least `need` bytes (grown on demand; its contents are per call).
+static grs_status records_call_scratch(grs_sorter* s, size_t need) {
+  if (s->rec_bytes >= need) return GRS_OK;
+  if (s->rec_buf) (void)hipFree(s->rec_buf);
+  s->rec_buf = nullptr;
+  s->rec_bytes = 0;
+  if (hipMalloc(&s->rec_buf, need) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(GRS_ENOMEM, "grs_sort_records: scratch allocation failed");
+  }
+  s->rec_bytes = need;
   return GRS_OK;
 }
 
@@ -2320,8 +2413,7 @@ grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes,
   int prev = 0;
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
-  void* copy = nullptr;
-  const grs_status r = records_scratch(s, record_bytes, d_keys, d_idx, &copy);
+  const grs_status r = records_key_scratch(s, d_keys, d_idx);
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
 }
@@ -2339,11 +2431,10 @@ grs_status grs_sort_records_by_keys(grs_sorter* s, void* d_records, size_t n, si
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  void* keys = nullptr;
-  uint32_t* idx = nullptr;
-  void* copy = nullptr;
-  grs_status r = records_scratch(s, record_bytes, &keys, &idx, &copy, d_keys, d_idx);
-  // the caller's keys / indices may live in the scratch (grs_records_key_buffers) or anywhere
+  // the caller's keys / indices may live in rec_kbuf (grs_records_key_buffers) or anywhere;
+  // the record copy goes to rec_buf, sized for this call
+  grs_status r = records_call_scratch(s, n * record_bytes);
+  void* copy = s->rec_buf;
   if (r == GRS_OK) r = grs_sort(s, d_keys, d_idx, n, stream);                     // stable pairs
   if (r == GRS_OK) r = gather_records(d_records, copy, d_idx, n, record_bytes, stream,
                                       static_cast<uint32_t>(n - 1));  // K5
@@ -2371,10 +2462,13 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
   GRS_HIP(hipGetDevice(&prev));
   if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  void* keys = nullptr;
-  uint32_t* idx = nullptr;
-  void* copy = nullptr;
-  grs_status r = records_scratch(s, record_bytes, &keys, &idx, &copy);
+  // keys | indices | record copy, sized for this call
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  grs_status r = records_call_scratch(s, al(n * kb) + al(n * 4) + n * record_bytes);
+  char* rb = static_cast<char*>(s->rec_buf);
+  void* keys = rb;
+  uint32_t* idx = reinterpret_cast<uint32_t*>(rb + al(n * kb));
+  void* copy = rb + al(n * kb) + al(n * 4);
   const grs::KeyExtract kx{key->kind, key->offset, key->transform,
                            {key->lo[0], key->lo[1], key->lo[2]}, {key->hi[0], key->hi[1], key->hi[2]}};
   if (r == GRS_OK) {   // K1: one fused pre-pass, key + index

@@ -615,7 +615,7 @@ __device__ __forceinline__ void st_status64(unsigned long long* p, unsigned long
 // of 4 x 64 per round measured 0.74 against 0.48 ms at 2^28: the steady state finds an
 // inclusive prefix a few tiles back, and the wider rounds only add latency; tools/ab_scan.py.)
 __device__ __forceinline__ uint32_t scan_lookback(const unsigned long long* status, uint32_t tile,
-                                                  uint32_t lane, uint32_t* ctl) {
+                                                  uint32_t lane, uint32_t* ctl, uint32_t* err2) {
   constexpr unsigned long long INC = 2ull << 32;
   int32_t j = static_cast<int32_t>(tile) - 1;   // newest predecessor not yet summed
   uint32_t excl = 0, spins = 0;
@@ -638,7 +638,10 @@ __device__ __forceinline__ uint32_t scan_lookback(const unsigned long long* stat
       continue;
     }
     if (++spins > static_cast<uint32_t>(GRS_SPIN_LIMIT)) {   // prefix underestimated
-      if (lane == 0) atomicOr(ctl, 1u);
+      if (lane == 0) {
+        atomicOr(ctl, 1u);
+        if (err2 != nullptr) atomicOr(err2, 1u);   // an internal caller's sorter error word
+      }
       return excl;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -648,7 +651,7 @@ __device__ __forceinline__ uint32_t scan_lookback(const unsigned long long* stat
 template <int R>
 __global__ __launch_bounds__(GRS_SCAN_OP_BLOCK) void grs_scan_onepass(
     const uint32_t* in, uint32_t* out, uint32_t n,   // may alias (in place)
-    uint32_t* __restrict__ ctl, uint32_t* __restrict__ total) {
+    uint32_t* __restrict__ ctl, uint32_t* __restrict__ total, uint32_t* __restrict__ err2) {
   constexpr int B = GRS_SCAN_OP_BLOCK, W = B / GRS_WAVE;
   constexpr uint32_t ROW = 4 * GRS_WAVE, CHUNK = R * ROW, TILE = W * CHUNK;
   constexpr unsigned long long AGG = 1ull << 32, INC = 2ull << 32;
@@ -659,7 +662,8 @@ __global__ __launch_bounds__(GRS_SCAN_OP_BLOCK) void grs_scan_onepass(
   if (t == 0) s_tk = atomicAdd(ctl + 1, 1u);
   __syncthreads();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(s_tk);
-  const uint32_t tiles = (n + TILE - 1) / TILE;
+  // (n + TILE - 1) / TILE would wrap for n > 2^32 - TILE, and GRS_SCAN_MAX_N is above that
+  const uint32_t tiles = n / TILE + (n % TILE != 0u ? 1u : 0u);
   const uint32_t base = tile * TILE;
   const uint32_t valid = n - base;   // tile-local bound (base + TILE may pass 2^32)
   const uint32_t wbase = w * CHUNK;  // this wave's first item, tile-local
@@ -704,7 +708,7 @@ __global__ __launch_bounds__(GRS_SCAN_OP_BLOCK) void grs_scan_onepass(
       if (lane == 0) st_status64(status, INC | agg);
     } else {
       if (lane == 0) st_status64(status + tile, AGG | agg);
-      excl = scan_lookback(status, tile, lane, ctl);
+      excl = scan_lookback(status, tile, lane, ctl, err2);
       if (lane == 0) st_status64(status + tile, INC | static_cast<unsigned long long>(excl + agg));
     }
     if (lane == 0) {
@@ -1032,6 +1036,18 @@ __global__ void grs_segment_split(const uint64_t* __restrict__ comp, uint32_t* _
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
     keys[i] = static_cast<uint32_t>(comp[i]);
+}
+
+// *dst |= *src, then *src = 0: an inner sorter's sticky error word (a look-back timeout) moved
+// into the calling sorter's, which its checks read (grs_check_error, grs_stream_check_error).
+__global__ void grs_fold_error(uint32_t* __restrict__ src, uint32_t* __restrict__ dst) {
+  if (threadIdx.x == 0) {
+    const uint32_t e = *src;
+    if (e != 0u) {
+      atomicOr(dst, e);
+      *src = 0u;
+    }
+  }
 }
 
 // Adjacent-order check of the reference (ParallelSort.cpp:336-352), strengthened: counts

@@ -352,7 +352,8 @@ grs_status grs_key_transform(void* d_keys, size_t n, int key_bytes, int kind, in
  *                        offset + 4, offset + 8: each axis mapped to [0, 2^B) by
  *                        floor((v - lo) / (hi - lo) * 2^B), clamped (NaN -> 0), B = 10 for
  *                        u32 keys, 21 for u64; bits interleaved x-y-z from the top
- * Scratch (keys + index + one copy of the records) is allocated on first use and kept. */
+ * Scratch (keys + index + one copy of the records) is sized for the call, grown on demand and
+ * kept. */
 #define GRS_EXTRACT_FIELD 0
 #define GRS_EXTRACT_MORTON3 1
 typedef struct grs_key_extract {
@@ -371,9 +372,9 @@ grs_status grs_sort_records(grs_sorter* s, void* d_records, size_t n, size_t rec
  * before this call; the (key, index) pairs are sorted stably (both buffers are overwritten),
  * the records gathered by index and copied back, so d_records[0..n) ends up sorted in place.
  * grs_records_key_buffers hands out sorter-owned device buffers for the keys and indices,
- * laid out for the sorter's capacity (any n <= capacity may be sorted with them); they stay
- * valid until a record-sort call with a LARGER record size grows the scratch, which
- * grs_sort_records_by_keys refuses (GRS_EINVAL) while the buffers it is passed live in it.  The C++ template
+ * laid out for the sorter's capacity (any n <= capacity may be sorted with them; their own
+ * allocation, made on first use); they stay valid until grs_destroy.  The record copy of a
+ * call is a separate buffer sized for that call's n and record size.  The C++ template
  * grs::ParallelSortBy (grs_parallel_sort.hpp) wraps both around a __device__ key functor. */
 grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes, void** d_keys,
                                    uint32_t** d_idx);

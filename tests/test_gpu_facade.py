@@ -77,8 +77,9 @@ def test_record_sort_gathers_whole_records(gpu):
 def test_record_key_buffers_at_capacity_then_smaller_n(gpu):
     """grs_records_key_buffers hands out the sorter's key / index buffers once (at capacity);
     a later grs_sort_records_by_keys of FEWER records must not lay its record copy over those
-    buffers (the scratch layout follows the capacity, not the call's n), and growing the
-    scratch under them (a larger record size) is refused instead of freeing them."""
+    buffers (they are their own capacity-sized allocation; the record copy is sized per call),
+    and a larger record size grows only the per-call copy: the handed-out buffers stay where
+    they are and stay valid."""
     import ctypes
 
     import gpuradixsort_amd as grs
@@ -103,10 +104,21 @@ def test_record_key_buffers_at_capacity_then_smaller_n(gpu):
                                           idx_p, stream) == 0
         torch.cuda.synchronize()
         assert np.array_equal(d_rec.cpu().numpy(), rec[oracle.stable_argsort(keys)]), n
-    # a larger record size would grow (free) the scratch the key buffers live in: refused
-    d_big = torch.zeros((16, 64), dtype=torch.uint8, device=gpu)
-    assert L.grs_sort_records_by_keys(s._h, ctypes.c_void_p(d_big.data_ptr()), 16, 64, keys_p,
-                                      idx_p, stream) == 1   # GRS_EINVAL
+    # a larger record size grows only the per-call record copy; the key buffers do not move
+    n = 3001
+    big = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    keys = rng.integers(0, 1 << 8, n).astype(np.uint32)
+    d_big = torch.from_numpy(big).to(gpu)
+    d_keys = torch.from_numpy(keys).to(gpu)
+    assert L.grs_copy_u32(ctypes.c_void_p(d_keys.data_ptr()), keys_p, n, stream) == 0
+    assert L.grs_iota_u32(idx_p, n, 0, stream) == 0
+    assert L.grs_sort_records_by_keys(s._h, ctypes.c_void_p(d_big.data_ptr()), n, 64, keys_p,
+                                      idx_p, stream) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(d_big.cpu().numpy(), big[oracle.stable_argsort(keys)])
+    k2, i2 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.grs_records_key_buffers(s._h, cap, 64, ctypes.byref(k2), ctypes.byref(i2)) == 0
+    assert (k2.value, i2.value) == (keys_p.value, idx_p.value)
 
 
 @pytest.mark.parametrize("kb", [32, 64])

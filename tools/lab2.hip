@@ -706,6 +706,8 @@ int lab2_replay(int block, int items, int rb, int x8, const uint32_t* pre, uint3
   }
   RP(1024, 36, 8) RP(768, 64, 8) RP(1024, 32, 4) RP(1024, 48, 8) RP(1024, 16, 8) RP(1024, 40, 8)
   RP(768, 56, 8) RP(768, 60, 8)
+  // round 5: 3-pass u32 (11/11/10-bit digits) floors
+  RP(768, 64, 11) RP(1024, 36, 11) RP(1024, 48, 11) RP(768, 64, 10) RP(1024, 36, 10)
 #undef RP
   return -1;
 }
@@ -718,11 +720,11 @@ int lab2_scan2(int rows, const uint32_t* in, uint32_t* out, uint32_t n, uint32_t
   const uint32_t tiles = (n + TILE - 1) / TILE;
   if (hipMemsetAsync(ctl, 0, 16 + 8 * static_cast<size_t>(tiles), s) != hipSuccess) return -2;
   if (rows == 16)
-    hipLaunchKernelGGL(grs::grs_scan_onepass<16>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total);
+    hipLaunchKernelGGL(grs::grs_scan_onepass<16>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total, (uint32_t*)nullptr);
   else if (rows == 8)
-    hipLaunchKernelGGL(grs::grs_scan_onepass<8>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total);
+    hipLaunchKernelGGL(grs::grs_scan_onepass<8>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total, (uint32_t*)nullptr);
   else if (rows == 32)
-    hipLaunchKernelGGL(grs::grs_scan_onepass<32>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total);
+    hipLaunchKernelGGL(grs::grs_scan_onepass<32>, dim3(tiles), dim3(GRS_SCAN_OP_BLOCK), 0, s, in, out, n, ctl, total, (uint32_t*)nullptr);
   else
     return -1;
   return hipGetLastError() == hipSuccess ? 0 : -2;
