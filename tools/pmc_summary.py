@@ -1,4 +1,4 @@
-"""Summarise tools/pmc.sh output: one row per kernel dispatch (lab passes), counters merged."""
+"""Summarise the output of the PMC sessions (tools/plans/history_r1_r4.txt == pmc.sh ==): one row per kernel dispatch (lab passes), counters merged."""
 import collections
 import csv
 import glob
