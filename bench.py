@@ -1,4 +1,4 @@
-"""bench.py — Gkeys/s of the MI355X LSD radix sort (BASELINE.json metric).
+"""bench.py — Gkeys/s of the MI355X radix sort (BASELINE.json metric).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5|ns]
   (N > 1: torchrun --nproc-per-node N ... bench.py --gpus N ...; one rank per GPU, RCCL)
@@ -15,7 +15,9 @@ recv per peer over xGMI, decode, merge), beyond that the partition-first one (ra
 one RCCL all-to-all, local sort).  `value` = 2^30 keys x steps / wall time.
 
 Rank 0 prints ONE JSON line with the driver contract plus:
-  roofline      dominant kernel (the pass: grs_onesweep_v4, or v6 on small grids): algorithmic bytes per launch
+  roofline      dominant kernel (the LSD schedule's pass: grs_onesweep_v4, or v6 on small
+                grids; the MSD schedule's slowest of its two scatters and its LDS sort, each of
+                which reads and writes every key once): algorithmic bytes per launch
                 (n_local x 2 x (key + value bytes)) / its mean duration from
                 hipEvents recorded on the sort's stream during the timed steps; `traffic` is
                 the HBM bytes per launch that rocprofv3's FETCH_SIZE / WRITE_SIZE counters
@@ -78,8 +80,9 @@ def parse():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="sorter option (grs_set_option, gpuradixsort_amd._lib.OPTIONS) for A/B "
                          "runs; repeatable")
-    ap.add_argument("--pool-gib", type=float, default=96.0,
-                    help="HBM budget for the distinct per-step input buffers")
+    ap.add_argument("--pool-gib", type=float, default=160.0,
+                    help="HBM budget for the distinct per-step input buffers (the default holds "
+                         "warmup + steps C4 inputs of 4 GiB at the default 3 + 20 and 5 + 20)")
     return ap.parse_args()
 
 
@@ -177,8 +180,9 @@ def pmc_probe(a, options):
     s.check_error()
 
 
-def measure_traffic(a, config, options, n_local):
-    """HBM bytes per launch of the pass from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM):
+def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
+    """HBM bytes per launch of the roofline kernel (the pass, or the MSD schedule's dominant
+    kernel; names match by prefix) from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM):
     one counter per rocprofv3 run (FETCH_SIZE, then WRITE_SIZE) over a child --pmc-probe run;
     each counter is corrected by known bytes / counter bytes of the calibration copy, which
     issues the pass's own access width (one dword per lane).  Returns (dict, None) or
@@ -219,7 +223,7 @@ def measure_traffic(a, config, options, n_local):
                     if r["Counter_Name"] != ctr:
                         continue
                     name = r["Kernel_Name"]
-                    if "grs_onesweep_v" in name:
+                    if kernel in name:
                         vals["pass"].append(float(r["Counter_Value"]) * 1024.0)   # KiB -> bytes
                     elif "grs_copy_u32" in name:
                         vals["cal"].append(float(r["Counter_Value"]) * 1024.0)
@@ -330,10 +334,23 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     barrier()
     (sorter.sorter if sharded else sorter).check_error()
     tims = [sorter.timing(k) for k in range(nprof)]
-    pass_ms = [p for t in tims for p in t["pass_ms"]]
-    mean_pass_ms = sum(pass_ms) / len(pass_ms)
     hist_ms = sum(t["hist_ms"] for t in tims) / len(tims)
     sort_ms = sum(t["total_ms"] for t in tims) / len(tims)
+    msd = tims[0].get("kind") == "msd"
+    msd_phases = None
+    if msd:
+        # the MSD schedule (grs_msd.hpp): H1 | P1 top-byte scatter, H2, P2 byte-2 scatter, P3
+        # LDS sort of the 16-bit segments, fallback; each of P1 / P2 / P3 reads and writes every
+        # key once, so the dominant one of them is the roofline kernel
+        names = ["p1_scatter_top_byte", "h2_hist_byte2", "p2_scatter_byte2", "p3_local_sort",
+                 "fallback"]
+        msd_phases = {nm: round(sum(t["pass_ms"][i] for t in tims) / len(tims), 5)
+                      for i, nm in enumerate(names)}
+        dom = max(("p1_scatter_top_byte", "p2_scatter_byte2", "p3_local_sort"), key=msd_phases.get)
+        mean_pass_ms = msd_phases[dom]
+    else:
+        pass_ms = [p for t in tims for p in t["pass_ms"]]
+        mean_pass_ms = sum(pass_ms) / len(pass_ms)
     # the exchange grs_sort_sharded took (include/grs.h): presorted = local sort of the shard
     # first, then the encoded exchange and a merge; partition-first = local sort of the received
     # run.  Its phases of the last step, with the xGMI bytes and rate of this rank
@@ -343,9 +360,13 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         exchange = xt["exchange"]
     n_sorted_local = sorter.last_n_out if exchange == "partition-first" else n_local
     kernel_name = (sorter.sorter if sharded else sorter).pass_kernel_for(n_sorted_local)
+    if msd:
+        kernel_name = {"p1_scatter_top_byte": kernel_name, "p2_scatter_byte2": "grs_onesweep_seg",
+                       "p3_local_sort": "grs_msd_local"}[dom]
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
-    passes = tims[0]["passes"]
+    # SURVEY §8d credits P_cfg = key bits / digit bits passes, whatever schedule ran
+    passes = kb // rb
     del keys_pool, vals_pool, sorter
     torch.cuda.empty_cache()
 
@@ -356,7 +377,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     # PMC bytes per launch: rocprofv3 child runs of this workload (after the timed region)
     traffic, traffic_info = None, None
     if rank == 0 and world == 1 and not sharded and not a.no_traffic:
-        traffic_info, why = measure_traffic(a, config, options, n_local)
+        traffic_info, why = measure_traffic(a, config, options, n_local, kernel_name)
         if traffic_info:
             traffic = traffic_info["bytes_per_launch"]
         else:
@@ -394,8 +415,12 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         "cpu_baseline": cpu,
         "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
                       "sort_total_gpu": round(sort_ms, 5)},
+        "schedule": "msd" if msd else "lsd",
         "check": {"inversions_last_step": inversions},
     }
+    if msd:
+        out["phases_ms"]["msd"] = msd_phases
+        out["config"]["passes"] = f"{passes} (credited, SURVEY §8d); MSD schedule: 2 scatters + LDS sort"
     if options:
         out["config"]["options"] = options
     if traffic_info:
@@ -445,7 +470,7 @@ def main():
         if out is not None and ns is not None:
             out["north_star"] = {k: ns[k] for k in ("value", "unit", "ms_per_step", "steps",
                                                     "warmup", "roofline", "sort_roofline",
-                                                    "phases_ms", "check")}
+                                                    "phases_ms", "check", "schedule")}
             out["north_star"]["config"] = ns["config"]
             if "traffic_pmc" in ns:
                 out["north_star"]["traffic_pmc"] = ns["traffic_pmc"]

@@ -35,7 +35,7 @@ class GrsError(RuntimeError):
 
 class grs_timing(ctypes.Structure):
     _fields_ = [("passes", c_int), ("total_ms", c_float), ("hist_ms", c_float),
-                ("pass_ms", c_float * 16), ("copy_ms", c_float)]
+                ("pass_ms", c_float * 16), ("copy_ms", c_float), ("kind", c_int)]
 
 
 class grs_sharded_timing(ctypes.Structure):
@@ -64,6 +64,7 @@ OPTIONS = {
     "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
     "merge": (9, {"rounds": 0, "kway": 1}),
     "fault_tile": (10, {"off": -1}),   # test hook: tile v of every pass never publishes
+    "msd": (11, {"size": -1, "never": 0, "always": 1}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares

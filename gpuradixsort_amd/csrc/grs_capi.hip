@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +23,7 @@
 #include "grs_config.h"
 #include "grs_kernels.hpp"
 #include "grs_pass.hpp"
+#include "grs_msd.hpp"
 #include "grs_shard.hpp"
 #include "grs_codec.hpp"
 
@@ -261,7 +263,7 @@ struct grs_sorter {
   int ring = 0;
   long long calls = 0;             // profiled calls recorded so far
   hipEvent_t* ev = nullptr;        // ring * EV_PER_CALL events
-  struct CallInfo { int ev_used; int passes; bool copy; };
+  struct CallInfo { int ev_used; int passes; bool copy; int kind = 0; };   // kind 1: MSD
   CallInfo* info = nullptr;        // ring entries
   // grs_sort_segmented scratch (allocated on first use, grown on demand)
   void* seg_buf = nullptr;
@@ -300,6 +302,9 @@ struct grs_sorter {
   int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
+  int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies
+  void* msd_buf = nullptr;         // the MSD sort's tables (u32 keys without payload, 8-bit)
+  size_t msd_bytes = 0;
 };
 
 extern "C" {
@@ -343,6 +348,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->xbuf) (void)hipFree(s->xbuf);
   if (s->xrbuf) (void)hipFree(s->xrbuf);
   if (s->codec_buf) (void)hipFree(s->codec_buf);
+  if (s->msd_buf) (void)hipFree(s->msd_buf);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   for (hipEvent_t e : s->xev)
@@ -382,6 +388,58 @@ bool use_xl(const grs_sorter* s, size_t n, size_t xl_tile) {
          (n + xl_tile - 1) / xl_tile >= 32u * static_cast<size_t>(std::max(1, s->cus));
 }
 
+// ---- MSD u32 sort (grs_msd.hpp): tables and their layout in the sorter's msd_buf ----
+// P3 shapes: one workgroup sorts a 16-bit segment of up to BLOCK * I keys in LDS.
+struct MsdLocalA { static constexpr int BLOCK = 256, I = 20; static constexpr bool C16 = false; };
+struct MsdLocalB { static constexpr int BLOCK = 512, I = 20; static constexpr bool C16 = false; };
+struct MsdLocalC { static constexpr int BLOCK = 768, I = 24; static constexpr bool C16 = true; };
+constexpr uint32_t kMsdSmaxMin = MsdLocalA::BLOCK * MsdLocalA::I;
+// fallback passes (segments longer than P3 takes): the big tile, persistent
+using MsdFallTile = BigTile<uint32_t, false>;
+constexpr uint32_t kMsdTileF = MsdFallTile::TILE;
+
+struct MsdLayout {   // word offsets into msd_buf
+  size_t h2, big, dstart, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
+  size_t r2, rf, bl, mr;   // capacities: P2 records, fallback records, big list, histogram rows
+  static MsdLayout of(size_t cap) {
+    MsdLayout L{};
+    cap = std::max<size_t>(cap, 1);
+    L.r2 = cap / std::min(BigTile<uint32_t, false>::TILE, XLTile<uint32_t, false>::TILE) + 257;
+    L.bl = std::min<size_t>(65536, cap / (kMsdSmaxMin + 1) + 2);
+    L.mr = cap / (kMsdTileF + 1) + 2;
+    L.rf = cap / kMsdTileF + L.bl + 1;
+    size_t o = 0;
+    auto take = [&](size_t w) { const size_t at = o; o += (w + 63) & ~static_cast<size_t>(63); return at; };
+    L.h2 = take(65536 + 64);   // h2 | big counters: zeroed together by H1
+    L.big = L.h2 + 65536;
+    L.dstart = take(65536);
+    L.hdr2 = take(4);
+    L.rec2 = take(L.r2 * 8);
+    L.hdrf = take(4);
+    L.recf = take(L.rf * 8);
+    L.bstart = take(L.bl);
+    L.blen = take(L.bl);
+    L.brow = take(L.bl);
+    L.rows = take(L.mr * 512);
+    L.spill = take(6 * (L.bl + 1));
+    L.words = o;
+    return L;
+  }
+  // status words of P2 (256 buckets) and of the fallback passes
+  static size_t status_words(size_t cap) {
+    cap = std::max<size_t>(cap, 1);
+    const size_t t2 = cap / BigTile<uint32_t, false>::TILE + 257;
+    const size_t w2 = (t2 + 2 * (t2 / GRS_LB_GROUP + 257)) * 256;
+    const size_t tf = 2 * (cap / kMsdTileF) + 2;            // tiles of multi-tile segments
+    const size_t gf = tf / GRS_LB_GROUP + cap / (kMsdTileF + 1) + 2;
+    return std::max(w2, (tf + 2 * gf) * 256);
+  }
+};
+
+bool msd_type(const grs_sorter* s) {
+  return s->key_type == GRS_KEY_U32 && !s->pairs && s->radix_bits == 8;
+}
+
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
 template <typename K, bool PAIRS>
 size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
@@ -405,7 +463,8 @@ size_t needed_status_words(const grs_sorter* s) {
   const size_t radix = std::max<size_t>(size_t(1) << s->radix_bits, 16);
   if (s->key_type == GRS_KEY_U32)
     return s->pairs ? max_status_words<uint32_t, true>(s, cap, radix)
-                    : max_status_words<uint32_t, false>(s, cap, radix);
+                    : std::max(max_status_words<uint32_t, false>(s, cap, radix),
+                               msd_type(s) ? MsdLayout::status_words(cap) : size_t(0));
   return s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
                   : max_status_words<uint64_t, false>(s, cap, radix);
 }
@@ -469,6 +528,10 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value < 0 || value > 1) return bad();
       s->merge_mode = value;
       break;
+    case GRS_OPT_MSD:
+      if (value < -1 || value > 1) return bad();
+      s->msd_mode = value;
+      break;
 
     default:
       return set_err(GRS_EINVAL, "grs_set_option: unknown option");
@@ -507,6 +570,7 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_EXCHANGE: *value = s->sharded_exchange; break;
     case GRS_OPT_MERGE: *value = s->merge_mode; break;
     case GRS_OPT_FAULT_TILE: *value = s->fault_tile; break;
+    case GRS_OPT_MSD: *value = s->msd_mode; break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -563,6 +627,10 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
     if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
   }
   alloc(reinterpret_cast<void**>(&s->status), 2 * s->status_words * 4);
+  if (msd_type(s)) {
+    s->msd_bytes = MsdLayout::of(cap).words * 4;
+    alloc(&s->msd_buf, s->msd_bytes);
+  }
   alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
   alloc(reinterpret_cast<void**>(&s->ctrl2), GRS_CTRL_ERROR * 4);
   if (st == GRS_OK && (hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess ||
@@ -725,7 +793,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     auto kern = full ? grs::grs_upfront_hist2<K, RB, true> : grs::grs_upfront_hist2<K, RB, false>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(grs::Hist2Layout<K>::BLOCK), 0, stream,
                        src_in ? src_in : keys, n, begin_bit, end_bit, passes, hist, st0,
-                       static_cast<uint32_t>(words), hist_next);
+                       static_cast<uint32_t>(words), hist_next, (uint32_t*)nullptr, 0u);
     GRS_HIP(hipGetLastError());
   }
   s->cb_i ^= 1;   // the next call's block (zero once this call's histogram kernel has run)
@@ -812,10 +880,168 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     if ((r = mark()) != GRS_OK) return r;
   }
   if (evs) {
-    s->info[s->calls % s->ring] = {ev, passes, copy};
+    s->info[s->calls % s->ring] = {ev, passes, copy, 0};
     ++s->calls;
   }
   return GRS_OK;
+}
+
+// ---- MSD-first u32 sort (grs_msd.hpp) ----
+// The P3 shape for n keys: a uniform 16-bit segment holds m = n / 65536 keys, +- sqrt(m); the
+// shape must take m + 8 sqrt(m) + 64 (longer segments take the segmented fallback).  0: none
+// fits (n above ~2^30.07): the LSD sort.
+int msd_local_shape(size_t n) {
+  const double m = static_cast<double>(n) / 65536.0;
+  const double need = m + 8.0 * std::sqrt(m) + 64.0;
+  if (need <= MsdLocalA::BLOCK * MsdLocalA::I) return 1;
+  if (need <= MsdLocalB::BLOCK * MsdLocalB::I) return 2;
+  if (need <= MsdLocalC::BLOCK * MsdLocalC::I) return 3;
+  return 0;
+}
+// From this many keys the MSD sort is the default (GRS_OPT_MSD = -1).
+constexpr size_t kMsdMinN = size_t(1) << 26;
+
+bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
+  if (!msd_type(s) || s->msd_mode == 0 || s->msd_buf == nullptr || s->rank_mode != 0) return false;
+  if (begin_bit != 0 || end_bit != 32 || msd_local_shape(n) == 0) return false;
+  return s->msd_mode == 1 || n >= kMsdMinN;
+}
+
+// H1 -> P1 -> H2 (+ P2's plan) -> P2 -> P3 -> fallback (plan, histograms, two segmented LSD
+// passes over the segments P3 left; persistent grids that leave at once when there are none).
+// src_in (out of place): H1 and P1 read it; the result lands in keys either way.
+template <typename P3C>
+grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream,
+                   const uint32_t* src_in) {
+  using Big = BigTile<uint32_t, false>;
+  using XL = XLTile<uint32_t, false>;
+  using Small = SmallTile<uint32_t, false>;
+  using Dig = grs::RadixDigit<uint32_t>;
+  constexpr uint32_t G = GRS_LB_GROUP;
+  const bool big = use_big_tiles(s, n, Big::TILE);
+  const bool xl = big && use_xl(s, n, XL::TILE);
+  const uint32_t tile1 = xl ? XL::TILE : big ? Big::TILE : Small::TILE;
+  const size_t words1 = status_words_for((n + tile1 - 1) / tile1, 256);
+  const uint32_t tile2 = xl ? XL::TILE : Big::TILE;
+  const size_t t2 = n / tile2 + 257;
+  const size_t words2 = (t2 + 2 * (t2 / G + 257)) * 256;
+  if (words1 > s->status_words || words2 > s->status_words)
+    return set_err(GRS_ECAPACITY, "status buffer too small");
+  const MsdLayout L = MsdLayout::of(s->capacity);
+  if (t2 > L.r2) return set_err(GRS_ECAPACITY, "internal: MSD plan capacity");
+  uint32_t* const mb = static_cast<uint32_t*>(s->msd_buf);
+  uint32_t* const h2 = mb + L.h2;
+  uint32_t* const bigc = mb + L.big;
+  uint32_t* const dstart = mb + L.dstart;
+  uint32_t* const hdr2 = mb + L.hdr2;
+  auto* const rec2 = reinterpret_cast<grs::SegTile*>(mb + L.rec2);
+  uint32_t* const hdrf = mb + L.hdrf;
+  auto* const recf = reinterpret_cast<grs::SegTile*>(mb + L.recf);
+  uint32_t* const st0 = s->status;
+  uint32_t* const st1 = s->status + s->status_words;
+  uint32_t* const err = s->ctrl + GRS_CTRL_ERROR;
+  uint32_t* const cb[2] = {s->ctrl, s->ctrl2};
+  uint32_t* const hist = cb[s->cb_i];
+  uint32_t* const tickets = hist + GRS_CTRL_TICKETS;
+  uint32_t* const hist_next = cb[s->cb_i ^ 1];
+  const uint32_t* src = src_in ? src_in : keys;
+  uint32_t* const alt = static_cast<uint32_t*>(s->alt_keys);
+  int ev = 0;
+  hipEvent_t* evs = s->ring ? s->ev + (s->calls % s->ring) * grs_sorter::EV_PER_CALL : nullptr;
+  auto mark = [&]() -> grs_status {
+    if (evs) GRS_HIP(hipEventRecord(evs[ev++], stream));
+    return GRS_OK;
+  };
+  grs_status r;
+  if ((r = mark()) != GRS_OK) return r;
+  if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
+  s->cb_dirty = false;
+  {  // H1: the top byte's histogram; zeroes P1's status, the next call's control block, h2 and
+     // the big-segment counters
+    const int slots = grs::Hist2Layout<uint32_t>::PER_CU * s->cus;
+    const int need = static_cast<int>(n >> grs::kHist2GridShift<uint32_t>) + 1;
+    int grid = n <= (1u << 25) ? s->cus : slots;
+    if (grid < need) grid = (need + slots - 1) / slots * slots;
+    hipLaunchKernelGGL((grs::grs_upfront_hist2<uint32_t, 8, false, 1>), dim3(grid),
+                       dim3(grs::Hist2Layout<uint32_t>::BLOCK), 0, stream, src, n, 24, 32, 1, hist,
+                       st0, static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u);
+    GRS_HIP(hipGetLastError());
+  }
+  s->cb_i ^= 1;
+  if ((r = mark()) != GRS_OK) return r;
+  // P1: stable scatter by the top byte (the LSD pass kernel), src -> alt
+  const Dig d1{24, 255u};
+  r = xl ? launch_pass<uint32_t, false, 8, XL, XL::OPT>(s, src, alt, nullptr, nullptr, n, d1, (const Dig*)nullptr, hist, tickets, st0, st1, stream, tile1)
+     : big ? launch_pass<uint32_t, false, 8, Big, Big::OPT>(s, src, alt, nullptr, nullptr, n, d1, (const Dig*)nullptr, hist, tickets, st0, st1, stream, tile1)
+           : launch_pass<uint32_t, false, 8, Small, kSmallOpt>(s, src, alt, nullptr, nullptr, n, d1, (const Dig*)nullptr, hist, tickets, st0, st1, stream, tile1);
+  if (r != GRS_OK) return r;
+  if ((r = mark()) != GRS_OK) return r;
+  // H2: byte-2 histogram per top-byte bucket over alt; zeroes P2's status; plans P2's tiles
+  {
+    const dim3 grid((n + GRS_H2_CHUNK - 1) / GRS_H2_CHUNK);
+    if (xl)
+      hipLaunchKernelGGL((grs::grs_msd_hist2<XL::TILE>), grid, dim3(1024), 0, stream, alt, n, h2, st1,
+                         static_cast<uint32_t>(words2), hist, rec2, hdr2);
+    else
+      hipLaunchKernelGGL((grs::grs_msd_hist2<Big::TILE>), grid, dim3(1024), 0, stream, alt, n, h2, st1,
+                         static_cast<uint32_t>(words2), hist, rec2, hdr2);
+    GRS_HIP(hipGetLastError());
+  }
+  if ((r = mark()) != GRS_OK) return r;
+  // P2: stable scatter by byte 2 inside each top-byte bucket, alt -> keys; each bucket's first
+  // tile writes where its 256 16-bit segments start (dstart)
+  {
+    const Dig d2{16, 255u};
+    const dim3 grid(static_cast<uint32_t>(t2));
+    if (xl)
+      hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, XL::BLOCK, XL::ITEMS, XL::MINW, XL::OPT, false>),
+                         grid, dim3(XL::BLOCK), 0, stream, alt, keys, nullptr, nullptr, d2, rec2, hdr2, h2,
+                         256u, tickets + GRS_XCDS, st1, st0, err, dstart);
+    else
+      hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, Big::BLOCK, Big::ITEMS, Big::MINW, Big::OPT, false>),
+                         grid, dim3(Big::BLOCK), 0, stream, alt, keys, nullptr, nullptr, d2, rec2, hdr2, h2,
+                         256u, tickets + GRS_XCDS, st1, st0, err, dstart);
+    GRS_HIP(hipGetLastError());
+  }
+  if ((r = mark()) != GRS_OK) return r;
+  // P3: every 16-bit segment sorted by its low 16 bits in LDS, in place; longer ones listed
+  hipLaunchKernelGGL((grs::grs_msd_local<P3C::BLOCK, P3C::I, P3C::C16, kMsdTileF>), dim3(65536),
+                     dim3(P3C::BLOCK), 0, stream, keys, h2, dstart, bigc, mb + L.bstart, mb + L.blen,
+                     mb + L.brow, mb + L.rows);
+  GRS_HIP(hipGetLastError());
+  if ((r = mark()) != GRS_OK) return r;
+  // fallback: the listed segments by a segmented LSD on bits 0..15 (keys -> alt -> keys)
+  hipLaunchKernelGGL((grs::grs_seg_plan<kMsdTileF, grs::kSegList>), dim3(1), dim3(1024), 0, stream,
+                     mb + L.bstart, mb + L.blen, mb + L.brow, 0u, bigc, mb + L.spill, recf, hdrf);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_seg_hist<uint32_t, 2>), dim3(2 * s->cus), dim3(256), 0, stream, keys,
+                     recf, hdrf, 0, mb + L.rows, st0, 256u);
+  GRS_HIP(hipGetLastError());
+  using FT = MsdFallTile;
+  hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
+                     dim3(s->cus), dim3(FT::BLOCK), 0, stream, keys, alt, nullptr, nullptr, Dig{0, 255u},
+                     recf, hdrf, mb + L.rows, 512u, tickets + 2 * GRS_XCDS, st0, st1, err, nullptr);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
+                     dim3(s->cus), dim3(FT::BLOCK), 0, stream, alt, keys, nullptr, nullptr, Dig{8, 255u},
+                     recf, hdrf, mb + L.rows + 256, 512u, tickets + 3 * GRS_XCDS, st1, st0, err, nullptr);
+  GRS_HIP(hipGetLastError());
+  if ((r = mark()) != GRS_OK) return r;
+  if (evs) {
+    s->info[s->calls % s->ring] = {ev, 5, false, 1};
+    ++s->calls;
+  }
+  return GRS_OK;
+}
+
+grs_status run_sort_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream,
+                        const uint32_t* src_in = nullptr) {
+  switch (msd_local_shape(n)) {
+    case 1: return run_msd<MsdLocalA>(s, keys, n, stream, src_in);
+    case 2: return run_msd<MsdLocalB>(s, keys, n, stream, src_in);
+    case 3: return run_msd<MsdLocalC>(s, keys, n, stream, src_in);
+    default: return set_err(GRS_EINVAL, "internal: no MSD shape for this n");
+  }
 }
 
 // Stable key-range partition with N (compile-time) splitters: one bucket histogram + one pass
@@ -993,7 +1219,9 @@ grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n
   const uint32_t n32 = static_cast<uint32_t>(n);
   grs_status r = GRS_EINVAL;
   const bool u64 = s->key_type == GRS_KEY_U64;
-  if (!u64 && !s->pairs && s->radix_bits == 8)
+  if (!u64 && !s->pairs && s->radix_bits == 8 && use_msd(s, n, begin_bit, end_bit))
+    r = run_sort_msd(s, (uint32_t*)d_keys, n32, st);
+  else if (!u64 && !s->pairs && s->radix_bits == 8)
     r = run_sort<uint32_t, false, 8>(s, (uint32_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
   else if (!u64 && !s->pairs && s->radix_bits == 4)
     r = run_sort<uint32_t, false, 4>(s, (uint32_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
@@ -1028,6 +1256,7 @@ grs_status grs_timing_history(grs_sorter* s, int k, grs_timing* out) {
   hipEvent_t* e = s->ev + slot * grs_sorter::EV_PER_CALL;
   GRS_HIP(hipEventSynchronize(e[ci.ev_used - 1]));
   out->passes = ci.passes;
+  out->kind = ci.kind;
   float ms = 0;
   GRS_HIP(hipEventElapsedTime(&ms, e[0], e[1]));
   out->hist_ms = ms;

@@ -176,7 +176,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 // keys:       n keys (the unsorted input)
 // g_hist:     [passes][RADIX] uint32 counters, zeroed by the caller (control-block memset)
 // clear/cw:   status buffer of pass 0, zeroed here (grid-stride) so no separate memset
-//             launch is needed.
+//             launch is needed; clear2: a second region (the MSD sort's counters).
 //
 // Counting always happens on 8-bit "super digits"; 4-bit passes (BASELINE C2) read their
 // counts off them: pass 2q's digit is the low nibble of super digit q, pass 2q+1's the high
@@ -217,7 +217,8 @@ template <typename K, int RB, bool FULL, int QN = Hist2Layout<K>::MAXQ>
 __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     const K* __restrict__ keys, uint32_t n, int begin_bit, int end_bit, int passes,
     uint32_t* __restrict__ g_hist, uint32_t* __restrict__ clear, uint32_t clear_words,
-    uint32_t* __restrict__ clear_ctrl = nullptr) {
+    uint32_t* __restrict__ clear_ctrl = nullptr, uint32_t* __restrict__ clear2 = nullptr,
+    uint32_t clear2_words = 0) {
   static_assert(RB == 4 || RB == 8, "4- or 8-bit digits");
   using HL = Hist2Layout<K>;
   constexpr int MAXQ = HL::MAXQ;
@@ -232,6 +233,8 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
     for (uint32_t i = t; i < HL::WORDS / 4; i += HB) z[i] = make_uint4(0, 0, 0, 0);
   }
   for (uint32_t i = blockIdx.x * HB + t; i < clear_words; i += gridDim.x * HB) clear[i] = 0;
+  // (the MSD sort: its byte-2 histogram and big-segment counters, grs_msd.hpp)
+  for (uint32_t i = blockIdx.x * HB + t; i < clear2_words; i += gridDim.x * HB) clear2[i] = 0;
   // the next sort's control block: its histograms (every row) and its tickets
   if (clear_ctrl != nullptr) {
     constexpr uint32_t H = GRS_CTRL_HIST_WORDS, TK = GRS_MAX_PASSES * GRS_XCDS;

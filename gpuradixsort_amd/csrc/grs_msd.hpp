@@ -1,0 +1,386 @@
+// grs_msd.hpp — the MSD-first u32 sort and the segment-table kernels of libgrs (gfx950).
+//
+// The reference sorts with 32 stable one-bit LSD splits (ParallelSort.cpp:236-298), and the
+// LSD path of this library (grs_pass.hpp) with 4 stable 8-bit scatter passes.  A scatter pass
+// costs what its digit runs cost: 256 runs per tile, the boundary lines two tiles share, 0.56
+// of 8 TB/s at the floor of its own loads and stores.  For u32 keys, two
+// stable MSD scatters already sort the keys by their top 16 bits into 65536 segments of
+// ~n / 65536 keys, which one workgroup can finish in LDS with contiguous HBM traffic:
+//
+//   H1  grs_upfront_hist2<.., QN = 1>   top-byte histogram (one LDS add per key)
+//   P1  grs_onesweep_v4                 stable scatter by bits 24..31          keys -> alt
+//   H2  grs_msd_hist2                   per top-byte bucket, the byte-2 histogram (65536 bins)
+//                                       over P1's output (a block meets 1-2 buckets: LDS);
+//                                       block 0 also plans P2's tiles (grs_seg_plan_block)
+//   P2  grs_onesweep_seg                stable scatter by bits 16..23 inside each bucket
+//                                                                              alt -> keys
+//   P3  grs_msd_local                   one workgroup per 16-bit prefix: its keys read once,
+//                                       sorted by bits 0..15 in LDS (two lane-ordered 8-bit
+//                                       rounds, as the pass ranks), written once, in place
+//
+// Stable scatters and a stable LDS sort: equal keys keep their input order, so the output is
+// the reference's (the stable sort by key).  A 16-bit segment longer than P3's LDS capacity is
+// appended to a list instead, and sorted by a segmented LSD on bits 0..15 over the listed
+// segments only (grs_seg_plan -> grs_seg_hist -> 2 x grs_onesweep_seg, persistent grids that
+// leave at once when the list is empty): skewed inputs stay correct and pay only for the
+// segments that need it.
+#pragma once
+
+#include "grs_kernels.hpp"
+#include "grs_pass.hpp"
+
+namespace grs {
+
+// ---------------------------------------------------------------------------------------
+// segment tables: one SegTile per tile of a segmented pass
+// ---------------------------------------------------------------------------------------
+// Segment sources of a plan: sizes (starts are their exclusive scan: the buckets of a pass),
+// explicit (start, length) lists, or offsets (num + 1 words, segment i = [off[i], off[i+1])).
+enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2 };
+
+// LDS of the planner: 6 words per segment (tile, row and group prefixes, start, length,
+// histogram row); larger tables keep them in global scratch (`spill`, 6 * (nseg + 1) words).
+#define GRS_PLAN_LDS_SEGS 2048
+#define GRS_PLAN_LDS_WORDS (6 * GRS_PLAN_LDS_SEGS + 4 * 16)
+
+// Block exclusive scan of NV values per thread over BLOCK threads (wsum: NV * waves words of
+// LDS); tot = the block totals.
+template <int BLOCK, int NV>
+__device__ __forceinline__ void block_scan(uint32_t (&v)[NV], uint32_t* wsum, uint32_t (&tot)[NV]) {
+  constexpr int W = BLOCK / GRS_WAVE;
+  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+  uint32_t inc[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    inc[q] = wave_scan_dpp(v[q]);
+    if (lane == GRS_WAVE - 1) wsum[q * W + w] = inc[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    uint32_t p = 0;
+    tot[q] = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const uint32_t x = wsum[q * W + k];
+      p += static_cast<uint32_t>(k) < w ? x : 0u;
+      tot[q] += x;
+    }
+    v[q] = p + inc[q] - v[q];
+  }
+  __syncthreads();   // wsum is reused by the next call
+}
+
+// One block (BLOCK threads) plans a segmented pass of TILE-key tiles: for every ticket, the
+// tile's place (SegTile) -- tiles in segment order; a segment of several tiles gets status rows
+// and starts new look-back groups, a segment of one tile is solo (no status words).
+// Sources: kSegSizes a = sizes (starts = their scan; histogram row = segment index);
+// kSegList a = starts, b = lengths, c = histogram rows; kSegOffsets a = offsets (histogram row =
+// segment index).  hdr[0] = tiles, hdr[1] = groups, hdr[2] = status rows.
+// lds: GRS_PLAN_LDS_WORDS words.
+template <uint32_t TILE, int BLOCK, int SRC>
+__device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                               const uint32_t* __restrict__ c, uint32_t nseg,
+                               uint32_t* __restrict__ spill, SegTile* __restrict__ rec,
+                               uint32_t* __restrict__ hdr, uint32_t* lds) {
+  constexpr uint32_t G = GRS_LB_GROUP;
+  const uint32_t t = threadIdx.x;
+  const bool in_lds = nseg < GRS_PLAN_LDS_SEGS;
+  uint32_t* const tpre = in_lds ? lds : spill;
+  const uint32_t cap = in_lds ? GRS_PLAN_LDS_SEGS : nseg + 1;
+  uint32_t* const rpre = tpre + cap;
+  uint32_t* const gpre = rpre + cap;
+  uint32_t* const sst = gpre + cap;
+  uint32_t* const sln = sst + cap;
+  uint32_t* const shr = sln + cap;
+  uint32_t* const wsum = lds + 6 * GRS_PLAN_LDS_SEGS;
+  uint32_t carry[4] = {0, 0, 0, 0};   // tiles, rows, groups, start (sizes source)
+  for (uint32_t c0 = 0; c0 < nseg; c0 += BLOCK) {
+    const uint32_t i = c0 + t;
+    uint32_t len = 0, st = 0, hr = i;
+    if (i < nseg) {
+      if constexpr (SRC == kSegSizes) {
+        len = a[i];
+      } else if constexpr (SRC == kSegList) {
+        st = a[i];
+        len = b[i];
+        hr = c[i];
+      } else {
+        st = a[i];
+        len = a[i + 1] - st;
+      }
+    }
+    const uint32_t tl = len / TILE + (len % TILE != 0u ? 1u : 0u);
+    const uint32_t multi = tl > 1 ? tl : 0u;
+    uint32_t v[4] = {tl, multi, (multi + G - 1) / G, len}, tot[4];
+    block_scan<BLOCK, 4>(v, wsum, tot);
+    if (i < nseg) {
+      tpre[i] = carry[0] + v[0];
+      rpre[i] = carry[1] + v[1];
+      gpre[i] = carry[2] + v[2];
+      sst[i] = SRC == kSegSizes ? carry[3] + v[3] : st;
+      sln[i] = len;
+      shr[i] = hr;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) carry[q] += tot[q];
+  }
+  if (t == 0) tpre[nseg] = carry[0];
+  __syncthreads();
+  const uint32_t tiles = carry[0];
+  for (uint32_t tk = t; tk < tiles; tk += BLOCK) {
+    uint32_t lo = 0, hi = nseg;   // the largest i with tpre[i] <= tk (a non-empty segment)
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (tpre[mid] <= tk) lo = mid; else hi = mid;
+    }
+    const uint32_t j = tk - tpre[lo];
+    const uint32_t tl = tpre[lo + 1] - tpre[lo];
+    const uint32_t len = sln[lo];
+    const uint32_t q = j / G;
+    const uint32_t flags = (j % G) | (min(G, tl - q * G) << 4) | ((tl == 1 ? 1u : 0u) << 8) | (q << 9);
+    rec[tk] = SegTile{rpre[lo] + j, gpre[lo] + q, flags, sst[lo] + j * TILE, min(TILE, len - j * TILE),
+                      sst[lo], len, shr[lo]};
+  }
+  if (t == 0) {
+    hdr[0] = tiles;
+    hdr[1] = carry[2];
+    hdr[2] = carry[1];
+  }
+}
+
+// Stand-alone planner (one block): nseg from the host, or from *nseg_dev when non-null.
+template <uint32_t TILE, int SRC>
+__global__ __launch_bounds__(1024) void grs_seg_plan(const uint32_t* __restrict__ a,
+                                                     const uint32_t* __restrict__ b,
+                                                     const uint32_t* __restrict__ c,
+                                                     uint32_t nseg_host,
+                                                     const uint32_t* __restrict__ nseg_dev,
+                                                     uint32_t* __restrict__ spill,
+                                                     SegTile* __restrict__ rec,
+                                                     uint32_t* __restrict__ hdr) {
+  __shared__ uint32_t lds[GRS_PLAN_LDS_WORDS];
+  const uint32_t nseg = nseg_dev != nullptr ? *nseg_dev : nseg_host;
+  seg_plan_block<TILE, 1024, SRC>(a, b, c, nseg, spill, rec, hdr, lds);
+}
+
+// Per-segment digit histograms of a segment table's keys: rows[seg * ND * 256 + p * 256 + d]
+// counts digit d (bits [shift0 + 8p, +8)) of the segment's keys, p < ND (rows zeroed by the
+// caller).  Solo segments (one tile) are skipped: their pass counts them itself.  Persistent
+// grid over the plan's tiles; also zeroes the status words of the first segmented pass
+// (`zero`, rows of `radix` words; the layout is known only from the plan).
+template <typename K, int ND>
+__global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
+                                                    const SegTile* __restrict__ rec,
+                                                    const uint32_t* __restrict__ hdr, int shift0,
+                                                    uint32_t* __restrict__ rows,
+                                                    uint32_t* __restrict__ zero, uint32_t radix) {
+  __shared__ uint32_t h[ND * 256];
+  const uint32_t t = threadIdx.x;
+  const uint32_t tiles = hdr[0];
+  const size_t zw = static_cast<size_t>(hdr[2] + 2 * hdr[1]) * radix;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + t; i < zw; i += static_cast<size_t>(gridDim.x) * 256)
+    zero[i] = 0;
+  for (uint32_t k = blockIdx.x; k < tiles; k += gridDim.x) {
+    const SegTile r = rec[k];
+    if ((r.flags >> 8) & 1u) continue;   // solo (uniform: one record per workgroup)
+    for (uint32_t i = t; i < ND * 256; i += 256) h[i] = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < r.valid; i += 256) {
+      const K x = keys[r.base + i];
+#pragma unroll
+      for (int p = 0; p < ND; ++p)
+        atomicAdd(&h[p * 256 + static_cast<uint32_t>((x >> (shift0 + 8 * p)) & 255u)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < ND * 256; i += 256)
+      if (h[i] != 0u) atomicAdd(&rows[static_cast<size_t>(r.seg) * ND * 256 + i], h[i]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// MSD u32 sort: H2 and P3
+// ---------------------------------------------------------------------------------------
+#define GRS_H2_CHUNK 262144
+#define GRS_H2_WIN 2        // buckets a block counts in LDS; keys of later buckets: global adds
+#define GRS_H2_COPIES 32
+
+// H2: h2[(top byte) * 256 + byte 2] over keys grouped by top byte (P1's output); a block's
+// chunk of GRS_H2_CHUNK keys meets at most a few buckets.  Also zeroes `zero_words` of `zero`
+// (P2's status layout) and block 0 plans P2's tiles from the top-byte sizes (hist1).
+template <uint32_t TILE2>
+__global__ __launch_bounds__(1024) void grs_msd_hist2(const uint32_t* __restrict__ keys, uint32_t n,
+                                                      uint32_t* __restrict__ h2,
+                                                      uint32_t* __restrict__ zero, uint32_t zero_words,
+                                                      const uint32_t* __restrict__ hist1,
+                                                      SegTile* __restrict__ rec2,
+                                                      uint32_t* __restrict__ hdr2) {
+  constexpr uint32_t B = 1024;
+  constexpr uint32_t LW = GRS_H2_WIN * 256 * GRS_H2_COPIES;
+  static_assert(LW >= GRS_PLAN_LDS_WORDS, "the planner reuses the histogram's LDS");
+  __shared__ __attribute__((aligned(16))) uint32_t h[LW];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < LW; i += B) h[i] = 0;
+  for (uint32_t i = blockIdx.x * B + t; i < zero_words; i += gridDim.x * B) zero[i] = 0;
+  const uint32_t c0 = blockIdx.x * GRS_H2_CHUNK;
+  const uint32_t len = min(static_cast<uint32_t>(GRS_H2_CHUNK), n - c0);
+  const uint32_t s0 = keys[c0] >> 24;
+  __syncthreads();
+  uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
+  auto count = [&](uint32_t k) {
+    const uint32_t s = (k >> 24) - s0;
+    if (s < GRS_H2_WIN)
+      atomicAdd(base + (s * 256 + ((k >> 16) & 255u)) * GRS_H2_COPIES, 1u);
+    else
+      atomicAdd(&h2[k >> 16], 1u);
+  };
+  const uint32_t* kc = keys + c0;
+  const bool al = (reinterpret_cast<uintptr_t>(kc) & 15u) == 0;
+  const uint32_t nv = al ? len / 4 : 0u;
+  const uint4* kv = reinterpret_cast<const uint4*>(kc);
+  uint32_t v = t;
+  for (; v + 3 * B < nv; v += 4 * B) {
+    uint4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = kv[v + u * B];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      count(x[u].x);
+      count(x[u].y);
+      count(x[u].z);
+      count(x[u].w);
+    }
+  }
+  for (; v < nv; v += B) {
+    const uint4 x = kv[v];
+    count(x.x);
+    count(x.y);
+    count(x.z);
+    count(x.w);
+  }
+  for (uint32_t i = nv * 4 + t; i < len; i += B) count(kc[i]);
+  __syncthreads();
+  for (uint32_t i = t; i < GRS_H2_WIN * 256; i += B) {
+    const uint32_t* row = h + i * GRS_H2_COPIES;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
+    const uint32_t s = s0 + i / 256;
+    if (c != 0 && s < 256) atomicAdd(&h2[s * 256 + i % 256], c);
+  }
+  if (blockIdx.x == 0) {   // P2's tiles: the 256 top-byte buckets (final since H1)
+    __syncthreads();
+    seg_plan_block<TILE2, B, kSegSizes>(hist1, nullptr, nullptr, 256u, nullptr, rec2, hdr2, h);
+  }
+}
+
+// P3: one workgroup per 16-bit prefix b (grid 65536): its len = h2[b] keys at dstart[b] (P2's
+// digit starts) sorted by bits 0..15 in LDS, in place.  Segments longer than BLOCK * I keys go
+// to the big list for the segmented LSD: big[0] counts them, big[1] counts those longer than
+// one fallback tile (TILEF keys), which get a histogram row (two digits) zeroed here;
+// big_start / big_len / big_row hold (start, length, row) per entry.
+// C16: 16-bit wave counters (two per word), so that two 18K-key workgroups share a CU's LDS.
+template <int BLOCK, int I, bool C16, uint32_t TILEF>
+__global__ __launch_bounds__(BLOCK) void grs_msd_local(uint32_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ h2,
+                                                       const uint32_t* __restrict__ dstart,
+                                                       uint32_t* __restrict__ big,
+                                                       uint32_t* __restrict__ big_start,
+                                                       uint32_t* __restrict__ big_len,
+                                                       uint32_t* __restrict__ big_row,
+                                                       uint32_t* __restrict__ rows) {
+  constexpr uint32_t W = BLOCK / GRS_WAVE, SMAX = BLOCK * I;
+  static_assert(W <= 16 && BLOCK >= 256, "digit threads: waves 0..3");
+  static_assert(!C16 || SMAX < 65536, "16-bit positions");
+  __shared__ uint32_t sk[SMAX];
+  __shared__ uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
+  __shared__ uint32_t wtot[4];
+  __shared__ uint32_t slot;
+  uint16_t* const c16 = reinterpret_cast<uint16_t*>(cnt);
+  auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return cnt[a]; };
+  auto cst = [&](uint32_t a, uint32_t v) {
+    if constexpr (C16) c16[a] = static_cast<uint16_t>(v); else cnt[a] = v;
+  };
+  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+  const uint32_t len = h2[blockIdx.x];
+  if (len <= 1) return;   // (the start of an empty segment was never written)
+  const uint32_t lo = dstart[blockIdx.x];
+  if (len > SMAX) {
+    if (t == 0) {
+      const uint32_t e = atomicAdd(&big[0], 1u);
+      const uint32_t row = len > TILEF ? atomicAdd(&big[1], 1u) : 0xFFFFFFFFu;
+      big_start[e] = lo;
+      big_len[e] = len;
+      big_row[e] = row;
+      slot = row;
+    }
+    __syncthreads();
+    if (slot != 0xFFFFFFFFu)
+      for (uint32_t i = t; i < 2 * 256; i += BLOCK) rows[static_cast<size_t>(slot) * 512 + i] = 0;
+    return;
+  }
+  uint32_t k[I];
+#pragma unroll
+  for (uint32_t j = 0; j < I; ++j) {
+    const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+    k[j] = i < len ? keys[lo + i] : 0u;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int shift = 8 * pass;
+    for (uint32_t c = t; c < W * 256 / (C16 ? 2 : 1); c += BLOCK) cnt[c] = 0;
+    __syncthreads();
+    uint32_t r[I];
+#pragma unroll
+    for (uint32_t j = 0; j < I; ++j) {
+      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+      const uint32_t d = (k[j] >> shift) & 255u;
+      if constexpr (C16) {
+        const uint32_t sh = (d & 1u) << 4;
+        r[j] = i < len ? (atomicAdd(&cnt[(w * 256 + d) >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
+      } else {
+        r[j] = i < len ? atomicAdd(&cnt[w * 256 + d], 1u) : 0u;
+      }
+    }
+    __syncthreads();
+    uint32_t c[W], tot = 0, incl = 0;
+    if (t < 256) {
+#pragma unroll
+      for (uint32_t ww = 0; ww < W; ++ww) {
+        c[ww] = cld(ww * 256 + t);
+        tot += c[ww];
+      }
+      incl = wave_scan_dpp(tot);
+      if (lane == GRS_WAVE - 1) wtot[w] = incl;
+    }
+    __syncthreads();
+    if (t < 256) {
+      uint32_t b = incl - tot;
+#pragma unroll
+      for (uint32_t ww = 0; ww < 4; ++ww) b += ww < w ? wtot[ww] : 0u;
+#pragma unroll
+      for (uint32_t ww = 0; ww < W; ++ww) {
+        cst(ww * 256 + t, b);
+        b += c[ww];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < I; ++j) {
+      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+      if (i < len) sk[cld(w * 256 + ((k[j] >> shift) & 255u)) + r[j]] = k[j];
+    }
+    __syncthreads();
+    if (pass == 0) {
+#pragma unroll
+      for (uint32_t j = 0; j < I; ++j) {
+        const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+        if (i < len) k[j] = sk[i];
+      }
+    }
+  }
+  for (uint32_t i = t; i < len; i += BLOCK) keys[lo + i] = sk[i];
+}
+
+}  // namespace grs

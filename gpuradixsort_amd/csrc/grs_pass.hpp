@@ -67,34 +67,43 @@ struct Lb3 {
   uint32_t gi[GW], ga[GW];
   int32_t ph;
 
+  int32_t g0;   // first group of the tile's segment (0 for an ordinary pass): the chain stops there
+
   __device__ __forceinline__ void load_groups(const uint32_t* gacc, const uint32_t* ginc,
                                               uint32_t d) {
 #pragma unroll
     for (int k = 0; k < GW; ++k) {
       const int32_t h = ph - k;
-      gi[k] = h >= 0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
-      ga[k] = h >= 0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      gi[k] = h >= g0 ? ld_status(ginc + static_cast<size_t>(h) * RADIX + d) : 0u;
+      ga[k] = h >= g0 ? ld_status(gacc + static_cast<size_t>(h) * RADIX + d) : 0u;
     }
   }
+  // tile: the tile's word row; jg: its place in its look-back group (the group's earlier tiles
+  // are rows tile - jg .. tile - 1); group: its group; group0: the first group of its segment
+  // (0 for an ordinary pass), where the chain stops.  Segmented passes start every segment on
+  // a new group, so a group never holds tiles of two segments.
   __device__ __forceinline__ void issue(const uint32_t* status, const uint32_t* gacc,
-                                        const uint32_t* ginc, uint32_t tile, uint32_t d) {
-    const uint32_t first = (tile / G) * G;
+                                        const uint32_t* ginc, uint32_t tile, uint32_t d,
+                                        uint32_t jg, uint32_t group, uint32_t group0) {
+    const uint32_t first = tile - jg;
 #pragma unroll
     for (int k = 0; k < G - 1; ++k)
-      tw[k] = first + k < tile ? ld_status(status + static_cast<size_t>(first + k) * RADIX + d) : 1u;
-    ph = static_cast<int32_t>(tile / G) - 1;
+      tw[k] = static_cast<uint32_t>(k) < jg ? ld_status(status + static_cast<size_t>(first + k) * RADIX + d) : 1u;
+    ph = static_cast<int32_t>(group) - 1;
+    g0 = static_cast<int32_t>(group0);
     load_groups(gacc, ginc, d);
   }
-  // gold: the value this tile's add to its group accumulator returned; publish: its count.
+  // gold: the value this tile's add to its group accumulator returned; publish: its count;
+  // in_group: the tiles of its group (G but in a segment's last group).
   // A spin that exceeds `limit` polls sets the error word and counts the word as 0: prefixes
   // can then only come out SMALLER than the true ones (onesweep_tile clamps the runs to
   // [0, n) for the passes after such a one).
   __device__ __forceinline__ uint32_t finish(const uint32_t* status, const uint32_t* gacc,
-                                             uint32_t* ginc, uint32_t tile, uint32_t tiles,
+                                             uint32_t* ginc, uint32_t tile, uint32_t jg,
+                                             uint32_t group, uint32_t in_group,
                                              uint32_t d, uint32_t gold, uint32_t publish,
                                              uint32_t* error_word, uint32_t limit) {
-    const uint32_t g = tile / G;
-    const uint32_t first = g * G;
+    const uint32_t first = tile - jg;
     uint32_t spins = 0, own = 0;
 #pragma unroll
     for (int k = 0; k < G - 1; ++k) {
@@ -111,12 +120,12 @@ struct Lb3 {
       own += v - 1u;
     }
     uint32_t gp = 0;
-    while (ph >= 0) {
+    while (ph >= g0) {
       int consumed = 0;
       bool done = false, blocked = false;
 #pragma unroll
       for (int k = 0; k < GW; ++k) {
-        if (!done && !blocked && ph - k >= 0) {
+        if (!done && !blocked && ph - k >= g0) {
           if (gi[k] != 0u) {
             gp += gi[k] - 1u;
             done = true;
@@ -130,7 +139,7 @@ struct Lb3 {
       }
       if (done) break;
       ph -= consumed;
-      if (ph < 0) break;
+      if (ph < g0) break;
       if (consumed == 0) {
         if (++spins > limit) {
           atomicOr(error_word, 1u);
@@ -140,10 +149,39 @@ struct Lb3 {
       }
       load_groups(gacc, ginc, d);
     }
-    const uint32_t in_group = min(static_cast<uint32_t>(G), tiles - g * G);
     if ((gold >> 24) == in_group - 1u)   // this tile's add completed the group
-      st_status(ginc + static_cast<size_t>(g) * RADIX + d, gp + (gold & 0xFFFFFFu) + publish + 1u);
+      st_status(ginc + static_cast<size_t>(group) * RADIX + d, gp + (gold & 0xFFFFFFu) + publish + 1u);
     return gp + own;
+  }
+};
+
+// Where one tile of a pass lies, and its place in the look-back status layout
+// [tiles][R] tile words, [groups][R] group accumulators, [groups][R] group inclusives.
+// Ordinary pass: tile = ticket, the pass is one segment [0, n), groups of G consecutive tiles.
+// Segmented pass (grs_onesweep_seg): tiles never straddle a segment and every segment starts a
+// new group, so its chain restarts at its first group and its digit runs start at the
+// segment's own base.
+struct TileSpan {
+  uint32_t tile;       // tile word row (the ticket)
+  uint32_t tiles;      // tile rows of the layout
+  uint32_t group;      // the tile's look-back group
+  uint32_t groups;     // groups of the layout
+  uint32_t jg;         // place of the tile in its group
+  uint32_t in_group;   // tiles of its group
+  uint32_t g0;         // first group of the tile's segment
+  uint32_t base;       // index of the tile's first key
+  uint32_t valid;      // keys in the tile (<= TILE)
+  uint32_t seg_start;  // first index of the tile's segment
+  uint32_t seg_len;    // keys in the segment
+  bool solo;           // segmented pass: the segment's only tile -- no status words, no
+                       // look-back, its own counts are the segment's
+  __device__ __forceinline__ static TileSpan whole(uint32_t tile, uint32_t n, uint32_t TILE) {
+    constexpr uint32_t G = GRS_LB_GROUP;
+    const uint32_t tiles = n / TILE + (n % TILE != 0u ? 1u : 0u);
+    const uint32_t b = tile * TILE;
+    const uint32_t g = tile / G;
+    return TileSpan{tile, tiles, g, (tiles + G - 1) / G, tile % G, min(G, tiles - g * G), 0u,
+                    b, (n - b) < TILE ? (n - b) : TILE, 0u, n, false};
   }
 };
 
@@ -187,21 +225,21 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
+// The same for the tile whose first key is index `tile_base`, `valid` keys of it in range
+// (valid >= TILE: a full tile).
 template <typename K, bool PAIRS, int BLOCK, int ITEMS, int OPT>
-__device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS],
-                                          const K* __restrict__ keys_in,
-                                          const uint32_t* __restrict__ vals_in, uint32_t n,
-                                          uint32_t tile, uint32_t t) {
+__device__ __forceinline__ void tile_load_at(K (&key)[ITEMS], uint32_t (&val)[ITEMS],
+                                             const K* __restrict__ keys_in,
+                                             const uint32_t* __restrict__ vals_in, uint32_t n,
+                                             uint32_t tile_base, uint32_t valid, uint32_t t) {
   constexpr uint32_t TILE = BLOCK * ITEMS;
   const uint32_t lane = t & (GRS_WAVE - 1);
   const uint32_t w = t >> 6;
-  const uint32_t tile_base = tile * TILE;
   const uint32_t wbase = tile_base + w * (GRS_WAVE * ITEMS) + lane;
   constexpr bool IN_REC = (OPT & 4096) != 0;
   static_assert(!IN_REC || (PAIRS && sizeof(K) == 4), "records: u32 key + u32 value");
   // tile-local bounds (compare offsets, never global indices: tile_base + TILE can pass 2^32
   // when n is near GRS_MAX_N, and a wrapped index would read as in range)
-  const uint32_t valid = n - tile_base;
   const uint32_t lbase = w * (GRS_WAVE * ITEMS) + lane;
   if constexpr (IN_REC) {
     const uint2* rec = reinterpret_cast<const uint2*>(keys_in);
@@ -233,6 +271,16 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
   }
 }
 
+template <typename K, bool PAIRS, int BLOCK, int ITEMS, int OPT>
+__device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS],
+                                          const K* __restrict__ keys_in,
+                                          const uint32_t* __restrict__ vals_in, uint32_t n,
+                                          uint32_t tile, uint32_t t) {
+  constexpr uint32_t TILE = BLOCK * ITEMS;
+  tile_load_at<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile * TILE,
+                                            n - tile * TILE, t);
+}
+
 // One tile, from its loaded (or in-flight) keys to its stores.  Precondition: sm.cnt is zero
 // and every thread passed a barrier since it was written and since the previous tile's last
 // LDS access.  Leaves sm.cnt dirty.
@@ -242,14 +290,15 @@ __device__ __forceinline__ void tile_load(K (&key)[ITEMS], uint32_t (&val)[ITEMS
 // behind the look-back and the stores.  Returns the next tile (>= tiles: none); without PF
 // returns tiles.
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, bool PF = false,
-          typename DigitF>
+          bool SEG = false, typename DigitF>
 __device__ __forceinline__ uint32_t onesweep_tile(
-    V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>& sm, uint32_t tile, K (&key)[ITEMS],
+    V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>& sm, const TileSpan sp, K (&key)[ITEMS],
     uint32_t (&val)[ITEMS], const K* __restrict__ keys_in,
     K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
-    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, PassDebug dbg) {
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, PassDebug dbg,
+    uint32_t* __restrict__ digit_starts = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr bool MATCH = (OPT & 512) != 0;
@@ -277,10 +326,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   asm volatile("" : "+v"(t));
   const uint32_t lane = t & (GRS_WAVE - 1);
   const uint32_t w = t >> 6;
-  const uint32_t tiles = (n + TILE - 1) / TILE;
-  const uint32_t groups = (tiles + G - 1) / G;
-  const uint32_t tile_base = tile * TILE;
-  const uint32_t valid = (n - tile_base) < static_cast<uint32_t>(TILE) ? (n - tile_base) : TILE;
+  const uint32_t tile = sp.tile;
+  const uint32_t tiles = sp.tiles;
+  const uint32_t groups = sp.groups;
+  const uint32_t tile_base = sp.base;
+  const uint32_t valid = sp.valid;
   const uint32_t pad = TILE - valid;
   const uint32_t dmask = dig.max_digit();
   uint32_t* gacc = status + static_cast<size_t>(tiles) * RADIX;
@@ -332,12 +382,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   if constexpr (PF) {
     if (t == 0) sm.next = atomicAdd(ticket, 1u);  // read after the reorder
   }
+  // a solo tile (segmented passes) has no status words and waits on nobody
+  const bool solo = SEG && sp.solo;
   // this tile's (and its group's) words of the next pass's status buffer
-  if (t < static_cast<uint32_t>(RADIX)) {
+  if (t < static_cast<uint32_t>(RADIX) && !solo) {
     status_next[static_cast<size_t>(tile) * RADIX + t] = 0;
-    if (tile % G == 0) {
-      status_next[static_cast<size_t>(tiles) * RADIX + (tile / G) * RADIX + t] = 0;
-      status_next[static_cast<size_t>(tiles + groups) * RADIX + (tile / G) * RADIX + t] = 0;
+    if (sp.jg == 0) {
+      status_next[static_cast<size_t>(tiles + sp.group) * RADIX + t] = 0;
+      status_next[static_cast<size_t>(tiles + groups + sp.group) * RADIX + t] = 0;
     }
   }
   lds_barrier();  // B1
@@ -351,10 +403,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       tile_cnt += c;
     }
     publish = (t == dmask) ? tile_cnt - pad : tile_cnt;  // padding is ranked, never counted
-    if (tile + 1u != dbg.fault_tile1)
-      st_status(status + static_cast<size_t>(tile) * RADIX + t, publish + 1u);
-    gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(tile / G) * RADIX + t,
-                                  (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (solo) {
+      gh = publish;   // the segment's counts: its digit starts are the tile's own
+    } else {
+      if (tile + 1u != dbg.fault_tile1)
+        st_status(status + static_cast<size_t>(tile) * RADIX + t, publish + 1u);
+      gold = __hip_atomic_fetch_add(gacc + static_cast<size_t>(sp.group) * RADIX + t,
+                                    (1u << 24) | publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (w < static_cast<uint32_t>(DW)) {
     const uint32_t li = wave_scan_dpp(tile_cnt);
@@ -374,13 +430,18 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       lstart += sm.wsum[ww];
       gstart += sm.wsum[WAVES + ww];
     }
+    // segmented pass, a segment's first tile: where each digit's run of the segment starts
+    // (the next level's segment table, grs_msd_local)
+    if (digit_starts != nullptr) digit_starts[t] = sp.seg_start + gstart;
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) cnt_st(ww * RADIX + t, cnt_ld(ww * RADIX + t) + lstart);
     if constexpr (IDX) {
       sm.lstart[t] = lstart;
       if (t == static_cast<uint32_t>(RADIX - 1)) sm.lstart[RADIX] = TILE;
     }
-    if constexpr (!LATE_LB) lb.issue(status, gacc, ginc, tile, t);
+    if constexpr (!LATE_LB) {
+      if (!solo) lb.issue(status, gacc, ginc, tile, t, sp.jg, sp.group, sp.g0);
+    }
   }
   lds_barrier();  // B3
 
@@ -412,7 +473,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     }
   }
   if constexpr (LATE_LB) {
-    if (t < static_cast<uint32_t>(RADIX)) lb.issue(status, gacc, ginc, tile, t);
+    if (t < static_cast<uint32_t>(RADIX) && !solo) lb.issue(status, gacc, ginc, tile, t, sp.jg, sp.group, sp.g0);
   }
   uint32_t next = tiles;
   if constexpr (PF && ROUNDS == 1) {   // two rounds: after round 2 sits in LDS
@@ -421,15 +482,21 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   }
   if (t < static_cast<uint32_t>(RADIX)) {
     const uint32_t prefix =
-        lb.finish(status, gacc, ginc, tile, tiles, t, gold, publish, error_word, dbg.spin_limit);
+        solo ? 0u
+             : lb.finish(status, gacc, ginc, tile, sp.jg, sp.group, sp.in_group, t, gold, publish,
+                         error_word, dbg.spin_limit);
     uint32_t start = gstart + prefix;
     if constexpr (!IDX) {
       // A timed-out look-back only underestimates this pass's prefixes, but the next pass of
       // the same sort then reads keys whose digits no longer match the upfront histogram, and
-      // a run could pass n.  Keep every run inside [0, n) (a no-op on consistent counts).
-      const uint32_t room = n - publish;
-      start = gstart > room ? room : gstart + min(prefix, room - gstart);
+      // a run could pass n.  Keep every run inside its segment, [0, n) for an ordinary pass (a
+      // no-op on consistent counts).
+      const uint32_t room = sp.seg_len - publish;
+      start = sp.seg_start + (gstart > room ? room : gstart + min(prefix, room - gstart));
     }
+    // (indexed digits, the partition pass: its one pass per call reads the input as given, so
+    // a timed-out look-back there only underestimates its own runs' starts; they stay >= 0 and
+    // end before n -- no clamp needed)
     sm.base[t] = start - lstart;
   }
   lds_barrier();  // B4
@@ -536,7 +603,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
-  onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, tile, key, val, keys_in, keys_out, vals_in,
+  onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, TileSpan::whole(tile, n, SM::TILE), key, val,
+                                                 keys_in, keys_out, vals_in,
                                                  vals_out, n, dg, gh, ticket, status, status_next,
                                                  error_word, PassDebug::read(error_word));
 }
@@ -576,12 +644,77 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);
   while (tile < tiles) {
     tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true>(
-        sm, tile, key, val, keys_in, keys_out, vals_in, vals_out, n, dg, gh, ticket, status,
+        sm, TileSpan::whole(tile, n, SM::TILE), key, val, keys_in, keys_out, vals_in, vals_out, n,
+        dg, gh, ticket, status,
         status_next, error_word, dbg);
     // every LDS read of the finished tile is done before the counters are reset
     lds_barrier();
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
     lds_barrier();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// segmented pass: every segment of a table sorted by one digit on its own
+// ---------------------------------------------------------------------------------------
+// One tile of a segmented pass, as the planner (grs_seg_plan, grs_msd.hpp) lays it out.
+struct SegTile {
+  uint32_t row;        // tile word row of the status layout (solo tiles: none)
+  uint32_t group;      // look-back group of the tile
+  uint32_t flags;      // place in the group (bits 0-3) | tiles of the group (4-7) | solo (8)
+                       // | the group's place in its segment (9-31)
+  uint32_t base;       // first key of the tile
+  uint32_t valid;      // keys in the tile
+  uint32_t seg_start;  // first key of the segment
+  uint32_t seg_len;    // keys in the segment
+  uint32_t seg;        // histogram row of the segment
+};
+
+// MSD sort and segmented sorts (grs_capi.hip): the same tile code as grs_onesweep_v4, over the
+// tiles of a segment table -- tiles never straddle a segment, each segment's look-back chain
+// restarts at its first tile, and its digit runs start at the segment's own first key, from
+// the segment's own digit counts (hist row `seg`; a segment of one tile ranks, scans and stores
+// it with no status words and no look-back).  hdr[0] = tiles (tickets), hdr[1] = look-back
+// groups, hdr[2] = tile word rows of the status layout.  PERSIST: grid = resident workgroups looping over tickets (tables whose
+// size is known only on the device); otherwise grid >= hdr[0], one tile per workgroup.
+// digit_starts (nullable): a segment's first tile writes the start of each digit run of the
+// segment to digit_starts[seg * RADIX + d].
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT, bool PERSIST>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, const RadixDigit<K> dig, const SegTile* __restrict__ rec,
+    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ hist, uint32_t hist_stride,
+    uint32_t* __restrict__ ticket, uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
+    uint32_t* __restrict__ error_word, uint32_t* __restrict__ digit_starts) {
+  using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, RadixDigit<K>>;
+  static_assert((OPT & (4096 | 8192 | 16384 | 32768)) == 0, "segmented passes move two arrays");
+  __shared__ SM sm;
+  const uint32_t t = threadIdx.x;
+  const PassDebug dbg = PassDebug::read(error_word);
+  for (;;) {
+    if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+    for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    __syncthreads();
+    const uint32_t tk = __builtin_amdgcn_readfirstlane(sm.ticket);
+    if (tk >= hdr[0]) return;   // every workgroup leaves once it draws a ticket past the table
+    const SegTile r = rec[tk];
+    const bool solo = (r.flags >> 8) & 1u;
+    const TileSpan sp{r.row, hdr[2], r.group, hdr[1], r.flags & 15u, (r.flags >> 4) & 15u,
+                      r.group - (r.flags >> 9), r.base, r.valid, r.seg_start, r.seg_len, solo};
+    K key[ITEMS];
+    uint32_t val[ITEMS];
+    uint32_t tt = t;
+    asm volatile("" : "+v"(tt));
+    tile_load_at<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, 0u, sp.base, sp.valid, tt);
+    const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) && !solo
+                            ? hist[static_cast<size_t>(r.seg) * hist_stride + t] : 0u;
+    uint32_t* ds = digit_starts != nullptr && r.base == r.seg_start
+                       ? digit_starts + static_cast<size_t>(r.seg) * SM::RADIX : nullptr;
+    onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, false, true>(sm, sp, key, val, keys_in, keys_out, vals_in,
+                                                   vals_out, 0u, dig, gh, ticket, status,
+                                                   status_next, error_word, dbg, ds);
+    if constexpr (!PERSIST) return;
+    lds_barrier();   // every LDS read of the finished tile before the next ticket's reset
   }
 }
 

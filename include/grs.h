@@ -70,6 +70,10 @@ typedef struct grs_timing {
   float hist_ms;             /* memset of the control block + upfront histogram */
   float pass_ms[16];         /* one onesweep launch per digit */
   float copy_ms;             /* final copy for an odd pass count (0 otherwise) */
+  int kind;                  /* 0: LSD passes; 1: the MSD sort (GRS_OPT_MSD): hist_ms = the top
+                                byte's histogram, pass_ms[0..4] = the top-byte scatter, the
+                                per-bucket byte-2 histogram, the byte-2 scatter, the LDS sort of
+                                the 16-bit segments, the fallback of the longer ones */
 } grs_timing;
 
 /* Library version (GRS_VERSION) and the last error message of this host thread. */
@@ -132,11 +136,16 @@ typedef enum grs_option {
   GRS_OPT_MERGE = 9,         /* presorted exchange, receive side: 0 (default) ceil(log2 k)
                                 2-way merge rounds over the k received runs, 1 one k-way merge
                                 pass (sample-delimited tiles merged in LDS; slower at 8 ranks) */
-  GRS_OPT_FAULT_TILE = 10    /* TEST HOOK: -1 (default) off; v >= 0: tile v of every pass never
+  GRS_OPT_FAULT_TILE = 10,   /* TEST HOOK: -1 (default) off; v >= 0: tile v of every pass never
                                 publishes its look-back tile words and spins give up after 2^12
                                 polls, so the later tiles of its look-back group time out: the
                                 sort's output is wrong and GRS_ETIMEOUT surfaces through
                                 grs_check_error / grs_stream_check_error (the error path's test) */
+  GRS_OPT_MSD = 11           /* u32 keys without payload, 8-bit digits, the whole key: -1 by size
+                                (default), 0 never, 1 always -- the MSD-first sort (two stable
+                                scatters by the top two bytes into 65536 segments, each finished
+                                in LDS by one workgroup; segments too long for LDS sorted by a
+                                segmented LSD on their low 16 bits) instead of 4 LSD passes */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);

@@ -1,0 +1,125 @@
+"""GPU tests of the MSD-first u32 sort (grs_msd.hpp; GRS_OPT_MSD).
+
+The MSD sort is a different schedule of the same stable sort: two stable scatters by the top
+two bytes, then each 16-bit segment sorted by its low 16 bits in LDS, and a segmented LSD for
+segments longer than LDS takes.  Its output must equal the reference's (the stable sort by key,
+ParallelSort.cpp:236-298 restated by oracle.ref_parallel_sort) bit for bit.  Keys only: the MSD
+path is the u32 keys-without-payload sort, so the check is the sorted multiset -- the same
+output order as the reference's path, which test_u32_matches_reference_path pins for the LSD
+schedule.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+_S = {}
+
+
+def msd_sorter(capacity, mode="always"):
+    import gpuradixsort_amd as grs
+
+    s = _S.get(mode)
+    if s is None or s.capacity < capacity:
+        if s is not None:
+            s.close()
+        s = grs.RadixSorter(max(capacity, 1 << 20), key_bits=32, pairs=False, radix_bits=8)
+        s.set_option("msd", mode)
+        _S[mode] = s
+    return s
+
+
+def run(keys: np.ndarray, dev, mode="always"):
+    s = msd_sorter(keys.size, mode)
+    k = torch.from_numpy(np.ascontiguousarray(keys)).to(dev)
+    s.sort(k)
+    torch.cuda.synchronize()
+    s.check_error()
+    return k.cpu().numpy()
+
+
+def dists(n, rng):
+    top = 0xFFFFFFFF
+    yield "uniform", rng.integers(0, top, n, dtype=np.uint32, endpoint=True)
+    yield "perm", rng.permutation(n).astype(np.uint32)
+    yield "all_equal", np.full(n, 7, np.uint32)
+    yield "all_max", np.full(n, top, np.uint32)
+    yield "sorted", np.sort(rng.integers(0, top, n, dtype=np.uint32, endpoint=True))
+    yield "reversed", np.arange(n, 0, -1).astype(np.uint32)
+    yield "16_unique", (rng.integers(0, 16, n).astype(np.uint32) * np.uint32(0x10000001))
+    yield "mixed_max", np.where(rng.random(n) < 0.3, top, rng.integers(0, 100, n)).astype(np.uint32)
+    yield "low_entropy", (rng.integers(0, top, n, dtype=np.uint32, endpoint=True)
+                          & rng.integers(0, top, n, dtype=np.uint32, endpoint=True)
+                          & rng.integers(0, top, n, dtype=np.uint32, endpoint=True))
+    yield "narrow_24bit", rng.integers(0, 1 << 24, n, dtype=np.uint32)
+    yield "narrow_29bit", rng.integers(0, 1 << 29, n, dtype=np.uint32)
+
+
+SIZES = [1, 2, 3, 64, 1000, 4097, 5121, 36865, 65537, 300007, 1 << 20]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_msd_matches_reference_path(gpu, n):
+    """Forced MSD schedule, every distribution: keys == the restated reference path."""
+    rng = np.random.default_rng(5000 + n)
+    for name, keys in dists(n, rng):
+        if n > 65537 and name not in ("uniform", "perm", "16_unique", "mixed_max", "narrow_29bit"):
+            continue
+        want = oracle.ref_parallel_sort(keys)[0]
+        got = run(keys, gpu)
+        assert np.array_equal(got, want), f"{name} n={n}"
+
+
+def _segment_keys(rng, sizes):
+    """Keys whose 16-bit prefixes p_i hold exactly sizes[i] keys each (random low halves),
+    shuffled: exercises P3's capacity edge and the fallback (solo and multi-tile segments)."""
+    parts = []
+    for i, c in enumerate(sizes):
+        prefix = np.uint32((i * 2654435761) & 0xFFFF) << np.uint32(16)
+        parts.append(prefix | rng.integers(0, 1 << 16, c, dtype=np.uint32))
+    keys = np.concatenate(parts)
+    rng.shuffle(keys)
+    return keys
+
+
+@pytest.mark.parametrize("sizes", [
+    [5120, 5121, 1, 2, 4096],                  # P3 shape A edge (n < 2^26: shape A)
+    [5121] * 7 + [100],                        # solo fallback segments
+    [36864, 36865, 73729, 200000, 3],          # one-tile, two-tile and multi-tile fallbacks
+    [1 << 20],                                 # one segment of everything
+])
+def test_msd_segment_edges(gpu, sizes):
+    rng = np.random.default_rng(sum(sizes))
+    keys = _segment_keys(rng, sizes)
+    got = run(keys, gpu)
+    assert np.array_equal(got, np.sort(keys))
+
+
+@pytest.mark.parametrize("n", [1 << 24, (1 << 26) + 12345])
+def test_msd_larger(gpu, n):
+    """Sizes where the MSD schedule is (or is about to be) the default: uniform and narrow
+    ranges, by the default option and forced, against torch.sort."""
+    rng = np.random.default_rng(n)
+    for name, keys in (("uniform", rng.integers(0, 1 << 32, n, dtype=np.uint32)),
+                       ("narrow_27bit", rng.integers(0, 1 << 27, n, dtype=np.uint32)),
+                       ("16_unique", rng.integers(0, 16, n).astype(np.uint32) << np.uint32(28))):
+        k = torch.from_numpy(keys).to(gpu)
+        want = torch.sort(k.view(torch.int32).to(torch.int64) & 0xFFFFFFFF)[0]
+        for mode in ("size", "always"):
+            got = run(keys, gpu, mode)
+            assert np.array_equal(got.astype(np.int64), want.cpu().numpy()), (name, mode)
+
+
+def test_msd_profile_kind(gpu):
+    """The profiled MSD sort reports its phases (grs_timing.kind = 1)."""
+    s = msd_sorter(1 << 22)
+    s.set_profiling(1)
+    k = torch.randint(0, 1 << 31, (1 << 22,), dtype=torch.int64, device=gpu).to(torch.int32)
+    s.sort(k.view(torch.uint32))
+    t = s.timing()
+    s.set_profiling(0)
+    assert t["kind"] == "msd" and t["passes"] == 5, t
+    assert all(x >= 0 for x in t["pass_ms"]) and t["total_ms"] > 0
