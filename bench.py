@@ -339,11 +339,12 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     msd = tims[0].get("kind") == "msd"
     msd_phases = None
     if msd:
-        # the MSD schedule (grs_msd.hpp): H1 | P1 top-byte scatter, H2, P2 byte-2 scatter, P3
-        # LDS sort of the 16-bit segments, fallback; each of P1 / P2 / P3 reads and writes every
-        # key once, so the dominant one of them is the roofline kernel
-        names = ["p1_scatter_top_byte", "h2_hist_byte2", "p2_scatter_byte2", "p3_local_sort",
-                 "fallback"]
+        # the MSD schedule (grs_msd.hpp): sample | P1 top-byte scatter into sampled regions,
+        # its redo (a run outgrew its region; empty launches otherwise), H2, P2 byte-2 scatter,
+        # P3 LDS sort of the 16-bit segments, fallback; each of P1 / P2 / P3 reads and writes
+        # every key once, so the dominant one of them is the roofline kernel
+        names = ["p1_scatter_top_byte", "p1_redo", "h2_hist_byte2", "p2_scatter_byte2",
+                 "p3_local_sort", "fallback"]
         msd_phases = {nm: round(sum(t["pass_ms"][i] for t in tims) / len(tims), 5)
                       for i, nm in enumerate(names)}
         dom = max(("p1_scatter_top_byte", "p2_scatter_byte2", "p3_local_sort"), key=msd_phases.get)
@@ -361,7 +362,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     n_sorted_local = sorter.last_n_out if exchange == "partition-first" else n_local
     kernel_name = (sorter.sorter if sharded else sorter).pass_kernel_for(n_sorted_local)
     if msd:
-        kernel_name = {"p1_scatter_top_byte": kernel_name, "p2_scatter_byte2": "grs_onesweep_seg",
+        kernel_name = {"p1_scatter_top_byte": "grs_onesweep_region", "p2_scatter_byte2": "grs_onesweep_seg",
                        "p3_local_sort": "grs_msd_local"}[dom]
     alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9

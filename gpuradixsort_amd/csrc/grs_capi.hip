@@ -436,6 +436,10 @@ struct MsdLayout {   // word offsets into msd_buf
   }
 };
 
+// Words of the sorter's second buffer for an MSD sorter: P1 writes its runs into sampled
+// regions (n + n/8 + 256 x 4096 + 256 keys at most, grs_msd.hpp).
+size_t msd_alt_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 8 + 256 * 4096 + 1024; }
+
 bool msd_type(const grs_sorter* s) {
   return s->key_type == GRS_KEY_U32 && !s->pairs && s->radix_bits == 8;
 }
@@ -622,6 +626,8 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
     alloc(&s->alt_keys, cap * 8);
     if (st == GRS_OK) s->alt_vals = static_cast<uint32_t*>(s->alt_keys) + cap;
     s->alt_joint = true;
+  } else if (msd_type(s)) {
+    alloc(&s->alt_keys, msd_alt_words(cap) * 4);   // + the MSD sort's region slack
   } else {
     alloc(&s->alt_keys, cap * kb);
     if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
@@ -952,39 +958,70 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
     if (evs) GRS_HIP(hipEventRecord(evs[ev++], stream));
     return GRS_OK;
   };
+  // rows of this call's control block (zeroed by the previous call): the sample's top-byte
+  // counts, the redo's exact counts, P1's digit totals + spill flag
+  uint32_t* const samp = hist;
+  uint32_t* const exact = hist + 256;
+  uint32_t* const totals = hist + 512;
+  // P1's regions: R_d = sample_d * n * 9/8 / sampled + pad (the sample reads every key up to
+  // 2^20 keys: exact counts, no pad needed)
+  const uint64_t sampled = std::min<uint64_t>(n, uint64_t(GRS_MSD_SAMPLE_CHUNKS) * GRS_WAVE);
+  const unsigned long long mult =
+      static_cast<unsigned long long>((static_cast<uint64_t>(n) * 9 * (uint64_t(1) << 20) + 8 * sampled - 1) /
+                                      (8 * sampled));
+  const uint32_t pad = n > sampled ? 4096u : 0u;
+  const uint64_t region_len = static_cast<uint64_t>(n) + n / 8 + 256u * pad + 256u;
+  if (region_len > msd_alt_words(s->capacity)) return set_err(GRS_ECAPACITY, "internal: MSD regions");
   grs_status r;
   if ((r = mark()) != GRS_OK) return r;
   if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = false;
-  {  // H1: the top byte's histogram; zeroes P1's status, the next call's control block, h2 and
-     // the big-segment counters
-    const int slots = grs::Hist2Layout<uint32_t>::PER_CU * s->cus;
-    const int need = static_cast<int>(n >> grs::kHist2GridShift<uint32_t>) + 1;
-    int grid = n <= (1u << 25) ? s->cus : slots;
-    if (grid < need) grid = (need + slots - 1) / slots * slots;
-    hipLaunchKernelGGL((grs::grs_upfront_hist2<uint32_t, 8, false, 1>), dim3(grid),
-                       dim3(grs::Hist2Layout<uint32_t>::BLOCK), 0, stream, src, n, 24, 32, 1, hist,
-                       st0, static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u);
-    GRS_HIP(hipGetLastError());
-  }
+  // S: the top byte's sampled histogram; zeroes P1's status, the next call's control block, h2
+  // and the big-segment counters
+  hipLaunchKernelGGL(grs::grs_msd_sample, dim3(1024), dim3(256), 0, stream, src, n, samp, st0,
+                     static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u);
+  GRS_HIP(hipGetLastError());
   s->cb_i ^= 1;
   if ((r = mark()) != GRS_OK) return r;
-  // P1: stable scatter by the top byte (the LSD pass kernel), src -> alt
+  // P1: stable scatter by the top byte into the sampled regions, src -> alt (no counting read)
   const Dig d1{24, 255u};
-  r = xl ? launch_pass<uint32_t, false, 8, XL, XL::OPT>(s, src, alt, nullptr, nullptr, n, d1, (const Dig*)nullptr, hist, tickets, st0, st1, stream, tile1)
-     : big ? launch_pass<uint32_t, false, 8, Big, Big::OPT>(s, src, alt, nullptr, nullptr, n, d1, (const Dig*)nullptr, hist, tickets, st0, st1, stream, tile1)
-           : launch_pass<uint32_t, false, 8, Small, kSmallOpt>(s, src, alt, nullptr, nullptr, n, d1, (const Dig*)nullptr, hist, tickets, st0, st1, stream, tile1);
-  if (r != GRS_OK) return r;
+  {
+    const uint32_t tiles = (n + tile1 - 1) / tile1;
+    auto go = [&](auto tshape, auto optc) {
+      using T = decltype(tshape);
+      constexpr uint32_t opt = decltype(optc)::value;
+      hipLaunchKernelGGL((grs::grs_onesweep_region<uint32_t, 8, T::BLOCK, T::ITEMS, T::MINW, opt, kMsdTileF>),
+                         dim3(tiles), dim3(T::BLOCK), 0, stream, src, alt, n, d1, samp, mult, pad,
+                         static_cast<uint32_t>(region_len), tickets, st0, st1, err, totals, recf, hdrf);
+    };
+    if (xl) go(XL{}, std::integral_constant<uint32_t, XL::OPT>{});
+    else if (big) go(Big{}, std::integral_constant<uint32_t, Big::OPT>{});
+    else go(Small{}, std::integral_constant<uint32_t, kSmallOpt>{});
+    GRS_HIP(hipGetLastError());
+  }
+  if ((r = mark()) != GRS_OK) return r;
+  // a run outgrew its region: P1 again into the exact layout (P1's last tile planned it: exact
+  // counts, persistent scatter); without a spill the two launches leave at once
+  {
+    using FT = MsdFallTile;
+    hipLaunchKernelGGL((grs::grs_seg_hist<uint32_t, 1>), dim3(2 * s->cus), dim3(256), 0, stream, src,
+                       recf, hdrf, 24, exact, st0, 256u);
+    GRS_HIP(hipGetLastError());
+    hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
+                       dim3(s->cus), dim3(FT::BLOCK), 0, stream, src, alt, nullptr, nullptr, d1, recf,
+                       hdrf, exact, 256u, tickets + 4 * GRS_XCDS, st0, st1, err, nullptr);
+    GRS_HIP(hipGetLastError());
+  }
   if ((r = mark()) != GRS_OK) return r;
   // H2: byte-2 histogram per top-byte bucket over alt; zeroes P2's status; plans P2's tiles
   {
-    const dim3 grid((n + GRS_H2_CHUNK - 1) / GRS_H2_CHUNK);
+    const dim3 grid(n / GRS_H2_CHUNK + 257);
     if (xl)
-      hipLaunchKernelGGL((grs::grs_msd_hist2<XL::TILE>), grid, dim3(1024), 0, stream, alt, n, h2, st1,
-                         static_cast<uint32_t>(words2), hist, rec2, hdr2);
+      hipLaunchKernelGGL((grs::grs_msd_hist2<XL::TILE>), grid, dim3(1024), 0, stream, alt, h2, st1,
+                         static_cast<uint32_t>(words2), samp, mult, pad, totals, exact, rec2, hdr2);
     else
-      hipLaunchKernelGGL((grs::grs_msd_hist2<Big::TILE>), grid, dim3(1024), 0, stream, alt, n, h2, st1,
-                         static_cast<uint32_t>(words2), hist, rec2, hdr2);
+      hipLaunchKernelGGL((grs::grs_msd_hist2<Big::TILE>), grid, dim3(1024), 0, stream, alt, h2, st1,
+                         static_cast<uint32_t>(words2), samp, mult, pad, totals, exact, rec2, hdr2);
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
@@ -1028,7 +1065,7 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
   GRS_HIP(hipGetLastError());
   if ((r = mark()) != GRS_OK) return r;
   if (evs) {
-    s->info[s->calls % s->ring] = {ev, 5, false, 1};
+    s->info[s->calls % s->ring] = {ev, 6, false, 1};
     ++s->calls;
   }
   return GRS_OK;

@@ -36,7 +36,7 @@ namespace grs {
 // ---------------------------------------------------------------------------------------
 // Segment sources of a plan: sizes (starts are their exclusive scan: the buckets of a pass),
 // explicit (start, length) lists, or offsets (num + 1 words, segment i = [off[i], off[i+1])).
-enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2 };
+enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2, kSegMoved = 3 };
 
 // LDS of the planner: 6 words per segment (tile, row and group prefixes, start, length,
 // histogram row); larger tables keep them in global scratch (`spill`, 6 * (nseg + 1) words).
@@ -76,7 +76,9 @@ __device__ __forceinline__ void block_scan(uint32_t (&v)[NV], uint32_t* wsum, ui
 // and starts new look-back groups, a segment of one tile is solo (no status words).
 // Sources: kSegSizes a = sizes (starts = their scan; histogram row = segment index);
 // kSegList a = starts, b = lengths, c = histogram rows; kSegOffsets a = offsets (histogram row =
-// segment index).  hdr[0] = tiles, hdr[1] = groups, hdr[2] = status rows.
+// segment index); kSegMoved a = where each segment's keys are read, b = lengths, c = where its
+// sorted runs go (histogram row = segment index).  hdr[0] = tiles, hdr[1] = groups, hdr[2] =
+// status rows.
 // lds: GRS_PLAN_LDS_WORDS words.
 template <uint32_t TILE, int BLOCK, int SRC>
 __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
@@ -92,7 +94,7 @@ __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* _
   uint32_t* const gpre = rpre + cap;
   uint32_t* const sst = gpre + cap;
   uint32_t* const sln = sst + cap;
-  uint32_t* const shr = sln + cap;
+  uint32_t* const shr = sln + cap;   // histogram row; kSegMoved: the output start
   uint32_t* const wsum = lds + 6 * GRS_PLAN_LDS_SEGS;
   uint32_t carry[4] = {0, 0, 0, 0};   // tiles, rows, groups, start (sizes source)
   for (uint32_t c0 = 0; c0 < nseg; c0 += BLOCK) {
@@ -101,7 +103,7 @@ __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* _
     if (i < nseg) {
       if constexpr (SRC == kSegSizes) {
         len = a[i];
-      } else if constexpr (SRC == kSegList) {
+      } else if constexpr (SRC == kSegList || SRC == kSegMoved) {
         st = a[i];
         len = b[i];
         hr = c[i];
@@ -139,8 +141,9 @@ __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* _
     const uint32_t len = sln[lo];
     const uint32_t q = j / G;
     const uint32_t flags = (j % G) | (min(G, tl - q * G) << 4) | ((tl == 1 ? 1u : 0u) << 8) | (q << 9);
+    const uint32_t out = SRC == kSegMoved ? shr[lo] : sst[lo];
     rec[tk] = SegTile{rpre[lo] + j, gpre[lo] + q, flags, sst[lo] + j * TILE, min(TILE, len - j * TILE),
-                      sst[lo], len, shr[lo]};
+                      out, len, SRC == kSegMoved ? lo : shr[lo]};
   }
   if (t == 0) {
     hdr[0] = tiles;
@@ -203,75 +206,158 @@ __global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
 // MSD u32 sort: H2 and P3
 // ---------------------------------------------------------------------------------------
 #define GRS_H2_CHUNK 262144
-#define GRS_H2_WIN 2        // buckets a block counts in LDS; keys of later buckets: global adds
 #define GRS_H2_COPIES 32
+#define GRS_MSD_SAMPLE_CHUNKS 16384   // 64-key chunks the sample reads (2^20 keys)
 
-// H2: h2[(top byte) * 256 + byte 2] over keys grouped by top byte (P1's output); a block's
-// chunk of GRS_H2_CHUNK keys meets at most a few buckets.  Also zeroes `zero_words` of `zero`
-// (P2's status layout) and block 0 plans P2's tiles from the top-byte sizes (hist1).
-template <uint32_t TILE2>
-__global__ __launch_bounds__(1024) void grs_msd_hist2(const uint32_t* __restrict__ keys, uint32_t n,
-                                                      uint32_t* __restrict__ h2,
-                                                      uint32_t* __restrict__ zero, uint32_t zero_words,
-                                                      const uint32_t* __restrict__ hist1,
-                                                      SegTile* __restrict__ rec2,
-                                                      uint32_t* __restrict__ hdr2) {
-  constexpr uint32_t B = 1024;
-  constexpr uint32_t LW = GRS_H2_WIN * 256 * GRS_H2_COPIES;
-  static_assert(LW >= GRS_PLAN_LDS_WORDS, "the planner reuses the histogram's LDS");
-  __shared__ __attribute__((aligned(16))) uint32_t h[LW];
-  const uint32_t t = threadIdx.x;
-  for (uint32_t i = t; i < LW; i += B) h[i] = 0;
-  for (uint32_t i = blockIdx.x * B + t; i < zero_words; i += gridDim.x * B) zero[i] = 0;
-  const uint32_t c0 = blockIdx.x * GRS_H2_CHUNK;
-  const uint32_t len = min(static_cast<uint32_t>(GRS_H2_CHUNK), n - c0);
-  const uint32_t s0 = keys[c0] >> 24;
+// S: the top byte's histogram from an evenly spaced sample of 64-key chunks (all keys when
+// n <= 64 * chunks), added into samp[256] (zero); also does the clearing the LSD sort's
+// histogram kernel does (P1's status, the next call's control block) plus clear2 (h2 and the
+// big-segment counters).
+__global__ __launch_bounds__(256) void grs_msd_sample(const uint32_t* __restrict__ keys, uint32_t n,
+                                                      uint32_t* __restrict__ samp,
+                                                      uint32_t* __restrict__ clear, uint32_t clear_words,
+                                                      uint32_t* __restrict__ clear_ctrl,
+                                                      uint32_t* __restrict__ clear2, uint32_t clear2_words) {
+  __shared__ uint32_t h[256];
+  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1);
+  h[t] = 0;
+  const uint32_t gs = gridDim.x * 256;
+  for (uint32_t i = blockIdx.x * 256 + t; i < clear_words; i += gs) clear[i] = 0;
+  for (uint32_t i = blockIdx.x * 256 + t; i < clear2_words; i += gs) clear2[i] = 0;
+  constexpr uint32_t H = GRS_CTRL_HIST_WORDS, TK = GRS_MAX_PASSES * GRS_XCDS;
+  for (uint32_t i = blockIdx.x * 256 + t; i < H + TK; i += gs) clear_ctrl[i] = 0;
   __syncthreads();
-  uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
-  auto count = [&](uint32_t k) {
-    const uint32_t s = (k >> 24) - s0;
-    if (s < GRS_H2_WIN)
-      atomicAdd(base + (s * 256 + ((k >> 16) & 255u)) * GRS_H2_COPIES, 1u);
-    else
-      atomicAdd(&h2[k >> 16], 1u);
-  };
-  const uint32_t* kc = keys + c0;
-  const bool al = (reinterpret_cast<uintptr_t>(kc) & 15u) == 0;
-  const uint32_t nv = al ? len / 4 : 0u;
-  const uint4* kv = reinterpret_cast<const uint4*>(kc);
-  uint32_t v = t;
-  for (; v + 3 * B < nv; v += 4 * B) {
-    uint4 x[4];
+  constexpr uint32_t C = GRS_MSD_SAMPLE_CHUNKS;
+  if (n <= C * GRS_WAVE) {
+    for (uint32_t i = blockIdx.x * 256 + t; i < n; i += gs) atomicAdd(&h[keys[i] >> 24], 1u);
+  } else {
+    // every wave's chunks loaded before any is counted (the loads overlap)
+    constexpr uint32_t U = 4;
+    const uint32_t waves = gridDim.x * 4;
+    for (uint32_t c0 = blockIdx.x * 4 + (t >> 6); c0 < C; c0 += U * waves) {
+      uint32_t k[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = kv[v + u * B];
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t c = c0 + u * waves;
+        const uint32_t pos = static_cast<uint32_t>(static_cast<uint64_t>(c) * (n - GRS_WAVE) / (C - 1));
+        k[u] = c < C ? keys[pos + lane] : 0u;
+      }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      count(x[u].x);
-      count(x[u].y);
-      count(x[u].z);
-      count(x[u].w);
+      for (uint32_t u = 0; u < U; ++u)
+        if (c0 + u * waves < C) atomicAdd(&h[k[u] >> 24], 1u);
     }
   }
-  for (; v < nv; v += B) {
-    const uint4 x = kv[v];
-    count(x.x);
-    count(x.y);
-    count(x.z);
-    count(x.w);
-  }
-  for (uint32_t i = nv * 4 + t; i < len; i += B) count(kc[i]);
   __syncthreads();
-  for (uint32_t i = t; i < GRS_H2_WIN * 256; i += B) {
-    const uint32_t* row = h + i * GRS_H2_COPIES;
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
-    const uint32_t s = s0 + i / 256;
-    if (c != 0 && s < 256) atomicAdd(&h2[s * 256 + i % 256], c);
+  if (h[t] != 0u) atomicAdd(&samp[t], h[t]);
+}
+
+// The top-byte bucket table after P1 (every H2 block rebuilds it in LDS): in[s] = where bucket
+// s's keys lie in alt, len[s] = its keys, out[s] = where its sorted keys go.  P1's regions when
+// no run outgrew its region (totals[256] == 0), the redone exact layout otherwise.
+__device__ void msd_bucket_table(const uint32_t* __restrict__ samp, unsigned long long mult,
+                                 uint32_t pad, const uint32_t* __restrict__ totals,
+                                 const uint32_t* __restrict__ exact, uint32_t* in,
+                                 uint32_t* len, uint32_t* out, uint32_t* wsum) {
+  const uint32_t t = threadIdx.x;   // blockDim >= 256
+  const bool redo = totals[256] != 0u;
+  uint32_t v[2] = {0, 0}, tot[2];
+  if (t < 256) {
+    const uint32_t l = redo ? exact[t] : totals[t];
+    const uint32_t r = redo ? l : static_cast<uint32_t>((static_cast<unsigned long long>(samp[t]) * mult) >> 20) + pad;
+    v[0] = l;
+    v[1] = r;
+    len[t] = l;
   }
-  if (blockIdx.x == 0) {   // P2's tiles: the 256 top-byte buckets (final since H1)
+  block_scan<1024, 2>(v, wsum, tot);
+  if (t < 256) {
+    out[t] = v[0];
+    in[t] = v[1];
+  }
+  __syncthreads();
+}
+
+// H2: h2[(top byte) * 256 + byte 2] over P1's output, one 256K-key chunk of one bucket per
+// block (grid >= n / chunk + 256); zeroes `zero_words` of `zero` (P2's status) and block 0 plans
+// P2's tiles (bucket s read at in[s], written at out[s]).
+// Two 1024-thread blocks per CU (8 waves per SIMD: 64 VGPRs; 54 KB of LDS each): one alone
+// leaves the CU's read queue half empty (0.29 against 0.18 ms at 2^28 keys).
+template <uint32_t TILE2>
+__global__ __launch_bounds__(1024, 8) void grs_msd_hist2(
+    const uint32_t* __restrict__ keys, uint32_t* __restrict__ h2, uint32_t* __restrict__ zero,
+    uint32_t zero_words, const uint32_t* __restrict__ samp, unsigned long long mult, uint32_t pad,
+    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ exact,
+    SegTile* __restrict__ rec2, uint32_t* __restrict__ hdr2) {
+  constexpr uint32_t B = 1024;
+  constexpr uint32_t LW = 256 * GRS_H2_COPIES;
+  constexpr uint32_t LOW = LW > GRS_PLAN_LDS_WORDS ? LW : GRS_PLAN_LDS_WORDS;
+  // histogram (or, block 0 at the end, the planner's LDS) | bucket table
+  __shared__ __attribute__((aligned(16))) uint32_t h[LOW + 4 * 257 + 64];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = blockIdx.x * B + t; i < zero_words; i += gridDim.x * B) zero[i] = 0;
+  uint32_t* const in = h + LOW;
+  uint32_t* const len = in + 256;
+  uint32_t* const out = len + 256;
+  uint32_t* const cpre = out + 256;
+  uint32_t* const wsum = cpre + 257;
+  msd_bucket_table(samp, mult, pad, totals, exact, in, len, out, wsum);
+  // this block's chunk: bucket s, chunk j of it
+  uint32_t v[1] = {t < 256 ? (len[t] + GRS_H2_CHUNK - 1) / GRS_H2_CHUNK : 0u}, tot[1];
+  block_scan<1024, 1>(v, wsum, tot);
+  if (t < 256) cpre[t] = v[0];
+  if (t == 0) cpre[256] = tot[0];
+  for (uint32_t i = t; i < LW; i += B) h[i] = 0;
+  __syncthreads();
+  const uint32_t b = blockIdx.x;
+  if (b < cpre[256]) {
+    uint32_t lo = 0, hi = 256;   // the largest s with cpre[s] <= b
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cpre[mid] <= b) lo = mid; else hi = mid;
+    }
+    const uint32_t s = lo, j = b - cpre[s];
+    const uint32_t c0 = in[s] + j * GRS_H2_CHUNK;
+    const uint32_t cl = min(static_cast<uint32_t>(GRS_H2_CHUNK), len[s] - j * GRS_H2_CHUNK);
+    uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
+    auto count = [&](uint32_t k) { atomicAdd(base + ((k >> 16) & 255u) * GRS_H2_COPIES, 1u); };
+    const uint32_t* kc = keys + c0;
+    // 16-B loads from the first aligned key on
+    const uint32_t head = min(cl, static_cast<uint32_t>((4u - ((reinterpret_cast<uintptr_t>(kc) >> 2) & 3u)) & 3u));
+    if (t < head) count(kc[t]);
+    const uint32_t nv = (cl - head) / 4;
+    const uint4* kv = reinterpret_cast<const uint4*>(kc + head);
+    uint32_t i = t;
+    for (; i + 3 * B < nv; i += 4 * B) {
+      uint4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = kv[i + u * B];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        count(x[u].x);
+        count(x[u].y);
+        count(x[u].z);
+        count(x[u].w);
+      }
+    }
+    for (; i < nv; i += B) {
+      const uint4 x = kv[i];
+      count(x.x);
+      count(x.y);
+      count(x.z);
+      count(x.w);
+    }
+    for (uint32_t r = head + nv * 4 + t; r < cl; r += B) count(kc[r]);
     __syncthreads();
-    seg_plan_block<TILE2, B, kSegSizes>(hist1, nullptr, nullptr, 256u, nullptr, rec2, hdr2, h);
+    if (t < 256) {
+      const uint32_t* row = h + t * GRS_H2_COPIES;
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
+      if (c != 0) atomicAdd(&h2[s * 256 + t], c);
+    }
+  }
+  if (blockIdx.x == 0) {   // P2's tiles: bucket s read at in[s], sorted into out[s]
+    __syncthreads();
+    seg_plan_block<TILE2, B, kSegMoved>(in, len, out, 256u, nullptr, rec2, hdr2, h);
   }
 }
 

@@ -185,6 +185,19 @@ struct TileSpan {
   }
 };
 
+// One tile of a segmented pass, as the planner (grs_seg_plan, grs_msd.hpp) lays it out.
+struct SegTile {
+  uint32_t row;        // tile word row of the status layout (solo tiles: none)
+  uint32_t group;      // look-back group of the tile
+  uint32_t flags;      // place in the group (bits 0-3) | tiles of the group (4-7) | solo (8)
+                       // | the group's place in its segment (9-31)
+  uint32_t base;       // first key of the tile
+  uint32_t valid;      // keys in the tile
+  uint32_t seg_start;  // first key of the segment
+  uint32_t seg_len;    // keys in the segment
+  uint32_t seg;        // histogram row of the segment
+};
+
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, bool CNT16 = false,
           bool IDX = false, int ROUNDS = 1>
 struct V4Smem {
@@ -208,7 +221,8 @@ template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typenam
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
                          (OPT & 1024) != 0 ? 2 : 1>;
 
-// OPT bits of the shipped pass (grs_capi.hip picks them per shape):
+// OPT bits of the shipped pass (grs_capi.hip picks them per shape; 131072 = region pass, set by
+// grs_onesweep_region only):
 //   16   look-back issued after the reorder (default: before it, overlapped with nothing)
 //   256  16-bit wave counters (two digits per LDS word: half the counter LDS)
 //   512  ballot-match ranking instead of lane-ordered LDS atomics (the fallback when the
@@ -298,7 +312,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
     uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, PassDebug dbg,
-    uint32_t* __restrict__ digit_starts = nullptr) {
+    uint32_t* __restrict__ digit_starts = nullptr, uint32_t* __restrict__ region_totals = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr bool MATCH = (OPT & 512) != 0;
@@ -485,6 +499,16 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         solo ? 0u
              : lb.finish(status, gacc, ginc, tile, sp.jg, sp.group, sp.in_group, t, gold, publish,
                          error_word, dbg.spin_limit);
+    if constexpr ((OPT & 131072) != 0) {
+      // region pass (grs_onesweep_region): gh is digit t's region, not its count; the last
+      // ticket's look-back covers every other tile, so it knows each digit's total and whether
+      // a run outgrew its region
+      if (tile + 1u == tiles) {
+        const uint32_t tot = prefix + publish;
+        region_totals[t] = tot;
+        if (tot > gh) atomicOr(&region_totals[RADIX], 1u);
+      }
+    }
     uint32_t start = gstart + prefix;
     if constexpr (!IDX) {
       // A timed-out look-back only underestimates this pass's prefixes, but the next pass of
@@ -609,6 +633,61 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
                                                  error_word, PassDebug::read(error_word));
 }
 
+// The MSD sort's first scatter without an upfront histogram (grs_msd.hpp): digit d's run goes
+// to a REGION of R_d = (sample[d] * mult >> 20) + pad keys -- the sampled share of the top byte,
+// with slack -- instead of its exact place, so the keys need no counting read before the pass.
+// region_len = sum of the regions (the clamp bound).  The last ticket writes the digit totals
+// to totals[0..RADIX) and sets totals[RADIX] when a run outgrew its region; it then also plans
+// the redo (the whole input as one segment of TILEF-key tiles, for grs_seg_hist and a persistent
+// grs_onesweep_seg) into redo_rec / redo_hdr, or writes an empty plan.
+template <typename K, int RB, int BLOCK, int ITEMS, int MINW, int OPT, uint32_t TILEF>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, uint32_t n, const RadixDigit<K> dig,
+    const uint32_t* __restrict__ sample, unsigned long long mult, uint32_t pad,
+    uint32_t region_len, uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
+    uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word,
+    uint32_t* __restrict__ totals, SegTile* __restrict__ redo_rec, uint32_t* __restrict__ redo_hdr) {
+  constexpr int ROPT = OPT | 131072;
+  using SM = V4SmemFor<K, false, RB, BLOCK, ITEMS, ROPT, RadixDigit<K>>;
+  __shared__ SM sm;
+  const uint32_t t = threadIdx.x;
+  uint32_t tt = t;
+  asm volatile("" : "+v"(tt));
+  K key[ITEMS];
+  uint32_t val[ITEMS];
+  if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+  for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+  __syncthreads();
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+  tile_load<K, false, BLOCK, ITEMS, ROPT>(key, val, keys_in, nullptr, n, tile, tt);
+  const uint32_t gh =
+      t < static_cast<uint32_t>(SM::RADIX)
+          ? static_cast<uint32_t>((static_cast<unsigned long long>(sample[t]) * mult) >> 20) + pad
+          : 0u;
+  TileSpan sp = TileSpan::whole(tile, n, SM::TILE);
+  sp.seg_len = region_len;
+  onesweep_tile<K, false, RB, BLOCK, ITEMS, ROPT>(sm, sp, key, val, keys_in, keys_out, nullptr,
+                                                  nullptr, n, dig, gh, ticket, status, status_next,
+                                                  error_word, PassDebug::read(error_word), nullptr,
+                                                  totals);
+  if (tile + 1u == sp.tiles) {   // the redo's plan (its digit threads wrote the spill flag)
+    __syncthreads();
+    constexpr uint32_t G = GRS_LB_GROUP;
+    const bool spill = __hip_atomic_load(&totals[SM::RADIX], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    const uint32_t T = spill ? n / TILEF + (n % TILEF != 0u ? 1u : 0u) : 0u;
+    for (uint32_t k = t; k < T; k += BLOCK) {
+      const uint32_t q = k / G;
+      const uint32_t flags = (k % G) | (min(G, T - q * G) << 4) | ((T == 1 ? 1u : 0u) << 8) | (q << 9);
+      redo_rec[k] = SegTile{k, q, flags, k * TILEF, min(TILEF, n - k * TILEF), 0u, n, 0u};
+    }
+    if (t == 0) {
+      redo_hdr[0] = T;
+      redo_hdr[1] = T > 1 ? (T + G - 1) / G : 0u;
+      redo_hdr[2] = T > 1 ? T : 0u;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // persistent pass with next-tile prefetch
 // ---------------------------------------------------------------------------------------
@@ -657,19 +736,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
 // ---------------------------------------------------------------------------------------
 // segmented pass: every segment of a table sorted by one digit on its own
 // ---------------------------------------------------------------------------------------
-// One tile of a segmented pass, as the planner (grs_seg_plan, grs_msd.hpp) lays it out.
-struct SegTile {
-  uint32_t row;        // tile word row of the status layout (solo tiles: none)
-  uint32_t group;      // look-back group of the tile
-  uint32_t flags;      // place in the group (bits 0-3) | tiles of the group (4-7) | solo (8)
-                       // | the group's place in its segment (9-31)
-  uint32_t base;       // first key of the tile
-  uint32_t valid;      // keys in the tile
-  uint32_t seg_start;  // first key of the segment
-  uint32_t seg_len;    // keys in the segment
-  uint32_t seg;        // histogram row of the segment
-};
-
 // MSD sort and segmented sorts (grs_capi.hip): the same tile code as grs_onesweep_v4, over the
 // tiles of a segment table -- tiles never straddle a segment, each segment's look-back chain
 // restarts at its first tile, and its digit runs start at the segment's own first key, from
@@ -708,7 +774,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
     tile_load_at<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, 0u, sp.base, sp.valid, tt);
     const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) && !solo
                             ? hist[static_cast<size_t>(r.seg) * hist_stride + t] : 0u;
-    uint32_t* ds = digit_starts != nullptr && r.base == r.seg_start
+    // the segment's first tile (place 0 of group 0; its keys may be read from elsewhere than
+    // its runs go, so base == seg_start does not tell)
+    const bool first = (r.flags & 15u) == 0u && (r.flags >> 9) == 0u;
+    uint32_t* ds = digit_starts != nullptr && first
                        ? digit_starts + static_cast<size_t>(r.seg) * SM::RADIX : nullptr;
     onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, false, true>(sm, sp, key, val, keys_in, keys_out, vals_in,
                                                    vals_out, 0u, dig, gh, ticket, status,
