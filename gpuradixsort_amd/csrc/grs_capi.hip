@@ -399,7 +399,7 @@ using MsdFallTile = BigTile<uint32_t, false>;
 constexpr uint32_t kMsdTileF = MsdFallTile::TILE;
 
 struct MsdLayout {   // word offsets into msd_buf
-  size_t h2, big, dstart, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
+  size_t h2, big, dstart, tab, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
   size_t r2, rf, bl, mr;   // capacities: P2 records, fallback records, big list, histogram rows
   static MsdLayout of(size_t cap) {
     MsdLayout L{};
@@ -413,6 +413,7 @@ struct MsdLayout {   // word offsets into msd_buf
     L.h2 = take(65536 + 64);   // h2 | big counters: zeroed together by H1
     L.big = L.h2 + 65536;
     L.dstart = take(65536);
+    L.tab = take(4 * 257);
     L.hdr2 = take(4);
     L.rec2 = take(L.r2 * 8);
     L.hdrf = take(4);
@@ -1013,15 +1014,19 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
-  // H2: byte-2 histogram per top-byte bucket over alt; zeroes P2's status; plans P2's tiles
+  // P2's plan (the bucket table: P1's regions, or the redo's exact layout), then H2: byte-2
+  // histogram per top-byte bucket over alt; zeroes P2's status
   {
-    const dim3 grid(n / GRS_H2_CHUNK + 257);
+    uint32_t* const tab = mb + L.tab;
     if (xl)
-      hipLaunchKernelGGL((grs::grs_msd_hist2<XL::TILE>), grid, dim3(1024), 0, stream, alt, h2, st1,
-                         static_cast<uint32_t>(words2), samp, mult, pad, totals, exact, rec2, hdr2);
+      hipLaunchKernelGGL((grs::grs_msd_plan2<XL::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
+                         totals, exact, tab, rec2, hdr2);
     else
-      hipLaunchKernelGGL((grs::grs_msd_hist2<Big::TILE>), grid, dim3(1024), 0, stream, alt, h2, st1,
-                         static_cast<uint32_t>(words2), samp, mult, pad, totals, exact, rec2, hdr2);
+      hipLaunchKernelGGL((grs::grs_msd_plan2<Big::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
+                         totals, exact, tab, rec2, hdr2);
+    GRS_HIP(hipGetLastError());
+    hipLaunchKernelGGL(grs::grs_msd_hist2, dim3(n / GRS_H2_CHUNK + 257), dim3(1024), 0, stream, alt, h2,
+                       st1, static_cast<uint32_t>(words2), tab);
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;

@@ -251,113 +251,119 @@ __global__ __launch_bounds__(256) void grs_msd_sample(const uint32_t* __restrict
   if (h[t] != 0u) atomicAdd(&samp[t], h[t]);
 }
 
-// The top-byte bucket table after P1 (every H2 block rebuilds it in LDS): in[s] = where bucket
-// s's keys lie in alt, len[s] = its keys, out[s] = where its sorted keys go.  P1's regions when
-// no run outgrew its region (totals[256] == 0), the redone exact layout otherwise.
+// The top-byte bucket table after P1: in[s] = where bucket s's keys lie in alt, len[s] = its
+// keys, out[s] = where its sorted keys go, cpre[s] = H2 chunks before bucket s (cpre[256] =
+// all).  P1's regions when no run outgrew its region (totals[256] == 0), the redone exact
+// layout otherwise.  One block computes it into LDS (in, len, out, cpre: 4 x 257 words).
 __device__ void msd_bucket_table(const uint32_t* __restrict__ samp, unsigned long long mult,
                                  uint32_t pad, const uint32_t* __restrict__ totals,
-                                 const uint32_t* __restrict__ exact, uint32_t* in,
-                                 uint32_t* len, uint32_t* out, uint32_t* wsum) {
-  const uint32_t t = threadIdx.x;   // blockDim >= 256
+                                 const uint32_t* __restrict__ exact, uint32_t* in, uint32_t* len,
+                                 uint32_t* out, uint32_t* cpre, uint32_t* wsum) {
+  const uint32_t t = threadIdx.x;   // blockDim == 1024
   const bool redo = totals[256] != 0u;
-  uint32_t v[2] = {0, 0}, tot[2];
+  uint32_t v[3] = {0, 0, 0}, tot[3];
   if (t < 256) {
     const uint32_t l = redo ? exact[t] : totals[t];
     const uint32_t r = redo ? l : static_cast<uint32_t>((static_cast<unsigned long long>(samp[t]) * mult) >> 20) + pad;
     v[0] = l;
     v[1] = r;
+    v[2] = (l + GRS_H2_CHUNK - 1) / GRS_H2_CHUNK;
     len[t] = l;
   }
-  block_scan<1024, 2>(v, wsum, tot);
+  block_scan<1024, 3>(v, wsum, tot);
   if (t < 256) {
     out[t] = v[0];
     in[t] = v[1];
+    cpre[t] = v[2];
   }
+  if (t == 0) cpre[256] = tot[2];
   __syncthreads();
 }
 
-// H2: h2[(top byte) * 256 + byte 2] over P1's output, one 256K-key chunk of one bucket per
-// block (grid >= n / chunk + 256); zeroes `zero_words` of `zero` (P2's status) and block 0 plans
-// P2's tiles (bucket s read at in[s], written at out[s]).
-// Two 1024-thread blocks per CU (8 waves per SIMD: 64 VGPRs; 54 KB of LDS each): one alone
-// leaves the CU's read queue half empty (0.29 against 0.18 ms at 2^28 keys).
+// The plan of P2 (one block): the bucket table (tab: in | len | out | cpre, 4 x 257 words, for
+// H2) and P2's tiles (bucket s read at in[s], its runs written from out[s]).
 template <uint32_t TILE2>
-__global__ __launch_bounds__(1024, 8) void grs_msd_hist2(
-    const uint32_t* __restrict__ keys, uint32_t* __restrict__ h2, uint32_t* __restrict__ zero,
-    uint32_t zero_words, const uint32_t* __restrict__ samp, unsigned long long mult, uint32_t pad,
-    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ exact,
-    SegTile* __restrict__ rec2, uint32_t* __restrict__ hdr2) {
+__global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict__ samp,
+                                                      unsigned long long mult, uint32_t pad,
+                                                      const uint32_t* __restrict__ totals,
+                                                      const uint32_t* __restrict__ exact,
+                                                      uint32_t* __restrict__ tab,
+                                                      SegTile* __restrict__ rec2,
+                                                      uint32_t* __restrict__ hdr2) {
+  __shared__ uint32_t lds[GRS_PLAN_LDS_WORDS + 4 * 257 + 64];
+  uint32_t* const in = lds + GRS_PLAN_LDS_WORDS;
+  uint32_t* const len = in + 257;
+  uint32_t* const out = len + 257;
+  uint32_t* const cpre = out + 257;
+  uint32_t* const wsum = cpre + 257;
+  msd_bucket_table(samp, mult, pad, totals, exact, in, len, out, cpre, wsum);
+  for (uint32_t i = threadIdx.x; i < 4 * 257; i += 1024) tab[i] = in[i];
+  seg_plan_block<TILE2, 1024, kSegMoved>(in, len, out, 256u, nullptr, rec2, hdr2, lds);
+}
+
+// H2: h2[(top byte) * 256 + byte 2] over P1's output, one 256K-key chunk of one bucket per
+// block (grid >= n / chunk + 256; tab from grs_msd_plan2); zeroes `zero_words` of `zero` (P2's
+// status).  Two 1024-thread blocks per CU (8 waves per SIMD).
+__global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const uint32_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ h2,
+                                                         uint32_t* __restrict__ zero,
+                                                         uint32_t zero_words,
+                                                         const uint32_t* __restrict__ tab) {
   constexpr uint32_t B = 1024;
   constexpr uint32_t LW = 256 * GRS_H2_COPIES;
-  constexpr uint32_t LOW = LW > GRS_PLAN_LDS_WORDS ? LW : GRS_PLAN_LDS_WORDS;
-  // histogram (or, block 0 at the end, the planner's LDS) | bucket table
-  __shared__ __attribute__((aligned(16))) uint32_t h[LOW + 4 * 257 + 64];
+  __shared__ __attribute__((aligned(16))) uint32_t h[LW];
+  __shared__ uint32_t cpre[257];
   const uint32_t t = threadIdx.x;
   for (uint32_t i = blockIdx.x * B + t; i < zero_words; i += gridDim.x * B) zero[i] = 0;
-  uint32_t* const in = h + LOW;
-  uint32_t* const len = in + 256;
-  uint32_t* const out = len + 256;
-  uint32_t* const cpre = out + 256;
-  uint32_t* const wsum = cpre + 257;
-  msd_bucket_table(samp, mult, pad, totals, exact, in, len, out, wsum);
-  // this block's chunk: bucket s, chunk j of it
-  uint32_t v[1] = {t < 256 ? (len[t] + GRS_H2_CHUNK - 1) / GRS_H2_CHUNK : 0u}, tot[1];
-  block_scan<1024, 1>(v, wsum, tot);
-  if (t < 256) cpre[t] = v[0];
-  if (t == 0) cpre[256] = tot[0];
   for (uint32_t i = t; i < LW; i += B) h[i] = 0;
+  if (t < 257) cpre[t] = tab[3 * 257 + t];
   __syncthreads();
   const uint32_t b = blockIdx.x;
-  if (b < cpre[256]) {
-    uint32_t lo = 0, hi = 256;   // the largest s with cpre[s] <= b
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (cpre[mid] <= b) lo = mid; else hi = mid;
-    }
-    const uint32_t s = lo, j = b - cpre[s];
-    const uint32_t c0 = in[s] + j * GRS_H2_CHUNK;
-    const uint32_t cl = min(static_cast<uint32_t>(GRS_H2_CHUNK), len[s] - j * GRS_H2_CHUNK);
-    uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
-    auto count = [&](uint32_t k) { atomicAdd(base + ((k >> 16) & 255u) * GRS_H2_COPIES, 1u); };
-    const uint32_t* kc = keys + c0;
-    // 16-B loads from the first aligned key on
-    const uint32_t head = min(cl, static_cast<uint32_t>((4u - ((reinterpret_cast<uintptr_t>(kc) >> 2) & 3u)) & 3u));
-    if (t < head) count(kc[t]);
-    const uint32_t nv = (cl - head) / 4;
-    const uint4* kv = reinterpret_cast<const uint4*>(kc + head);
-    uint32_t i = t;
-    for (; i + 3 * B < nv; i += 4 * B) {
-      uint4 x[4];
+  if (b >= cpre[256]) return;
+  uint32_t lo = 0, hi = 256;   // the largest s with cpre[s] <= b
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (cpre[mid] <= b) lo = mid; else hi = mid;
+  }
+  const uint32_t s = lo, j = b - cpre[s];
+  const uint32_t c0 = tab[s] + j * GRS_H2_CHUNK;
+  const uint32_t cl = min(static_cast<uint32_t>(GRS_H2_CHUNK), tab[257 + s] - j * GRS_H2_CHUNK);
+  uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
+  auto count = [&](uint32_t k) { atomicAdd(base + ((k >> 16) & 255u) * GRS_H2_COPIES, 1u); };
+  const uint32_t* kc = keys + c0;
+  // 16-B loads from the first aligned key on
+  const uint32_t head = min(cl, static_cast<uint32_t>((4u - ((reinterpret_cast<uintptr_t>(kc) >> 2) & 3u)) & 3u));
+  if (t < head) count(kc[t]);
+  const uint32_t nv = (cl - head) / 4;
+  const uint4* kv = reinterpret_cast<const uint4*>(kc + head);
+  uint32_t i = t;
+  for (; i + 3 * B < nv; i += 4 * B) {
+    uint4 x[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = kv[i + u * B];
+    for (int u = 0; u < 4; ++u) x[u] = kv[i + u * B];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        count(x[u].x);
-        count(x[u].y);
-        count(x[u].z);
-        count(x[u].w);
-      }
-    }
-    for (; i < nv; i += B) {
-      const uint4 x = kv[i];
-      count(x.x);
-      count(x.y);
-      count(x.z);
-      count(x.w);
-    }
-    for (uint32_t r = head + nv * 4 + t; r < cl; r += B) count(kc[r]);
-    __syncthreads();
-    if (t < 256) {
-      const uint32_t* row = h + t * GRS_H2_COPIES;
-      uint32_t c = 0;
-#pragma unroll
-      for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
-      if (c != 0) atomicAdd(&h2[s * 256 + t], c);
+    for (int u = 0; u < 4; ++u) {
+      count(x[u].x);
+      count(x[u].y);
+      count(x[u].z);
+      count(x[u].w);
     }
   }
-  if (blockIdx.x == 0) {   // P2's tiles: bucket s read at in[s], sorted into out[s]
-    __syncthreads();
-    seg_plan_block<TILE2, B, kSegMoved>(in, len, out, 256u, nullptr, rec2, hdr2, h);
+  for (; i < nv; i += B) {
+    const uint4 x = kv[i];
+    count(x.x);
+    count(x.y);
+    count(x.z);
+    count(x.w);
+  }
+  for (uint32_t r = head + nv * 4 + t; r < cl; r += B) count(kc[r]);
+  __syncthreads();
+  if (t < 256) {
+    const uint32_t* row = h + t * GRS_H2_COPIES;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
+    if (c != 0) atomicAdd(&h2[s * 256 + t], c);
   }
 }
 
