@@ -388,29 +388,38 @@ bool use_xl(const grs_sorter* s, size_t n, size_t xl_tile) {
          (n + xl_tile - 1) / xl_tile >= 32u * static_cast<size_t>(std::max(1, s->cus));
 }
 
-// ---- MSD u32 sort (grs_msd.hpp): tables and their layout in the sorter's msd_buf ----
-// P3 shapes: one workgroup sorts a 16-bit segment of up to BLOCK * I keys in LDS.
-struct MsdLocalA { static constexpr int BLOCK = 256, I = 20; static constexpr bool C16 = false; };
-struct MsdLocalB { static constexpr int BLOCK = 512, I = 20; static constexpr bool C16 = false; };
-struct MsdLocalC { static constexpr int BLOCK = 768, I = 24; static constexpr bool C16 = true; };
-constexpr uint32_t kMsdSmaxMin = MsdLocalA::BLOCK * MsdLocalA::I;
-// fallback passes (segments longer than P3 takes): the big tile, persistent
-using MsdFallTile = BigTile<uint32_t, false>;
-constexpr uint32_t kMsdTileF = MsdFallTile::TILE;
+// ---- MSD sort (grs_msd.hpp): tables and their layout in the sorter's msd_buf ----
+// u32 keys, u32 keys + u32 payload, u64 keys (8-bit digits).
+// P3 shapes: one workgroup sorts a 16-bit segment of up to BLOCK * I elements in LDS.
+template <int B, int I_, bool C> struct MsdLocal {
+  static constexpr int BLOCK = B, I = I_;
+  static constexpr bool C16 = C;
+  static constexpr uint32_t SMAX = B * I_;
+};
+using MsdLocalA = MsdLocal<256, 20, false>;   // any element (40 KB of LDS at 8 B)
+using MsdLocalB = MsdLocal<512, 20, false>;
+using MsdLocalC = MsdLocal<768, 24, true>;    // 4-byte elements: two 72-KB workgroups per CU
+constexpr uint32_t kMsdSmaxMin = MsdLocalA::SMAX;
+// fallback and redo passes (persistent): the big tile of the key type; 17408 keys is the
+// smallest of them (u32 pairs, u64 keys), which sizes the tables
+constexpr uint32_t kMsdTileMin = 17408;
+static_assert(BigTile<uint32_t, true>::TILE == kMsdTileMin && BigTile<uint64_t, false>::TILE == kMsdTileMin &&
+              BigTile<uint32_t, false>::TILE > kMsdTileMin, "MSD table sizing");
 
 struct MsdLayout {   // word offsets into msd_buf
   size_t h2, big, dstart, tab, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
   size_t r2, rf, bl, mr;   // capacities: P2 records, fallback records, big list, histogram rows
-  static MsdLayout of(size_t cap) {
+  // nd: digits of the fallback (2 for u32 keys, 6 for u64)
+  static MsdLayout of(size_t cap, size_t nd) {
     MsdLayout L{};
     cap = std::max<size_t>(cap, 1);
-    L.r2 = cap / std::min(BigTile<uint32_t, false>::TILE, XLTile<uint32_t, false>::TILE) + 257;
+    L.r2 = cap / kMsdTileMin + 257;
     L.bl = std::min<size_t>(65536, cap / (kMsdSmaxMin + 1) + 2);
-    L.mr = cap / (kMsdTileF + 1) + 2;
-    L.rf = cap / kMsdTileF + L.bl + 1;
+    L.mr = cap / (kMsdTileMin + 1) + 2;
+    L.rf = cap / kMsdTileMin + L.bl + 1;
     size_t o = 0;
     auto take = [&](size_t w) { const size_t at = o; o += (w + 63) & ~static_cast<size_t>(63); return at; };
-    L.h2 = take(65536 + 64);   // h2 | big counters: zeroed together by H1
+    L.h2 = take(65536 + 64);   // h2 | big counters: zeroed together by the sample kernel
     L.big = L.h2 + 65536;
     L.dstart = take(65536);
     L.tab = take(4 * 257);
@@ -421,7 +430,7 @@ struct MsdLayout {   // word offsets into msd_buf
     L.bstart = take(L.bl);
     L.blen = take(L.bl);
     L.brow = take(L.bl);
-    L.rows = take(L.mr * 512);
+    L.rows = take(L.mr * nd * 256);
     L.spill = take(6 * (L.bl + 1));
     L.words = o;
     return L;
@@ -429,21 +438,22 @@ struct MsdLayout {   // word offsets into msd_buf
   // status words of P2 (256 buckets) and of the fallback passes
   static size_t status_words(size_t cap) {
     cap = std::max<size_t>(cap, 1);
-    const size_t t2 = cap / BigTile<uint32_t, false>::TILE + 257;
+    const size_t t2 = cap / kMsdTileMin + 257;
     const size_t w2 = (t2 + 2 * (t2 / GRS_LB_GROUP + 257)) * 256;
-    const size_t tf = 2 * (cap / kMsdTileF) + 2;            // tiles of multi-tile segments
-    const size_t gf = tf / GRS_LB_GROUP + cap / (kMsdTileF + 1) + 2;
+    const size_t tf = 2 * (cap / kMsdTileMin) + 2;            // tiles of multi-tile segments
+    const size_t gf = tf / GRS_LB_GROUP + cap / (kMsdTileMin + 1) + 2;
     return std::max(w2, (tf + 2 * gf) * 256);
   }
 };
 
-// Words of the sorter's second buffer for an MSD sorter: P1 writes its runs into sampled
-// regions (n + n/8 + 256 x 4096 + 256 keys at most, grs_msd.hpp).
+// Elements of the sorter's second buffer (per array) for an MSD sorter: P1 writes its runs
+// into sampled regions (n + n/8 + 256 x 4096 + 256 elements at most, grs_msd.hpp).
 size_t msd_alt_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 8 + 256 * 4096 + 1024; }
 
 bool msd_type(const grs_sorter* s) {
-  return s->key_type == GRS_KEY_U32 && !s->pairs && s->radix_bits == 8;
+  return s->radix_bits == 8 && !(s->key_type == GRS_KEY_U64 && s->pairs);
 }
+size_t msd_digits(const grs_sorter* s) { return s->key_type == GRS_KEY_U64 ? 6 : 2; }
 
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
 template <typename K, bool PAIRS>
@@ -466,12 +476,14 @@ size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
 size_t needed_status_words(const grs_sorter* s) {
   const size_t cap = std::max<size_t>(s->capacity, 1);
   const size_t radix = std::max<size_t>(size_t(1) << s->radix_bits, 16);
+  size_t w;
   if (s->key_type == GRS_KEY_U32)
-    return s->pairs ? max_status_words<uint32_t, true>(s, cap, radix)
-                    : std::max(max_status_words<uint32_t, false>(s, cap, radix),
-                               msd_type(s) ? MsdLayout::status_words(cap) : size_t(0));
-  return s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
-                  : max_status_words<uint64_t, false>(s, cap, radix);
+    w = s->pairs ? max_status_words<uint32_t, true>(s, cap, radix)
+                 : max_status_words<uint32_t, false>(s, cap, radix);
+  else
+    w = s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
+                 : max_status_words<uint64_t, false>(s, cap, radix);
+  return msd_type(s) ? std::max(w, MsdLayout::status_words(cap)) : w;
 }
 
 }  // namespace
@@ -623,19 +635,20 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   };
   if (s->pairs && key_type == GRS_KEY_U32) {
     // one allocation: keys | payload, or the same bytes as 8-byte (key, value) records (the
-    // record passes of run_sort)
-    alloc(&s->alt_keys, cap * 8);
-    if (st == GRS_OK) s->alt_vals = static_cast<uint32_t*>(s->alt_keys) + cap;
+    // record passes of run_sort); each array with the MSD sort's region slack
+    const size_t half = msd_type(s) ? msd_alt_words(cap) : cap;
+    alloc(&s->alt_keys, half * 8);
+    if (st == GRS_OK) s->alt_vals = static_cast<uint32_t*>(s->alt_keys) + half;
     s->alt_joint = true;
   } else if (msd_type(s)) {
-    alloc(&s->alt_keys, msd_alt_words(cap) * 4);   // + the MSD sort's region slack
+    alloc(&s->alt_keys, msd_alt_words(cap) * kb);   // + the MSD sort's region slack
   } else {
     alloc(&s->alt_keys, cap * kb);
     if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
   }
   alloc(reinterpret_cast<void**>(&s->status), 2 * s->status_words * 4);
   if (msd_type(s)) {
-    s->msd_bytes = MsdLayout::of(cap).words * 4;
+    s->msd_bytes = MsdLayout::of(cap, msd_digits(s)).words * 4;
     alloc(&s->msd_buf, s->msd_bytes);
   }
   alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
@@ -893,16 +906,16 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   return GRS_OK;
 }
 
-// ---- MSD-first u32 sort (grs_msd.hpp) ----
-// The P3 shape for n keys: a uniform 16-bit segment holds m = n / 65536 keys, +- sqrt(m); the
-// shape must take m + 8 sqrt(m) + 64 (longer segments take the segmented fallback).  0: none
-// fits (n above ~2^30.07): the LSD sort.
-int msd_local_shape(size_t n) {
+// ---- MSD-first sort (grs_msd.hpp) ----
+// The P3 shape for n elements of E bytes: a uniform 16-bit segment holds m = n / 65536, +-
+// sqrt(m); the shape must take m + 8 sqrt(m) + 64 (longer segments take the segmented
+// fallback).  0: none fits (the LSD sort).
+int msd_local_shape(size_t n, size_t elem) {
   const double m = static_cast<double>(n) / 65536.0;
   const double need = m + 8.0 * std::sqrt(m) + 64.0;
-  if (need <= MsdLocalA::BLOCK * MsdLocalA::I) return 1;
-  if (need <= MsdLocalB::BLOCK * MsdLocalB::I) return 2;
-  if (need <= MsdLocalC::BLOCK * MsdLocalC::I) return 3;
+  if (need <= MsdLocalA::SMAX) return 1;
+  if (need <= MsdLocalB::SMAX) return 2;
+  if (elem == 4 && need <= MsdLocalC::SMAX) return 3;
   return 0;
 }
 // From this many keys the MSD sort is the default (GRS_OPT_MSD = -1).
@@ -910,20 +923,27 @@ constexpr size_t kMsdMinN = size_t(1) << 26;
 
 bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
   if (!msd_type(s) || s->msd_mode == 0 || s->msd_buf == nullptr || s->rank_mode != 0) return false;
-  if (begin_bit != 0 || end_bit != 32 || msd_local_shape(n) == 0) return false;
+  const int kbits = s->key_type == GRS_KEY_U64 ? 64 : 32;
+  const size_t elem = kbits / 8 + (s->pairs ? 4 : 0);
+  if (begin_bit != 0 || end_bit != kbits || msd_local_shape(n, elem) == 0) return false;
   return s->msd_mode == 1 || n >= kMsdMinN;
 }
 
-// H1 -> P1 -> H2 (+ P2's plan) -> P2 -> P3 -> fallback (plan, histograms, two segmented LSD
-// passes over the segments P3 left; persistent grids that leave at once when there are none).
-// src_in (out of place): H1 and P1 read it; the result lands in keys either way.
-template <typename P3C>
-grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream,
-                   const uint32_t* src_in) {
-  using Big = BigTile<uint32_t, false>;
-  using XL = XLTile<uint32_t, false>;
-  using Small = SmallTile<uint32_t, false>;
-  using Dig = grs::RadixDigit<uint32_t>;
+// sample -> P1 (regions) -> [redo] -> P2's plan -> H2 -> P2 -> P3 -> fallback (plan,
+// histograms, a segmented LSD over the bits below the prefix for the segments P3 left;
+// persistent grids that leave at once when there are none).  src_in / vsrc_in (out of place):
+// the sample and P1 read them; the result lands in keys / vals either way.
+template <typename K, bool PAIRS, typename P3C>
+grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
+                   const K* src_in, const uint32_t* vsrc_in) {
+  using Big = BigTile<K, PAIRS>;
+  using XL = XLTile<K, PAIRS>;
+  using Small = SmallTile<K, PAIRS>;
+  using FT = BigTile<K, PAIRS>;   // the redo's and the fallback's persistent passes
+  using Dig = grs::RadixDigit<K>;
+  constexpr int KB = 8 * static_cast<int>(sizeof(K));
+  constexpr int ND = (KB - 16) / 8;
+  static_assert(!Big::TWO_ROUNDS, "u64 pairs take the LSD sort");
   constexpr uint32_t G = GRS_LB_GROUP;
   const bool big = use_big_tiles(s, n, Big::TILE);
   const bool xl = big && use_xl(s, n, XL::TILE);
@@ -934,7 +954,7 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
   const size_t words2 = (t2 + 2 * (t2 / G + 257)) * 256;
   if (words1 > s->status_words || words2 > s->status_words)
     return set_err(GRS_ECAPACITY, "status buffer too small");
-  const MsdLayout L = MsdLayout::of(s->capacity);
+  const MsdLayout L = MsdLayout::of(s->capacity, ND);
   if (t2 > L.r2) return set_err(GRS_ECAPACITY, "internal: MSD plan capacity");
   uint32_t* const mb = static_cast<uint32_t*>(s->msd_buf);
   uint32_t* const h2 = mb + L.h2;
@@ -944,15 +964,17 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
   auto* const rec2 = reinterpret_cast<grs::SegTile*>(mb + L.rec2);
   uint32_t* const hdrf = mb + L.hdrf;
   auto* const recf = reinterpret_cast<grs::SegTile*>(mb + L.recf);
-  uint32_t* const st0 = s->status;
-  uint32_t* const st1 = s->status + s->status_words;
+  uint32_t* const rows = mb + L.rows;
+  uint32_t* const st[2] = {s->status, s->status + s->status_words};
   uint32_t* const err = s->ctrl + GRS_CTRL_ERROR;
   uint32_t* const cb[2] = {s->ctrl, s->ctrl2};
   uint32_t* const hist = cb[s->cb_i];
   uint32_t* const tickets = hist + GRS_CTRL_TICKETS;
   uint32_t* const hist_next = cb[s->cb_i ^ 1];
-  const uint32_t* src = src_in ? src_in : keys;
-  uint32_t* const alt = static_cast<uint32_t*>(s->alt_keys);
+  const K* src = src_in ? src_in : keys;
+  const uint32_t* vsrc = src_in ? vsrc_in : vals;
+  K* const alt = static_cast<K*>(s->alt_keys);
+  uint32_t* const valt = PAIRS ? s->alt_vals : nullptr;
   int ev = 0;
   hipEvent_t* evs = s->ring ? s->ev + (s->calls % s->ring) * grs_sorter::EV_PER_CALL : nullptr;
   auto mark = [&]() -> grs_status {
@@ -977,23 +999,24 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
   if ((r = mark()) != GRS_OK) return r;
   if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = false;
-  // S: the top byte's sampled histogram; zeroes P1's status, the next call's control block, h2
+  // sample: the top byte's histogram; zeroes P1's status, the next call's control block, h2
   // and the big-segment counters
-  hipLaunchKernelGGL(grs::grs_msd_sample, dim3(1024), dim3(256), 0, stream, src, n, samp, st0,
+  hipLaunchKernelGGL((grs::grs_msd_sample<K>), dim3(1024), dim3(256), 0, stream, src, n, samp, st[0],
                      static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u);
   GRS_HIP(hipGetLastError());
   s->cb_i ^= 1;
   if ((r = mark()) != GRS_OK) return r;
   // P1: stable scatter by the top byte into the sampled regions, src -> alt (no counting read)
-  const Dig d1{24, 255u};
+  const Dig d1{KB - 8, 255u};
   {
     const uint32_t tiles = (n + tile1 - 1) / tile1;
     auto go = [&](auto tshape, auto optc) {
       using T = decltype(tshape);
       constexpr uint32_t opt = decltype(optc)::value;
-      hipLaunchKernelGGL((grs::grs_onesweep_region<uint32_t, 8, T::BLOCK, T::ITEMS, T::MINW, opt, kMsdTileF>),
-                         dim3(tiles), dim3(T::BLOCK), 0, stream, src, alt, n, d1, samp, mult, pad,
-                         static_cast<uint32_t>(region_len), tickets, st0, st1, err, totals, recf, hdrf);
+      hipLaunchKernelGGL((grs::grs_onesweep_region<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, opt, FT::TILE>),
+                         dim3(tiles), dim3(T::BLOCK), 0, stream, src, alt, vsrc, valt, n, d1, samp, mult,
+                         pad, static_cast<uint32_t>(region_len), tickets, st[0], st[1], err, totals,
+                         recf, hdrf);
     };
     if (xl) go(XL{}, std::integral_constant<uint32_t, XL::OPT>{});
     else if (big) go(Big{}, std::integral_constant<uint32_t, Big::OPT>{});
@@ -1003,16 +1026,13 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
   if ((r = mark()) != GRS_OK) return r;
   // a run outgrew its region: P1 again into the exact layout (P1's last tile planned it: exact
   // counts, persistent scatter); without a spill the two launches leave at once
-  {
-    using FT = MsdFallTile;
-    hipLaunchKernelGGL((grs::grs_seg_hist<uint32_t, 1>), dim3(2 * s->cus), dim3(256), 0, stream, src,
-                       recf, hdrf, 24, exact, st0, 256u);
-    GRS_HIP(hipGetLastError());
-    hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
-                       dim3(s->cus), dim3(FT::BLOCK), 0, stream, src, alt, nullptr, nullptr, d1, recf,
-                       hdrf, exact, 256u, tickets + 4 * GRS_XCDS, st0, st1, err, nullptr);
-    GRS_HIP(hipGetLastError());
-  }
+  hipLaunchKernelGGL((grs::grs_seg_hist<K, 1>), dim3(2 * s->cus), dim3(256), 0, stream, src, recf, hdrf,
+                     KB - 8, exact, st[0], 256u);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
+                     dim3(s->cus), dim3(FT::BLOCK), 0, stream, src, alt, vsrc, valt, d1, recf, hdrf,
+                     exact, 256u, tickets + 15 * GRS_XCDS, st[0], st[1], err, nullptr);
+  GRS_HIP(hipGetLastError());
   if ((r = mark()) != GRS_OK) return r;
   // P2's plan (the bucket table: P1's regions, or the redo's exact layout), then H2: byte-2
   // histogram per top-byte bucket over alt; zeroes P2's status
@@ -1025,49 +1045,54 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
       hipLaunchKernelGGL((grs::grs_msd_plan2<Big::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
                          totals, exact, tab, rec2, hdr2);
     GRS_HIP(hipGetLastError());
-    hipLaunchKernelGGL(grs::grs_msd_hist2, dim3(n / GRS_H2_CHUNK + 257), dim3(1024), 0, stream, alt, h2,
-                       st1, static_cast<uint32_t>(words2), tab);
+    hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / GRS_H2_CHUNK + 257), dim3(1024), 0, stream, alt,
+                       h2, st[1], static_cast<uint32_t>(words2), tab);
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
-  // P2: stable scatter by byte 2 inside each top-byte bucket, alt -> keys; each bucket's first
-  // tile writes where its 256 16-bit segments start (dstart)
+  // P2: stable scatter by the second byte inside each top-byte bucket, alt -> keys; each
+  // bucket's first tile writes where its 256 16-bit segments start (dstart)
   {
-    const Dig d2{16, 255u};
+    const Dig d2{KB - 16, 255u};
     const dim3 grid(static_cast<uint32_t>(t2));
     if (xl)
-      hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, XL::BLOCK, XL::ITEMS, XL::MINW, XL::OPT, false>),
-                         grid, dim3(XL::BLOCK), 0, stream, alt, keys, nullptr, nullptr, d2, rec2, hdr2, h2,
-                         256u, tickets + GRS_XCDS, st1, st0, err, dstart);
+      hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, XL::BLOCK, XL::ITEMS, XL::MINW, XL::OPT, false>),
+                         grid, dim3(XL::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2,
+                         256u, tickets + GRS_XCDS, st[1], st[0], err, dstart);
     else
-      hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, Big::BLOCK, Big::ITEMS, Big::MINW, Big::OPT, false>),
-                         grid, dim3(Big::BLOCK), 0, stream, alt, keys, nullptr, nullptr, d2, rec2, hdr2, h2,
-                         256u, tickets + GRS_XCDS, st1, st0, err, dstart);
+      hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, Big::BLOCK, Big::ITEMS, Big::MINW, Big::OPT, false>),
+                         grid, dim3(Big::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2,
+                         256u, tickets + GRS_XCDS, st[1], st[0], err, dstart);
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
-  // P3: every 16-bit segment sorted by its low 16 bits in LDS, in place; longer ones listed
-  hipLaunchKernelGGL((grs::grs_msd_local<P3C::BLOCK, P3C::I, P3C::C16, kMsdTileF>), dim3(65536),
-                     dim3(P3C::BLOCK), 0, stream, keys, h2, dstart, bigc, mb + L.bstart, mb + L.blen,
-                     mb + L.brow, mb + L.rows);
+  // P3: every 16-bit segment sorted by the bits below its prefix in LDS, in place; longer
+  // ones listed
+  hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
+                     dim3(P3C::BLOCK), 0, stream, keys, vals, h2, dstart, bigc, mb + L.bstart,
+                     mb + L.blen, mb + L.brow, rows);
   GRS_HIP(hipGetLastError());
   if ((r = mark()) != GRS_OK) return r;
-  // fallback: the listed segments by a segmented LSD on bits 0..15 (keys -> alt -> keys)
-  hipLaunchKernelGGL((grs::grs_seg_plan<kMsdTileF, grs::kSegList>), dim3(1), dim3(1024), 0, stream,
+  // fallback: the listed segments by a segmented LSD on the bits below the prefix
+  // (keys -> alt -> ... -> keys: ND is even)
+  static_assert(ND % 2 == 0, "the fallback ends in keys");
+  hipLaunchKernelGGL((grs::grs_seg_plan<FT::TILE, grs::kSegList>), dim3(1), dim3(1024), 0, stream,
                      mb + L.bstart, mb + L.blen, mb + L.brow, 0u, bigc, mb + L.spill, recf, hdrf);
   GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL((grs::grs_seg_hist<uint32_t, 2>), dim3(2 * s->cus), dim3(256), 0, stream, keys,
-                     recf, hdrf, 0, mb + L.rows, st0, 256u);
+  hipLaunchKernelGGL((grs::grs_seg_hist<K, ND>), dim3(2 * s->cus), dim3(256), 0, stream, keys, recf, hdrf,
+                     0, rows, st[0], 256u);
   GRS_HIP(hipGetLastError());
-  using FT = MsdFallTile;
-  hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
-                     dim3(s->cus), dim3(FT::BLOCK), 0, stream, keys, alt, nullptr, nullptr, Dig{0, 255u},
-                     recf, hdrf, mb + L.rows, 512u, tickets + 2 * GRS_XCDS, st0, st1, err, nullptr);
-  GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL((grs::grs_onesweep_seg<uint32_t, false, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
-                     dim3(s->cus), dim3(FT::BLOCK), 0, stream, alt, keys, nullptr, nullptr, Dig{8, 255u},
-                     recf, hdrf, mb + L.rows + 256, 512u, tickets + 3 * GRS_XCDS, st1, st0, err, nullptr);
-  GRS_HIP(hipGetLastError());
+  for (int p = 0; p < ND; ++p) {
+    K* const ik = (p & 1) ? alt : keys;
+    K* const ok = (p & 1) ? keys : alt;
+    uint32_t* const iv = (p & 1) ? valt : vals;
+    uint32_t* const ov = (p & 1) ? vals : valt;
+    hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
+                       dim3(s->cus), dim3(FT::BLOCK), 0, stream, ik, ok, iv, ov, Dig{8 * p, 255u}, recf, hdrf,
+                       rows + 256 * p, static_cast<uint32_t>(ND * 256), tickets + (2 + p) * GRS_XCDS,
+                       st[p & 1], st[(p + 1) & 1], err, nullptr);
+    GRS_HIP(hipGetLastError());
+  }
   if ((r = mark()) != GRS_OK) return r;
   if (evs) {
     s->info[s->calls % s->ring] = {ev, 6, false, 1};
@@ -1076,12 +1101,15 @@ grs_status run_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream
   return GRS_OK;
 }
 
-grs_status run_sort_msd(grs_sorter* s, uint32_t* keys, uint32_t n, hipStream_t stream,
-                        const uint32_t* src_in = nullptr) {
-  switch (msd_local_shape(n)) {
-    case 1: return run_msd<MsdLocalA>(s, keys, n, stream, src_in);
-    case 2: return run_msd<MsdLocalB>(s, keys, n, stream, src_in);
-    case 3: return run_msd<MsdLocalC>(s, keys, n, stream, src_in);
+template <typename K, bool PAIRS>
+grs_status run_sort_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
+                        const K* src_in = nullptr, const uint32_t* vsrc_in = nullptr) {
+  switch (msd_local_shape(n, sizeof(K) + (PAIRS ? 4 : 0))) {
+    case 1: return run_msd<K, PAIRS, MsdLocalA>(s, keys, vals, n, stream, src_in, vsrc_in);
+    case 2: return run_msd<K, PAIRS, MsdLocalB>(s, keys, vals, n, stream, src_in, vsrc_in);
+    case 3:
+      if constexpr (sizeof(K) == 4 && !PAIRS) return run_msd<K, PAIRS, MsdLocalC>(s, keys, vals, n, stream, src_in, vsrc_in);
+      [[fallthrough]];
     default: return set_err(GRS_EINVAL, "internal: no MSD shape for this n");
   }
 }
@@ -1261,9 +1289,14 @@ grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n
   const uint32_t n32 = static_cast<uint32_t>(n);
   grs_status r = GRS_EINVAL;
   const bool u64 = s->key_type == GRS_KEY_U64;
-  if (!u64 && !s->pairs && s->radix_bits == 8 && use_msd(s, n, begin_bit, end_bit))
-    r = run_sort_msd(s, (uint32_t*)d_keys, n32, st);
-  else if (!u64 && !s->pairs && s->radix_bits == 8)
+  if (use_msd(s, n, begin_bit, end_bit)) {
+    if (!u64 && !s->pairs)
+      r = run_sort_msd<uint32_t, false>(s, (uint32_t*)d_keys, nullptr, n32, st);
+    else if (!u64)
+      r = run_sort_msd<uint32_t, true>(s, (uint32_t*)d_keys, d_vals, n32, st);
+    else
+      r = run_sort_msd<uint64_t, false>(s, (uint64_t*)d_keys, nullptr, n32, st);
+  } else if (!u64 && !s->pairs && s->radix_bits == 8)
     r = run_sort<uint32_t, false, 8>(s, (uint32_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);
   else if (!u64 && !s->pairs && s->radix_bits == 4)
     r = run_sort<uint32_t, false, 4>(s, (uint32_t*)d_keys, nullptr, n32, begin_bit, end_bit, st);

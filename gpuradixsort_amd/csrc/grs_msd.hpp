@@ -213,7 +213,8 @@ __global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
 // n <= 64 * chunks), added into samp[256] (zero); also does the clearing the LSD sort's
 // histogram kernel does (P1's status, the next call's control block) plus clear2 (h2 and the
 // big-segment counters).
-__global__ __launch_bounds__(256) void grs_msd_sample(const uint32_t* __restrict__ keys, uint32_t n,
+template <typename K>
+__global__ __launch_bounds__(256) void grs_msd_sample(const K* __restrict__ keys, uint32_t n,
                                                       uint32_t* __restrict__ samp,
                                                       uint32_t* __restrict__ clear, uint32_t clear_words,
                                                       uint32_t* __restrict__ clear_ctrl,
@@ -228,23 +229,25 @@ __global__ __launch_bounds__(256) void grs_msd_sample(const uint32_t* __restrict
   for (uint32_t i = blockIdx.x * 256 + t; i < H + TK; i += gs) clear_ctrl[i] = 0;
   __syncthreads();
   constexpr uint32_t C = GRS_MSD_SAMPLE_CHUNKS;
+  constexpr int TOP = 8 * static_cast<int>(sizeof(K)) - 8;
   if (n <= C * GRS_WAVE) {
-    for (uint32_t i = blockIdx.x * 256 + t; i < n; i += gs) atomicAdd(&h[keys[i] >> 24], 1u);
+    for (uint32_t i = blockIdx.x * 256 + t; i < n; i += gs)
+      atomicAdd(&h[static_cast<uint32_t>(keys[i] >> TOP)], 1u);
   } else {
     // every wave's chunks loaded before any is counted (the loads overlap)
     constexpr uint32_t U = 4;
     const uint32_t waves = gridDim.x * 4;
     for (uint32_t c0 = blockIdx.x * 4 + (t >> 6); c0 < C; c0 += U * waves) {
-      uint32_t k[U];
+      K k[U];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         const uint32_t c = c0 + u * waves;
         const uint32_t pos = static_cast<uint32_t>(static_cast<uint64_t>(c) * (n - GRS_WAVE) / (C - 1));
-        k[u] = c < C ? keys[pos + lane] : 0u;
+        k[u] = c < C ? keys[pos + lane] : K(0);
       }
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u)
-        if (c0 + u * waves < C) atomicAdd(&h[k[u] >> 24], 1u);
+        if (c0 + u * waves < C) atomicAdd(&h[static_cast<uint32_t>(k[u] >> TOP)], 1u);
     }
   }
   __syncthreads();
@@ -304,7 +307,8 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
 // H2: h2[(top byte) * 256 + byte 2] over P1's output, one 256K-key chunk of one bucket per
 // block (grid >= n / chunk + 256; tab from grs_msd_plan2); zeroes `zero_words` of `zero` (P2's
 // status).  Two 1024-thread blocks per CU (8 waves per SIMD).
-__global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const uint32_t* __restrict__ keys,
+template <typename K>
+__global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ keys,
                                                          uint32_t* __restrict__ h2,
                                                          uint32_t* __restrict__ zero,
                                                          uint32_t zero_words,
@@ -329,34 +333,33 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const uint32_t* __restr
   const uint32_t c0 = tab[s] + j * GRS_H2_CHUNK;
   const uint32_t cl = min(static_cast<uint32_t>(GRS_H2_CHUNK), tab[257 + s] - j * GRS_H2_CHUNK);
   uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
-  auto count = [&](uint32_t k) { atomicAdd(base + ((k >> 16) & 255u) * GRS_H2_COPIES, 1u); };
-  const uint32_t* kc = keys + c0;
+  constexpr int SH = 8 * static_cast<int>(sizeof(K)) - 16;   // the second byte from the top
+  auto count = [&](K k) {
+    atomicAdd(base + (static_cast<uint32_t>(k >> SH) & 255u) * GRS_H2_COPIES, 1u);
+  };
+  constexpr uint32_t VEC = 16 / sizeof(K);
+  const K* kc = keys + c0;
   // 16-B loads from the first aligned key on
-  const uint32_t head = min(cl, static_cast<uint32_t>((4u - ((reinterpret_cast<uintptr_t>(kc) >> 2) & 3u)) & 3u));
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(kc) & 15u) / sizeof(K);
+  const uint32_t head = min(cl, (VEC - mis) % VEC);
   if (t < head) count(kc[t]);
-  const uint32_t nv = (cl - head) / 4;
+  const uint32_t nv = (cl - head) / VEC;
   const uint4* kv = reinterpret_cast<const uint4*>(kc + head);
+  auto count4 = [&](const uint4& x) {
+    const K* e = reinterpret_cast<const K*>(&x);
+#pragma unroll
+    for (uint32_t q = 0; q < VEC; ++q) count(e[q]);
+  };
   uint32_t i = t;
   for (; i + 3 * B < nv; i += 4 * B) {
     uint4 x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) x[u] = kv[i + u * B];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      count(x[u].x);
-      count(x[u].y);
-      count(x[u].z);
-      count(x[u].w);
-    }
+    for (int u = 0; u < 4; ++u) count4(x[u]);
   }
-  for (; i < nv; i += B) {
-    const uint4 x = kv[i];
-    count(x.x);
-    count(x.y);
-    count(x.z);
-    count(x.w);
-  }
-  for (uint32_t r = head + nv * 4 + t; r < cl; r += B) count(kc[r]);
+  for (; i < nv; i += B) count4(kv[i]);
+  for (uint32_t r = head + nv * VEC + t; r < cl; r += B) count(kc[r]);
   __syncthreads();
   if (t < 256) {
     const uint32_t* row = h + t * GRS_H2_COPIES;
@@ -367,14 +370,16 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const uint32_t* __restr
   }
 }
 
-// P3: one workgroup per 16-bit prefix b (grid 65536): its len = h2[b] keys at dstart[b] (P2's
-// digit starts) sorted by bits 0..15 in LDS, in place.  Segments longer than BLOCK * I keys go
-// to the big list for the segmented LSD: big[0] counts them, big[1] counts those longer than
-// one fallback tile (TILEF keys), which get a histogram row (two digits) zeroed here;
-// big_start / big_len / big_row hold (start, length, row) per entry.
-// C16: 16-bit wave counters (two per word), so that two 18K-key workgroups share a CU's LDS.
-template <int BLOCK, int I, bool C16, uint32_t TILEF>
-__global__ __launch_bounds__(BLOCK) void grs_msd_local(uint32_t* __restrict__ keys,
+// P3: one workgroup per 16-bit prefix b (grid 65536): its len = h2[b] keys (and payload) at
+// dstart[b] (P2's digit starts) sorted by the bits below the prefix in LDS, in place: 8-bit
+// rounds of lane-ordered returning LDS adds, as the pass ranks (2 rounds for u32 keys, 6 for
+// u64).  Segments longer than BLOCK * I keys go to the big list for the segmented LSD: big[0]
+// counts them, big[1] counts those longer than one fallback tile (TILEF keys), which get a
+// histogram row (ND digits) zeroed here; big_start / big_len / big_row hold (start, length,
+// row) per entry.  C16: 16-bit wave counters (two per word), so that two 18K-key workgroups
+// share a CU's LDS.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF>
+__global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ h2,
                                                        const uint32_t* __restrict__ dstart,
                                                        uint32_t* __restrict__ big,
@@ -383,9 +388,12 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(uint32_t* __restrict__ ke
                                                        uint32_t* __restrict__ big_row,
                                                        uint32_t* __restrict__ rows) {
   constexpr uint32_t W = BLOCK / GRS_WAVE, SMAX = BLOCK * I;
+  constexpr int ROUNDS = (8 * static_cast<int>(sizeof(K)) - 16) / 8;
+  constexpr uint32_t ND = ROUNDS;   // fallback digits (histogram row of ND x 256 words)
   static_assert(W <= 16 && BLOCK >= 256, "digit threads: waves 0..3");
   static_assert(!C16 || SMAX < 65536, "16-bit positions");
-  __shared__ uint32_t sk[SMAX];
+  __shared__ K sk[SMAX];
+  __shared__ uint32_t sv[PAIRS ? SMAX : 1];
   __shared__ uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
   __shared__ uint32_t wtot[4];
   __shared__ uint32_t slot;
@@ -409,25 +417,28 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(uint32_t* __restrict__ ke
     }
     __syncthreads();
     if (slot != 0xFFFFFFFFu)
-      for (uint32_t i = t; i < 2 * 256; i += BLOCK) rows[static_cast<size_t>(slot) * 512 + i] = 0;
+      for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(slot) * ND * 256 + i] = 0;
     return;
   }
-  uint32_t k[I];
+  K k[I];
+  uint32_t v[PAIRS ? I : 1];
 #pragma unroll
   for (uint32_t j = 0; j < I; ++j) {
     const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-    k[j] = i < len ? keys[lo + i] : 0u;
+    k[j] = i < len ? keys[lo + i] : K(0);
+    if constexpr (PAIRS) v[j] = i < len ? vals[lo + i] : 0u;
   }
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < ROUNDS; ++pass) {
     const int shift = 8 * pass;
+    auto digit = [&](K x) { return static_cast<uint32_t>(x >> shift) & 255u; };
     for (uint32_t c = t; c < W * 256 / (C16 ? 2 : 1); c += BLOCK) cnt[c] = 0;
     __syncthreads();
     uint32_t r[I];
 #pragma unroll
     for (uint32_t j = 0; j < I; ++j) {
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      const uint32_t d = (k[j] >> shift) & 255u;
+      const uint32_t d = digit(k[j]);
       if constexpr (C16) {
         const uint32_t sh = (d & 1u) << 4;
         r[j] = i < len ? (atomicAdd(&cnt[(w * 256 + d) >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
@@ -461,18 +472,28 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(uint32_t* __restrict__ ke
 #pragma unroll
     for (uint32_t j = 0; j < I; ++j) {
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      if (i < len) sk[cld(w * 256 + ((k[j] >> shift) & 255u)) + r[j]] = k[j];
+      if (i < len) {
+        const uint32_t dst = cld(w * 256 + digit(k[j])) + r[j];
+        sk[dst] = k[j];
+        if constexpr (PAIRS) sv[dst] = v[j];
+      }
     }
     __syncthreads();
-    if (pass == 0) {
+    if (pass + 1 < ROUNDS) {
 #pragma unroll
       for (uint32_t j = 0; j < I; ++j) {
         const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-        if (i < len) k[j] = sk[i];
+        if (i < len) {
+          k[j] = sk[i];
+          if constexpr (PAIRS) v[j] = sv[i];
+        }
       }
     }
   }
-  for (uint32_t i = t; i < len; i += BLOCK) keys[lo + i] = sk[i];
+  for (uint32_t i = t; i < len; i += BLOCK) {
+    keys[lo + i] = sk[i];
+    if constexpr (PAIRS) vals[lo + i] = sv[i];
+  }
 }
 
 }  // namespace grs

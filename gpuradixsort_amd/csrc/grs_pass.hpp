@@ -640,15 +640,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
 // to totals[0..RADIX) and sets totals[RADIX] when a run outgrew its region; it then also plans
 // the redo (the whole input as one segment of TILEF-key tiles, for grs_seg_hist and a persistent
 // grs_onesweep_seg) into redo_rec / redo_hdr, or writes an empty plan.
-template <typename K, int RB, int BLOCK, int ITEMS, int MINW, int OPT, uint32_t TILEF>
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT, uint32_t TILEF>
 __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
-    const K* __restrict__ keys_in, K* __restrict__ keys_out, uint32_t n, const RadixDigit<K> dig,
+    const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, uint32_t n, const RadixDigit<K> dig,
     const uint32_t* __restrict__ sample, unsigned long long mult, uint32_t pad,
     uint32_t region_len, uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
     uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word,
     uint32_t* __restrict__ totals, SegTile* __restrict__ redo_rec, uint32_t* __restrict__ redo_hdr) {
   constexpr int ROPT = OPT | 131072;
-  using SM = V4SmemFor<K, false, RB, BLOCK, ITEMS, ROPT, RadixDigit<K>>;
+  using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, ROPT, RadixDigit<K>>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
   uint32_t tt = t;
@@ -659,15 +660,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   __syncthreads();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
-  tile_load<K, false, BLOCK, ITEMS, ROPT>(key, val, keys_in, nullptr, n, tile, tt);
+  tile_load<K, PAIRS, BLOCK, ITEMS, ROPT>(key, val, keys_in, vals_in, n, tile, tt);
   const uint32_t gh =
       t < static_cast<uint32_t>(SM::RADIX)
           ? static_cast<uint32_t>((static_cast<unsigned long long>(sample[t]) * mult) >> 20) + pad
           : 0u;
   TileSpan sp = TileSpan::whole(tile, n, SM::TILE);
   sp.seg_len = region_len;
-  onesweep_tile<K, false, RB, BLOCK, ITEMS, ROPT>(sm, sp, key, val, keys_in, keys_out, nullptr,
-                                                  nullptr, n, dig, gh, ticket, status, status_next,
+  onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, ROPT>(sm, sp, key, val, keys_in, keys_out, vals_in,
+                                                  vals_out, n, dig, gh, ticket, status, status_next,
                                                   error_word, PassDebug::read(error_word), nullptr,
                                                   totals);
   if (tile + 1u == sp.tiles) {   // the redo's plan (its digit threads wrote the spill flag)

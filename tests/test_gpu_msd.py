@@ -1,4 +1,4 @@
-"""GPU tests of the MSD-first u32 sort (grs_msd.hpp; GRS_OPT_MSD).
+"""GPU tests of the MSD-first sort (grs_msd.hpp; GRS_OPT_MSD): u32 keys, u32 pairs, u64 keys.
 
 The MSD sort is a different schedule of the same stable sort: two stable scatters by the top
 two bytes, then each 16-bit segment sorted by its low 16 bits in LDS, and a segmented LSD for
@@ -19,16 +19,17 @@ pytestmark = pytest.mark.gpu
 _S = {}
 
 
-def msd_sorter(capacity, mode="always"):
+def msd_sorter(capacity, mode="always", key_bits=32, pairs=False):
     import gpuradixsort_amd as grs
 
-    s = _S.get(mode)
+    key = (mode, key_bits, pairs)
+    s = _S.get(key)
     if s is None or s.capacity < capacity:
         if s is not None:
             s.close()
-        s = grs.RadixSorter(max(capacity, 1 << 20), key_bits=32, pairs=False, radix_bits=8)
+        s = grs.RadixSorter(max(capacity, 1 << 20), key_bits=key_bits, pairs=pairs, radix_bits=8)
         s.set_option("msd", mode)
-        _S[mode] = s
+        _S[key] = s
     return s
 
 
@@ -142,3 +143,73 @@ def test_msd_region_spill_redo(gpu):
     # and the sorter keeps working (the spill flag lives in the per-call control block)
     keys2 = rng.integers(0, 1 << 32, n, dtype=np.uint32)
     assert np.array_equal(run(keys2, gpu), np.sort(keys2))
+
+
+def run_typed(keys: np.ndarray, dev, pairs: bool, mode="always"):
+    kb = keys.dtype.itemsize * 8
+    s = msd_sorter(keys.size, mode, kb, pairs)
+    k = torch.from_numpy(np.ascontiguousarray(keys)).to(dev)
+    v = torch.arange(keys.size, dtype=torch.int64, device=dev).to(torch.int32).view(torch.uint32) if pairs else None
+    s.sort(k, v)
+    torch.cuda.synchronize()
+    s.check_error()
+    return k.cpu().numpy(), (v.cpu().numpy() if pairs else None)
+
+
+@pytest.mark.parametrize("n", [1, 2, 64, 4097, 5121, 65537, 300007, 1 << 20])
+def test_msd_pairs_match_reference_path(gpu, n):
+    """u32 keys + u32 payload (the reference's IntermediateData {key, index}): keys AND the
+    stable permutation == the restated reference path (ParallelSort.cpp:236-298)."""
+    rng = np.random.default_rng(6000 + n)
+    for name, keys in dists(n, rng):
+        if n > 65537 and name not in ("uniform", "perm", "16_unique", "mixed_max"):
+            continue
+        rk, rp = oracle.ref_parallel_sort(keys)
+        gk, gv = run_typed(keys, gpu, True)
+        assert np.array_equal(gk, rk), f"{name} n={n}: keys"
+        assert np.array_equal(gv, rp), f"{name} n={n}: permutation (stability)"
+
+
+@pytest.mark.parametrize("n", [1, 3, 64, 4097, 5121, 65537, 300007, 1 << 20])
+def test_msd_u64_matches_stable_sort(gpu, n):
+    """u64 keys (6 LDS rounds below the 16-bit prefix; 6-pass segmented fallback)."""
+    rng = np.random.default_rng(7000 + n)
+    top = np.iinfo(np.uint64).max
+    cases = [("uniform", rng.integers(0, top, n, dtype=np.uint64, endpoint=True)),
+             ("all_equal", np.full(n, 9, np.uint64)),
+             ("16_unique", rng.integers(0, 16, n).astype(np.uint64) * np.uint64(0x1000000000000001)),
+             ("narrow_40bit", rng.integers(0, 1 << 40, n, dtype=np.uint64)),
+             ("mixed_max", np.where(rng.random(n) < 0.3, top, rng.integers(0, 100, n)).astype(np.uint64))]
+    for name, keys in cases:
+        gk, _ = run_typed(keys, gpu, False)
+        assert np.array_equal(gk, np.sort(keys)), f"{name} n={n}"
+
+
+@pytest.mark.parametrize("kb,pairs", [(32, True), (64, False)])
+def test_msd_typed_segment_edges_and_spill(gpu, kb, pairs):
+    """The fallback (solo and multi-tile segments) and the region redo for u32 pairs and u64."""
+    rng = np.random.default_rng(kb + pairs)
+    dt = np.uint32 if kb == 32 else np.uint64
+    sizes = [5120, 5121, 17408, 17409, 40000, 3]
+    parts = []
+    for i, c in enumerate(sizes):
+        prefix = dt((i * 2654435761) & 0xFFFF) << dt(kb - 16)
+        parts.append(prefix | rng.integers(0, 1 << 16, c).astype(dt))
+    keys = np.concatenate(parts)
+    rng.shuffle(keys)
+    gk, gv = run_typed(keys, gpu, pairs)
+    perm = oracle.stable_argsort(keys)
+    assert np.array_equal(gk, keys[perm])
+    if pairs:
+        assert np.array_equal(gv, perm.astype(np.uint32))
+    # region spill: sampled chunks in bucket 0, the rest in bucket 255
+    n, chunks, w = 1 << 22, 16384, 64
+    keys = (dt(0xFF) << dt(kb - 8)) | rng.integers(0, 1 << 24, n).astype(dt)
+    pos = (np.arange(chunks, dtype=np.uint64) * np.uint64(n - w) // np.uint64(chunks - 1)).astype(np.int64)
+    idx = (pos[:, None] + np.arange(w)[None, :]).ravel()
+    keys[idx] = rng.integers(0, 1 << 24, idx.size).astype(dt)
+    gk, gv = run_typed(keys, gpu, pairs)
+    perm = oracle.stable_argsort(keys)
+    assert np.array_equal(gk, keys[perm])
+    if pairs:
+        assert np.array_equal(gv, perm.astype(np.uint32))
