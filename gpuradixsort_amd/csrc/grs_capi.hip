@@ -396,10 +396,12 @@ template <int B, int I_, bool C> struct MsdLocal {
   static constexpr bool C16 = C;
   static constexpr uint32_t SMAX = B * I_;
 };
+using MsdLocalS = MsdLocal<256, 8, false>;    // small sorts: the unrolled item loop costs what
+using MsdLocalM = MsdLocal<256, 12, false>;   // the shape holds, not what the segment holds
 using MsdLocalA = MsdLocal<256, 20, false>;   // any element (40 KB of LDS at 8 B)
 using MsdLocalB = MsdLocal<512, 20, false>;
 using MsdLocalC = MsdLocal<768, 24, true>;    // 4-byte elements: two 72-KB workgroups per CU
-constexpr uint32_t kMsdSmaxMin = MsdLocalA::SMAX;
+constexpr uint32_t kMsdSmaxMin = MsdLocalS::SMAX;
 // fallback and redo passes (persistent): the big tile of the key type; 17408 keys is the
 // smallest of them (u32 pairs, u64 keys), which sizes the tables
 constexpr uint32_t kMsdTileMin = 17408;
@@ -407,7 +409,7 @@ static_assert(BigTile<uint32_t, true>::TILE == kMsdTileMin && BigTile<uint64_t, 
               BigTile<uint32_t, false>::TILE > kMsdTileMin, "MSD table sizing");
 
 struct MsdLayout {   // word offsets into msd_buf
-  size_t h2, big, dstart, tab, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
+  size_t h2, big, mid, dstart, tab, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
   size_t r2, rf, bl, mr;   // capacities: P2 records, fallback records, big list, histogram rows
   // nd: digits of the fallback (2 for u32 keys, 6 for u64)
   static MsdLayout of(size_t cap, size_t nd) {
@@ -419,8 +421,10 @@ struct MsdLayout {   // word offsets into msd_buf
     L.rf = cap / kMsdTileMin + L.bl + 1;
     size_t o = 0;
     auto take = [&](size_t w) { const size_t at = o; o += (w + 63) & ~static_cast<size_t>(63); return at; };
-    L.h2 = take(65536 + 64);   // h2 | big counters: zeroed together by the sample kernel
+    // h2 | big counters | mid list (its count zeroed with h2 by the sample kernel)
+    L.h2 = take(65536 + 64 + 2 + 2 * 65536);
     L.big = L.h2 + 65536;
+    L.mid = L.h2 + 65536 + 64;
     L.dstart = take(65536);
     L.tab = take(4 * 257);
     L.hdr2 = take(4);
@@ -913,13 +917,15 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
 int msd_local_shape(size_t n, size_t elem) {
   const double m = static_cast<double>(n) / 65536.0;
   const double need = m + 8.0 * std::sqrt(m) + 64.0;
+  if (need <= MsdLocalS::SMAX) return 4;
+  if (need <= MsdLocalM::SMAX) return 5;
   if (need <= MsdLocalA::SMAX) return 1;
   if (need <= MsdLocalB::SMAX) return 2;
   if (elem == 4 && need <= MsdLocalC::SMAX) return 3;
   return 0;
 }
 // From this many keys the MSD sort is the default (GRS_OPT_MSD = -1).
-constexpr size_t kMsdMinN = size_t(1) << 26;
+constexpr size_t kMsdMinN = size_t(3) << 24;   // MSD vs LSD, same box (r5 s12-13): 2^25 84 vs 88, 2^26 106 vs 96 Gkeys/s
 
 bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
   if (!msd_type(s) || s->msd_mode == 0 || s->msd_buf == nullptr || s->rank_mode != 0) return false;
@@ -1002,7 +1008,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // sample: the top byte's histogram; zeroes P1's status, the next call's control block, h2
   // and the big-segment counters
   hipLaunchKernelGGL((grs::grs_msd_sample<K>), dim3(1024), dim3(256), 0, stream, src, n, samp, st[0],
-                     static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u);
+                     static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u + 2u);
   GRS_HIP(hipGetLastError());
   s->cb_i ^= 1;
   if ((r = mark()) != GRS_OK) return r;
@@ -1067,11 +1073,22 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   }
   if ((r = mark()) != GRS_OK) return r;
   // P3: every 16-bit segment sorted by the bits below its prefix in LDS, in place; longer
-  // ones listed
+  // ones listed: up to the largest LDS shape's capacity for its persistent kernel (inputs
+  // narrower than the key, e.g. a rank's range after the multi-GPU exchange), beyond that for
+  // the fallback
+  using P3L = std::conditional_t<sizeof(K) == 4 && !PAIRS, MsdLocalC, MsdLocalB>;
+  const uint32_t mid_max = P3L::SMAX > P3C::SMAX ? P3L::SMAX : P3C::SMAX;
   hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
-                     dim3(P3C::BLOCK), 0, stream, keys, vals, h2, dstart, bigc, mb + L.bstart,
-                     mb + L.blen, mb + L.brow, rows);
+                     dim3(P3C::BLOCK), 0, stream, keys, vals, h2, dstart, mid_max, mb + L.mid, bigc,
+                     mb + L.bstart, mb + L.blen, mb + L.brow, rows);
   GRS_HIP(hipGetLastError());
+  if (P3L::SMAX > P3C::SMAX) {
+    constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
+    constexpr int minw = per_cu * P3L::BLOCK / GRS_WAVE / 4;
+    hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw>),
+                       dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, mb + L.mid);
+    GRS_HIP(hipGetLastError());
+  }
   if ((r = mark()) != GRS_OK) return r;
   // fallback: the listed segments by a segmented LSD on the bits below the prefix
   // (keys -> alt -> ... -> keys: ND is even)
@@ -1105,6 +1122,8 @@ template <typename K, bool PAIRS>
 grs_status run_sort_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
                         const K* src_in = nullptr, const uint32_t* vsrc_in = nullptr) {
   switch (msd_local_shape(n, sizeof(K) + (PAIRS ? 4 : 0))) {
+    case 4: return run_msd<K, PAIRS, MsdLocalS>(s, keys, vals, n, stream, src_in, vsrc_in);
+    case 5: return run_msd<K, PAIRS, MsdLocalM>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 1: return run_msd<K, PAIRS, MsdLocalA>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 2: return run_msd<K, PAIRS, MsdLocalB>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 3:
@@ -2325,8 +2344,11 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
 
   if ((r = xmark(s, 0, st)) != GRS_OK) return r;
   // 1. local sort, out of place: the sorted shard lands in out_k
-  if (n > 0 && (r = run_sort<uint32_t, false, 8>(s, out_k, nullptr, n, 0, 32, st, keys)) != GRS_OK)
-    return r;
+  if (n > 0) {
+    r = use_msd(s, n, 0, 32) ? run_sort_msd<uint32_t, false>(s, out_k, nullptr, n, st, keys)
+                             : run_sort<uint32_t, false, 8>(s, out_k, nullptr, n, 0, 32, st, keys);
+    if (r != GRS_OK) return r;
+  }
   // 2-3. samples of the sorted shard (rank-major gather), splitters on the device
   hipLaunchKernelGGL((grs::grs_shard_samples<uint32_t>), dim3((S + 255) / 256), dim3(256), 0, st,
                      out_k, n, S, sk, sp);

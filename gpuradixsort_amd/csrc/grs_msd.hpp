@@ -370,129 +370,169 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   }
 }
 
+// One workgroup sorts one segment [lo, lo + len) (len <= BLOCK * I) by the bits below its
+// 16-bit prefix in LDS, in place: 8-bit rounds of lane-ordered returning LDS adds, as the pass
+// ranks (2 rounds for u32 keys, 6 for u64).  C16: 16-bit wave counters (two per word), so that
+// two 18K-key workgroups share a CU's LDS.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16>
+struct LocalSort {
+  static constexpr uint32_t W = BLOCK / GRS_WAVE, SMAX = BLOCK * I;
+  static constexpr int ROUNDS = (8 * static_cast<int>(sizeof(K)) - 16) / 8;
+  static_assert(W <= 16 && BLOCK >= 256, "digit threads: waves 0..3");
+  static_assert(!C16 || SMAX < 65536, "16-bit positions");
+  struct Smem {
+    K sk[SMAX];
+    uint32_t sv[PAIRS ? SMAX : 1];
+    uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
+    uint32_t wtot[4];
+    uint32_t slot;
+  };
+  __device__ __forceinline__ static void run(Smem& sm, K* __restrict__ keys, uint32_t* __restrict__ vals,
+                             uint32_t lo, uint32_t len) {
+    uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
+    auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return sm.cnt[a]; };
+    auto cst = [&](uint32_t a, uint32_t v) {
+      if constexpr (C16) c16[a] = static_cast<uint16_t>(v); else sm.cnt[a] = v;
+    };
+    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+    K k[I];
+    uint32_t v[PAIRS ? I : 1];
+#pragma unroll
+    for (uint32_t j = 0; j < I; ++j) {
+      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+      k[j] = i < len ? keys[lo + i] : K(0);
+      if constexpr (PAIRS) v[j] = i < len ? vals[lo + i] : 0u;
+    }
+#pragma unroll
+    for (int pass = 0; pass < ROUNDS; ++pass) {
+      const int shift = 8 * pass;
+      auto digit = [&](K x) { return static_cast<uint32_t>(x >> shift) & 255u; };
+      for (uint32_t c = t; c < W * 256 / (C16 ? 2 : 1); c += BLOCK) sm.cnt[c] = 0;
+      __syncthreads();
+      uint32_t r[I];
+#pragma unroll
+      for (uint32_t j = 0; j < I; ++j) {
+        const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+        const uint32_t d = digit(k[j]);
+        if constexpr (C16) {
+          const uint32_t sh = (d & 1u) << 4;
+          r[j] = i < len ? (atomicAdd(&sm.cnt[(w * 256 + d) >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
+        } else {
+          r[j] = i < len ? atomicAdd(&sm.cnt[w * 256 + d], 1u) : 0u;
+        }
+      }
+      __syncthreads();
+      uint32_t c[W], tot = 0, incl = 0;
+      if (t < 256) {
+#pragma unroll
+        for (uint32_t ww = 0; ww < W; ++ww) {
+          c[ww] = cld(ww * 256 + t);
+          tot += c[ww];
+        }
+        incl = wave_scan_dpp(tot);
+        if (lane == GRS_WAVE - 1) sm.wtot[w] = incl;
+      }
+      __syncthreads();
+      if (t < 256) {
+        uint32_t b = incl - tot;
+#pragma unroll
+        for (uint32_t ww = 0; ww < 4; ++ww) b += ww < w ? sm.wtot[ww] : 0u;
+#pragma unroll
+        for (uint32_t ww = 0; ww < W; ++ww) {
+          cst(ww * 256 + t, b);
+          b += c[ww];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < I; ++j) {
+        const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+        if (i < len) {
+          const uint32_t dst = cld(w * 256 + digit(k[j])) + r[j];
+          sm.sk[dst] = k[j];
+          if constexpr (PAIRS) sm.sv[dst] = v[j];
+        }
+      }
+      __syncthreads();
+      if (pass + 1 < ROUNDS) {
+#pragma unroll
+        for (uint32_t j = 0; j < I; ++j) {
+          const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+          if (i < len) {
+            k[j] = sm.sk[i];
+            if constexpr (PAIRS) v[j] = sm.sv[i];
+          }
+        }
+      }
+    }
+    for (uint32_t i = t; i < len; i += BLOCK) {
+      keys[lo + i] = sm.sk[i];
+      if constexpr (PAIRS) vals[lo + i] = sm.sv[i];
+    }
+  }
+};
+
 // P3: one workgroup per 16-bit prefix b (grid 65536): its len = h2[b] keys (and payload) at
-// dstart[b] (P2's digit starts) sorted by the bits below the prefix in LDS, in place: 8-bit
-// rounds of lane-ordered returning LDS adds, as the pass ranks (2 rounds for u32 keys, 6 for
-// u64).  Segments longer than BLOCK * I keys go to the big list for the segmented LSD: big[0]
-// counts them, big[1] counts those longer than one fallback tile (TILEF keys), which get a
-// histogram row (ND digits) zeroed here; big_start / big_len / big_row hold (start, length,
-// row) per entry.  C16: 16-bit wave counters (two per word), so that two 18K-key workgroups
-// share a CU's LDS.
+// dstart[b] (P2's digit starts) sorted in LDS (LocalSort).  Longer segments are listed: up to
+// MID keys in the mid list (mid[0] = count, mid_start / mid_len) for grs_msd_local_list's
+// larger shape, longer ones in the big list for the segmented LSD: big[0] counts them, big[1]
+// counts those longer than one fallback tile (TILEF keys), which get a histogram row (ND
+// digits) zeroed here; big_start / big_len / big_row hold (start, length, row) per entry.
 template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF>
 __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ h2,
                                                        const uint32_t* __restrict__ dstart,
+                                                       uint32_t mid_max, uint32_t* __restrict__ mid,
                                                        uint32_t* __restrict__ big,
                                                        uint32_t* __restrict__ big_start,
                                                        uint32_t* __restrict__ big_len,
                                                        uint32_t* __restrict__ big_row,
                                                        uint32_t* __restrict__ rows) {
-  constexpr uint32_t W = BLOCK / GRS_WAVE, SMAX = BLOCK * I;
-  constexpr int ROUNDS = (8 * static_cast<int>(sizeof(K)) - 16) / 8;
-  constexpr uint32_t ND = ROUNDS;   // fallback digits (histogram row of ND x 256 words)
-  static_assert(W <= 16 && BLOCK >= 256, "digit threads: waves 0..3");
-  static_assert(!C16 || SMAX < 65536, "16-bit positions");
-  __shared__ K sk[SMAX];
-  __shared__ uint32_t sv[PAIRS ? SMAX : 1];
-  __shared__ uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
-  __shared__ uint32_t wtot[4];
-  __shared__ uint32_t slot;
-  uint16_t* const c16 = reinterpret_cast<uint16_t*>(cnt);
-  auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return cnt[a]; };
-  auto cst = [&](uint32_t a, uint32_t v) {
-    if constexpr (C16) c16[a] = static_cast<uint16_t>(v); else cnt[a] = v;
-  };
-  const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+  using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
+  constexpr uint32_t ND = LS::ROUNDS;   // fallback digits (histogram row of ND x 256 words)
+  __shared__ typename LS::Smem sm;
+  const uint32_t t = threadIdx.x;
   const uint32_t len = h2[blockIdx.x];
   if (len <= 1) return;   // (the start of an empty segment was never written)
   const uint32_t lo = dstart[blockIdx.x];
-  if (len > SMAX) {
+  if (len > LS::SMAX) {
+    if (len <= mid_max) {   // the mid list (a larger LDS shape)
+      if (t == 0) {
+        const uint32_t e = atomicAdd(&mid[0], 1u);
+        mid[2 + 2 * e] = lo;
+        mid[3 + 2 * e] = len;
+      }
+      return;
+    }
     if (t == 0) {
       const uint32_t e = atomicAdd(&big[0], 1u);
       const uint32_t row = len > TILEF ? atomicAdd(&big[1], 1u) : 0xFFFFFFFFu;
       big_start[e] = lo;
       big_len[e] = len;
       big_row[e] = row;
-      slot = row;
+      sm.slot = row;
     }
     __syncthreads();
-    if (slot != 0xFFFFFFFFu)
-      for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(slot) * ND * 256 + i] = 0;
+    if (sm.slot != 0xFFFFFFFFu)
+      for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(sm.slot) * ND * 256 + i] = 0;
     return;
   }
-  K k[I];
-  uint32_t v[PAIRS ? I : 1];
-#pragma unroll
-  for (uint32_t j = 0; j < I; ++j) {
-    const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-    k[j] = i < len ? keys[lo + i] : K(0);
-    if constexpr (PAIRS) v[j] = i < len ? vals[lo + i] : 0u;
-  }
-#pragma unroll
-  for (int pass = 0; pass < ROUNDS; ++pass) {
-    const int shift = 8 * pass;
-    auto digit = [&](K x) { return static_cast<uint32_t>(x >> shift) & 255u; };
-    for (uint32_t c = t; c < W * 256 / (C16 ? 2 : 1); c += BLOCK) cnt[c] = 0;
-    __syncthreads();
-    uint32_t r[I];
-#pragma unroll
-    for (uint32_t j = 0; j < I; ++j) {
-      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      const uint32_t d = digit(k[j]);
-      if constexpr (C16) {
-        const uint32_t sh = (d & 1u) << 4;
-        r[j] = i < len ? (atomicAdd(&cnt[(w * 256 + d) >> 1], 1u << sh) >> sh) & 0xFFFFu : 0u;
-      } else {
-        r[j] = i < len ? atomicAdd(&cnt[w * 256 + d], 1u) : 0u;
-      }
-    }
-    __syncthreads();
-    uint32_t c[W], tot = 0, incl = 0;
-    if (t < 256) {
-#pragma unroll
-      for (uint32_t ww = 0; ww < W; ++ww) {
-        c[ww] = cld(ww * 256 + t);
-        tot += c[ww];
-      }
-      incl = wave_scan_dpp(tot);
-      if (lane == GRS_WAVE - 1) wtot[w] = incl;
-    }
-    __syncthreads();
-    if (t < 256) {
-      uint32_t b = incl - tot;
-#pragma unroll
-      for (uint32_t ww = 0; ww < 4; ++ww) b += ww < w ? wtot[ww] : 0u;
-#pragma unroll
-      for (uint32_t ww = 0; ww < W; ++ww) {
-        cst(ww * 256 + t, b);
-        b += c[ww];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < I; ++j) {
-      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      if (i < len) {
-        const uint32_t dst = cld(w * 256 + digit(k[j])) + r[j];
-        sk[dst] = k[j];
-        if constexpr (PAIRS) sv[dst] = v[j];
-      }
-    }
-    __syncthreads();
-    if (pass + 1 < ROUNDS) {
-#pragma unroll
-      for (uint32_t j = 0; j < I; ++j) {
-        const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-        if (i < len) {
-          k[j] = sk[i];
-          if constexpr (PAIRS) v[j] = sv[i];
-        }
-      }
-    }
-  }
-  for (uint32_t i = t; i < len; i += BLOCK) {
-    keys[lo + i] = sk[i];
-    if constexpr (PAIRS) vals[lo + i] = sv[i];
+  LS::run(sm, keys, vals, lo, len);
+}
+
+// P3's second shape: the mid list's segments (persistent grid, a segment per workgroup in
+// turn; leaves at once when the list is empty).  MINW: waves per SIMD to keep the registers
+// of two workgroups per CU where their LDS fits.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict__ keys,
+                                                            uint32_t* __restrict__ vals,
+                                                            const uint32_t* __restrict__ mid) {
+  using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
+  __shared__ typename LS::Smem sm;
+  const uint32_t count = mid[0];
+  for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
+    LS::run(sm, keys, vals, mid[2 + 2 * e], mid[3 + 2 * e]);
+    __syncthreads();   // every LDS read of this segment before the next one's
   }
 }
 

@@ -91,6 +91,7 @@ def _segment_keys(rng, sizes):
     [5121] * 7 + [100],                        # solo fallback segments
     [36864, 36865, 73729, 200000, 3],          # one-tile, two-tile and multi-tile fallbacks
     [1 << 20],                                 # one segment of everything
+    [6000, 10000, 18432, 18433, 100],          # the mid list (the larger LDS shape) and past it
 ])
 def test_msd_segment_edges(gpu, sizes):
     rng = np.random.default_rng(sum(sizes))
@@ -190,7 +191,7 @@ def test_msd_typed_segment_edges_and_spill(gpu, kb, pairs):
     """The fallback (solo and multi-tile segments) and the region redo for u32 pairs and u64."""
     rng = np.random.default_rng(kb + pairs)
     dt = np.uint32 if kb == 32 else np.uint64
-    sizes = [5120, 5121, 17408, 17409, 40000, 3]
+    sizes = [5120, 5121, 10240, 10241, 17408, 17409, 40000, 3]
     parts = []
     for i, c in enumerate(sizes):
         prefix = dt((i * 2654435761) & 0xFFFF) << dt(kb - 16)

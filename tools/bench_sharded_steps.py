@@ -6,7 +6,8 @@ python tools/bench_sharded_steps.py [--ranks 8] [--reps 10]
 Prints one JSON line per step:
   partition      grs_partition_ranges of one rank's shard into N buckets with tie-breaking
                  splitters (the splitters of rank 0, from the host twin over all ranks' samples)
-  local_sort     grs_sort of the received run (2^30 / N keys)
+  local_sort     grs_sort of the received run (2^30 / N keys), full-range keys and (the
+                 realistic case) keys of one of the N key ranges
   sharded_world1 grs_sort_sharded on a one-rank RCCL communicator (samples, device splitters,
                  partition into one bucket, count all-gather, the one host sync, the self copy,
                  local sort): its difference to local_sort is the fixed orchestration cost
@@ -93,6 +94,18 @@ def main():
     s.check_error()
     print(json.dumps({"step": "local_sort", "n": n, "ms": round(ms, 4),
                       "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
+    # what a rank really receives: the keys of one of G key ranges (uniform keys: the top
+    # log2(G) bits fixed), i.e. a narrower key for the local sort's MSD schedule
+    lg = max(0, G.bit_length() - 1)
+    for b in bufs:
+        grs.fill_splitmix(b, seed)
+        if lg:
+            b.view(torch.int32).bitwise_and_((1 << (32 - lg)) - 1)
+    it = iter(bufs)
+    ms = timed(lambda: s.sort(next(it)), a.reps)
+    s.check_error()
+    print(json.dumps({"step": "local_sort_one_range", "n": n, "key_range_bits": 32 - lg,
+                      "ms": round(ms, 4), "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
     del bufs
 
     with socket.socket() as so:

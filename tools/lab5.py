@@ -66,7 +66,7 @@ def main():
     print("   top-byte histogram", "OK" if torch.equal(hist[:256].to(torch.int64), ref) else "WRONG", flush=True)
 
     # P1's output: stable by top byte
-    p1 = keys[torch.sort(k64 >> 24, stable=True)[1]].contiguous()
+    p1 = keys.view(torch.int32)[torch.sort(k64 >> 24, stable=True)[1]].view(torch.uint32).contiguous()
     h2 = torch.zeros(65536, dtype=torch.uint32, device=dev)
     ref2 = torch.bincount(k64 >> 16, minlength=65536)
     for ch in (int(x) for x in a.h2chunk.split(",")):
@@ -79,7 +79,7 @@ def main():
 
     # P2's output: stable by the top 16 bits; segments = the 65536 prefixes
     p64 = k64 >> 16
-    p2 = keys[torch.sort(p64, stable=True)[1]].contiguous()
+    p2 = keys.view(torch.int32)[torch.sort(p64, stable=True)[1]].view(torch.uint32).contiguous()
     off = torch.zeros(65537, dtype=torch.int64, device=dev)
     off[1:] = torch.cumsum(ref2, 0)
     off32 = off.to(torch.int32).view(torch.uint32).contiguous()
