@@ -1685,6 +1685,203 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
   return r;
 }
 
+}  // extern "C"
+
+namespace {
+grs_status grow_buf(void** p, size_t* have, size_t need, const char* what);
+
+// Segments of any length (round 5): a segmented LSD over the segment table -- one planner
+// block (tiles never straddle a segment; a segment of one tile is solo), one histogram launch
+// (digit counts per segment of several tiles; solo tiles count themselves), then one
+// grs_onesweep_seg launch per 8-bit digit whose look-back chains restart at every segment.
+// No host synchronisation.  Scratch (seg_buf): header | tile records | histogram rows | two
+// status buffers | planner spill.
+template <typename K, bool PAIRS>
+grs_status sort_segmented_seg(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n,
+                              const uint32_t* d_offsets, uint32_t nseg, hipStream_t st) {
+  using T = BigTile<K, PAIRS>;
+  constexpr int ND = static_cast<int>(sizeof(K));   // 8-bit digits
+  constexpr uint32_t G = GRS_LB_GROUP;
+  const size_t tiles_max = n / T::TILE + nseg + 1;
+  const size_t multi_max = n / (T::TILE + 1) + 1;
+  const size_t rows_tiles = 2 * (n / T::TILE) + 2;   // tiles of the segments of several tiles
+  const size_t groups_max = rows_tiles / G + multi_max + 1;
+  const size_t sw = (rows_tiles + 2 * groups_max) * 256;
+  auto al = [](size_t w) { return (w + 63) & ~static_cast<size_t>(63); };
+  const size_t o_rec = 64, o_rows = o_rec + al(tiles_max * 8), o_st0 = o_rows + al(multi_max * ND * 256);
+  const size_t o_st1 = o_st0 + al(sw), o_spill = o_st1 + al(sw), words = o_spill + al(6 * (size_t(nseg) + 1));
+  grs_status r = grow_buf(&s->seg_buf, &s->seg_bytes, words * 4, "grs_sort_segmented");
+  if (r != GRS_OK) return r;
+  uint32_t* const b = static_cast<uint32_t*>(s->seg_buf);
+  uint32_t* const hdr = b;
+  auto* const rec = reinterpret_cast<grs::SegTile*>(b + o_rec);
+  uint32_t* const rows = b + o_rows;
+  uint32_t* const st0 = b + o_st0;
+  uint32_t* const st1 = b + o_st1;
+  uint32_t* const err = s->ctrl + GRS_CTRL_ERROR;
+  // per-pass tickets: the tail of the control block's ticket area (zeroed here: the sort
+  // calls' alternation does not cover this path)
+  uint32_t* const tickets = b + 16;
+  GRS_HIP(hipMemsetAsync(tickets, 0, 16 * 4, st));
+  GRS_HIP(hipMemsetAsync(rows, 0, multi_max * ND * 256 * 4, st));
+  hipLaunchKernelGGL((grs::grs_seg_plan<T::TILE, grs::kSegOffsets>), dim3(1), dim3(1024), 0, st, d_offsets,
+                     nullptr, nullptr, nseg, nullptr, b + o_spill, rec, hdr);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_seg_hist<K, ND>), dim3(8 * s->cus), dim3(256), 0, st, keys, rec, hdr, 0, rows,
+                     st0, 256u);
+  GRS_HIP(hipGetLastError());
+  K* const alt = static_cast<K*>(s->alt_keys);
+  uint32_t* const valt = PAIRS ? s->alt_vals : nullptr;
+  const dim3 grid(static_cast<uint32_t>(tiles_max));
+  for (int p = 0; p < ND; ++p) {
+    K* const ik = (p & 1) ? alt : keys;
+    K* const ok = (p & 1) ? keys : alt;
+    uint32_t* const iv = (p & 1) ? valt : vals;
+    uint32_t* const ov = (p & 1) ? vals : valt;
+    hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, false>), grid,
+                       dim3(T::BLOCK), 0, st, ik, ok, iv, ov, grs::RadixDigit<K>{8 * p, 255u}, rec, hdr,
+                       rows + 256 * p, static_cast<uint32_t>(ND * 256), tickets + p, (p & 1) ? st1 : st0,
+                       (p & 1) ? st0 : st1, err, nullptr);
+    GRS_HIP(hipGetLastError());
+  }
+  return GRS_OK;
+}
+
+// Segments of 16K keys and more on average, whose top-byte runs fit LDS (round 5): one stable
+// scatter by the top byte inside every segment (keys -> alt; grs_onesweep_seg over a
+// kSegOffsetsAll plan, each segment's first tile writing its 256 run starts), the runs as work
+// lists (grs_seg_runs), each run sorted by the bits below the top byte in LDS (alt -> keys:
+// grs_seg_local_list, a primary shape sized for the average run and the largest shape), and
+// runs longer than the largest shape by a segmented LSD on those bits over the big list
+// (kSegList plan, histograms, KB/8 - 1 persistent passes alt -> keys -> ... -> keys: an odd
+// count; leave at once when the list is empty).  Two HBM round trips per key where runs fit,
+// against KB/8 for the segmented LSD.  No host synchronisation.  Scratch (seg_buf): headers |
+// tickets and list counters | tile records | top-byte rows | run starts | lists | fallback rows
+// and records | two status buffers | planner spill.
+template <typename K, bool PAIRS, typename P, typename L>
+grs_status sort_segmented_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, const uint32_t* d_offsets,
+                              uint32_t nseg, hipStream_t st) {
+  using T = BigTile<K, PAIRS>;
+  constexpr int KB = 8 * static_cast<int>(sizeof(K));
+  constexpr int NDF = KB / 8 - 1;   // fallback digits (odd: alt -> ... -> keys)
+  constexpr uint32_t G = GRS_LB_GROUP, TF = T::TILE;
+  static_assert(NDF % 2 == 1, "the fallback ends in keys");
+  static_assert(L::SMAX >= P::SMAX, "shapes");
+  const size_t tiles_max = n / TF + nseg + 1;
+  const size_t ecap = std::min<size_t>(size_t(nseg) * 256, n) + 1;   // entries of a list
+  const size_t bcap = std::min<size_t>(size_t(nseg) * 256, n / (L::SMAX + 1) + 1);
+  const size_t mr = n / (TF + 1) + 1;                                // fallback histogram rows
+  const size_t rows_tiles = 2 * (n / TF) + 2;
+  const size_t groups_max = rows_tiles / G + std::max<size_t>(mr, n / (TF + 1) + 1) + 1;
+  const size_t sw = (rows_tiles + 2 * groups_max) * 256;
+  auto al = [](size_t w) { return (w + 63) & ~static_cast<size_t>(63); };
+  const size_t o_tk = 64, o_cnt = o_tk + 64;   // 64 ticket words, then 4 list counters
+  const size_t o_rec = 256, o_rows = o_rec + al(tiles_max * 8), o_ds = o_rows + al(size_t(nseg) * 256);
+  const size_t o_prim = o_ds + al(size_t(nseg) * 256), o_mid = o_prim + al(2 * ecap);
+  const size_t o_bst = o_mid + al(2 * ecap), o_bln = o_bst + al(bcap), o_brw = o_bln + al(bcap);
+  const size_t o_rowf = o_brw + al(bcap), o_recf = o_rowf + al(mr * NDF * 256);
+  const size_t o_st0 = o_recf + al((n / TF + bcap + 1) * 8), o_st1 = o_st0 + al(sw);
+  const size_t o_spill = o_st1 + al(sw), words = o_spill + al(6 * (std::max<size_t>(nseg, bcap) + 1));
+  grs_status r = grow_buf(&s->seg_buf, &s->seg_bytes, words * 4, "grs_sort_segmented");
+  if (r != GRS_OK) return r;
+  uint32_t* const b = static_cast<uint32_t*>(s->seg_buf);
+  uint32_t* const hdr = b;
+  uint32_t* const hdrf = b + 4;
+  uint32_t* const tickets = b + o_tk;
+  uint32_t* const cnt = b + o_cnt;
+  auto* const rec = reinterpret_cast<grs::SegTile*>(b + o_rec);
+  auto* const recf = reinterpret_cast<grs::SegTile*>(b + o_recf);
+  uint32_t* const rows = b + o_rows;
+  uint32_t* const ds = b + o_ds;
+  uint32_t* const stt[2] = {b + o_st0, b + o_st1};
+  uint32_t* const err = s->ctrl + GRS_CTRL_ERROR;
+  K* const alt = static_cast<K*>(s->alt_keys);
+  uint32_t* const valt = PAIRS ? s->alt_vals : nullptr;
+  using Dig = grs::RadixDigit<K>;
+  GRS_HIP(hipMemsetAsync(tickets, 0, (64 + 4) * 4, st));
+  GRS_HIP(hipMemsetAsync(rows, 0, size_t(nseg) * 256 * 4, st));
+  // the top-byte scatter inside every segment
+  hipLaunchKernelGGL((grs::grs_seg_plan<TF, grs::kSegOffsetsAll>), dim3(1), dim3(1024), 0, st, d_offsets,
+                     nullptr, nullptr, nseg, nullptr, b + o_spill, rec, hdr);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_seg_hist<K, 1>), dim3(8 * s->cus), dim3(256), 0, st, keys, rec, hdr, KB - 8, rows,
+                     stt[0], 256u);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, false>),
+                     dim3(static_cast<uint32_t>(tiles_max)), dim3(T::BLOCK), 0, st, keys, alt, vals, valt,
+                     Dig{KB - 8, 255u}, rec, hdr, rows, 256u, tickets, stt[0], stt[1], err, ds);
+  GRS_HIP(hipGetLastError());
+  // the runs as lists, then sorted in LDS, alt -> keys
+  hipLaunchKernelGGL((grs::grs_seg_runs<P::SMAX, L::SMAX, TF, NDF>), dim3(nseg), dim3(256), 0, st, d_offsets, ds,
+                     cnt, b + o_prim, b + o_mid, b + o_bst, b + o_bln, b + o_brw, b + o_rowf);
+  GRS_HIP(hipGetLastError());
+  auto local = [&](auto shape, const uint32_t* count, const uint32_t* list) {
+    using S = decltype(shape);
+    using LS = grs::LocalSort<K, PAIRS, S::BLOCK, S::I, S::C16, KB / 8>;
+    constexpr int per_cu = std::max<int>(1, std::min<int>(2048 / S::BLOCK, 160 * 1024 / static_cast<int>(sizeof(typename LS::Smem))));
+    constexpr int minw = std::max(1, per_cu * S::BLOCK / GRS_WAVE / 4);
+    hipLaunchKernelGGL((grs::grs_seg_local_list<K, PAIRS, S::BLOCK, S::I, S::C16, minw>), dim3(per_cu * s->cus),
+                       dim3(S::BLOCK), 0, st, alt, valt, keys, vals, count, list);
+  };
+  local(P{}, cnt, b + o_prim);
+  GRS_HIP(hipGetLastError());
+  if constexpr (L::SMAX > P::SMAX) {
+    local(L{}, cnt + 1, b + o_mid);
+    GRS_HIP(hipGetLastError());
+  }
+  // fallback: runs longer than the largest shape, a segmented LSD below the top byte
+  hipLaunchKernelGGL((grs::grs_seg_plan<TF, grs::kSegList>), dim3(1), dim3(1024), 0, st, b + o_bst, b + o_bln,
+                     b + o_brw, 0u, cnt + 2, b + o_spill, recf, hdrf);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_seg_hist<K, NDF>), dim3(2 * s->cus), dim3(256), 0, st, alt, recf, hdrf, 0,
+                     b + o_rowf, stt[0], 256u);
+  GRS_HIP(hipGetLastError());
+  for (int p = 0; p < NDF; ++p) {
+    K* const ik = (p & 1) ? keys : alt;
+    K* const ok = (p & 1) ? alt : keys;
+    uint32_t* const iv = (p & 1) ? vals : valt;
+    uint32_t* const ov = (p & 1) ? valt : vals;
+    hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, true>), dim3(s->cus),
+                       dim3(T::BLOCK), 0, st, ik, ok, iv, ov, Dig{8 * p, 255u}, recf, hdrf,
+                       b + o_rowf + 256 * p, static_cast<uint32_t>(NDF * 256), tickets + 8 * (1 + p),
+                       stt[p & 1], stt[(p + 1) & 1], err, nullptr);
+    GRS_HIP(hipGetLastError());
+  }
+  return GRS_OK;
+}
+
+// The largest LDS shape of the segmented top-byte sort, and the primary shape for segments of
+// n / nseg keys on average: a uniform run holds m = n / nseg / 256 keys, +- sqrt(m) (as
+// msd_local_shape); 0 when even the largest shape would leave most runs to the fallback.
+template <typename K, bool PAIRS>
+using SegMsdLargest = std::conditional_t<sizeof(K) + (PAIRS ? 4 : 0) <= 8, MsdLocalC, MsdLocalB>;
+template <typename K, bool PAIRS>
+int seg_msd_shape(size_t n, size_t nseg) {
+  const double m = static_cast<double>(n) / static_cast<double>(nseg) / 256.0;
+  const double need = m + 8.0 * std::sqrt(m) + 64.0;
+  // no smaller shape than A: short runs merge into entries of up to the shape's capacity
+  if (need <= MsdLocalA::SMAX) return 1;
+  if (need <= MsdLocalB::SMAX) return 2;
+  if (need <= SegMsdLargest<K, PAIRS>::SMAX) return 3;
+  return 0;
+}
+
+template <typename K, bool PAIRS>
+grs_status sort_segmented_msd_any(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, const uint32_t* d_offsets,
+                                  uint32_t nseg, hipStream_t st) {
+  using L = SegMsdLargest<K, PAIRS>;
+  switch (seg_msd_shape<K, PAIRS>(n, nseg)) {
+    case 1: return sort_segmented_msd<K, PAIRS, MsdLocalA, L>(s, keys, vals, n, d_offsets, nseg, st);
+    case 2: return sort_segmented_msd<K, PAIRS, MsdLocalB, L>(s, keys, vals, n, d_offsets, nseg, st);
+    case 3: return sort_segmented_msd<K, PAIRS, L, L>(s, keys, vals, n, d_offsets, nseg, st);
+    default: return set_err(GRS_EINVAL, "internal: no segmented LDS shape");
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
                               const uint32_t* d_offsets, int num_segments, void* stream) {
   if (!s) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL sorter");
@@ -1755,6 +1952,35 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
     }
     if (prev != s->device) (void)hipSetDevice(prev);
     if (r != GRS_OK || small) return r;
+  }
+  // atomic ranking, 8-bit digits: a few segments of 4M keys and more on average are sorted one
+  // by one (each a whole sort: MSD or LSD); segments of 4K keys and more on average whose top-byte
+  // runs fit LDS take the top-byte scatter + LDS sorts; anything else the segmented LSD
+  const size_t avg = n / static_cast<size_t>(num_segments);
+  if (s->rank_mode == 0 && s->radix_bits == 8 &&
+      !(num_segments <= GRS_MAX_SPLITTERS + 1 && avg >= (size_t(1) << 22))) {
+    int prev = 0;
+    GRS_HIP(hipGetDevice(&prev));
+    if (prev != s->device) GRS_HIP(hipSetDevice(s->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint32_t n32 = static_cast<uint32_t>(n), ns = static_cast<uint32_t>(num_segments);
+    const bool u32 = s->key_type == GRS_KEY_U32;
+    auto go = [&](auto kt, auto pairs) -> grs_status {
+      using KT = decltype(kt);
+      constexpr bool PR = decltype(pairs)::value;
+      KT* const k = static_cast<KT*>(d_keys);
+      uint32_t* const v = PR ? d_vals : nullptr;
+      if (s->msd_mode != 0 && avg >= 4096 && seg_msd_shape<KT, PR>(n, ns) != 0)
+        return sort_segmented_msd_any<KT, PR>(s, k, v, n32, d_offsets, ns, st);
+      return sort_segmented_seg<KT, PR>(s, k, v, n32, d_offsets, ns, st);
+    };
+    grs_status r;
+    if (u32 && d_vals) r = go(uint32_t{}, std::true_type{});
+    else if (u32) r = go(uint32_t{}, std::false_type{});
+    else if (d_vals) r = go(uint64_t{}, std::true_type{});
+    else r = go(uint64_t{}, std::false_type{});
+    if (prev != s->device) (void)hipSetDevice(prev);
+    return r;
   }
   if (num_segments <= GRS_MAX_SPLITTERS + 1)
     return sort_segmented_few(s, d_keys, d_vals, n, d_offsets, num_segments, stream);

@@ -36,12 +36,13 @@ namespace grs {
 // ---------------------------------------------------------------------------------------
 // Segment sources of a plan: sizes (starts are their exclusive scan: the buckets of a pass),
 // explicit (start, length) lists, or offsets (num + 1 words, segment i = [off[i], off[i+1])).
-enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2, kSegMoved = 3 };
+// kSegOffsetsAll: offsets, every segment's histogram row = its index (tables per segment).
+enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2, kSegMoved = 3, kSegOffsetsAll = 4 };
 
 // LDS of the planner: 6 words per segment (tile, row and group prefixes, start, length,
 // histogram row); larger tables keep them in global scratch (`spill`, 6 * (nseg + 1) words).
 #define GRS_PLAN_LDS_SEGS 2048
-#define GRS_PLAN_LDS_WORDS (6 * GRS_PLAN_LDS_SEGS + 4 * 16)
+#define GRS_PLAN_LDS_WORDS (6 * GRS_PLAN_LDS_SEGS + 5 * 16)
 
 // Block exclusive scan of NV values per thread over BLOCK threads (wsum: NV * waves words of
 // LDS); tot = the block totals.
@@ -76,8 +77,9 @@ __device__ __forceinline__ void block_scan(uint32_t (&v)[NV], uint32_t* wsum, ui
 // and starts new look-back groups, a segment of one tile is solo (no status words).
 // Sources: kSegSizes a = sizes (starts = their scan; histogram row = segment index);
 // kSegList a = starts, b = lengths, c = histogram rows; kSegOffsets a = offsets (histogram row =
-// segment index); kSegMoved a = where each segment's keys are read, b = lengths, c = where its
-// sorted runs go (histogram row = segment index).  hdr[0] = tiles, hdr[1] = groups, hdr[2] =
+// the segment's place among the segments of several tiles: solo segments need none);
+// kSegMoved a = where each segment's keys are read, b = lengths, c = where its sorted runs go
+// (histogram row = segment index).  hdr[0] = tiles, hdr[1] = groups, hdr[2] =
 // status rows.
 // lds: GRS_PLAN_LDS_WORDS words.
 template <uint32_t TILE, int BLOCK, int SRC>
@@ -96,7 +98,7 @@ __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* _
   uint32_t* const sln = sst + cap;
   uint32_t* const shr = sln + cap;   // histogram row; kSegMoved: the output start
   uint32_t* const wsum = lds + 6 * GRS_PLAN_LDS_SEGS;
-  uint32_t carry[4] = {0, 0, 0, 0};   // tiles, rows, groups, start (sizes source)
+  uint32_t carry[5] = {0, 0, 0, 0, 0};   // tiles, rows, groups, start (sizes), multi ordinal
   for (uint32_t c0 = 0; c0 < nseg; c0 += BLOCK) {
     const uint32_t i = c0 + t;
     uint32_t len = 0, st = 0, hr = i;
@@ -114,18 +116,18 @@ __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* _
     }
     const uint32_t tl = len / TILE + (len % TILE != 0u ? 1u : 0u);
     const uint32_t multi = tl > 1 ? tl : 0u;
-    uint32_t v[4] = {tl, multi, (multi + G - 1) / G, len}, tot[4];
-    block_scan<BLOCK, 4>(v, wsum, tot);
+    uint32_t v[5] = {tl, multi, (multi + G - 1) / G, len, multi ? 1u : 0u}, tot[5];
+    block_scan<BLOCK, 5>(v, wsum, tot);
     if (i < nseg) {
       tpre[i] = carry[0] + v[0];
       rpre[i] = carry[1] + v[1];
       gpre[i] = carry[2] + v[2];
       sst[i] = SRC == kSegSizes ? carry[3] + v[3] : st;
       sln[i] = len;
-      shr[i] = hr;
+      shr[i] = SRC == kSegOffsets ? carry[4] + v[4] : hr;   // kSegOffsetsAll: hr = i
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) carry[q] += tot[q];
+    for (int q = 0; q < 5; ++q) carry[q] += tot[q];
   }
   if (t == 0) tpre[nseg] = carry[0];
   __syncthreads();
@@ -189,11 +191,23 @@ __global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
     if ((r.flags >> 8) & 1u) continue;   // solo (uniform: one record per workgroup)
     for (uint32_t i = t; i < ND * 256; i += 256) h[i] = 0;
     __syncthreads();
-    for (uint32_t i = t; i < r.valid; i += 256) {
-      const K x = keys[r.base + i];
+    // U loads in flight per thread before any is counted (a tile is 17-36K keys: 8-18 each)
+    constexpr uint32_t U = 8;
+    for (uint32_t i0 = t; i0 < r.valid; i0 += 256 * U) {
+      K x[U];
 #pragma unroll
-      for (int p = 0; p < ND; ++p)
-        atomicAdd(&h[p * 256 + static_cast<uint32_t>((x >> (shift0 + 8 * p)) & 255u)], 1u);
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * 256;
+        x[u] = i < r.valid ? keys[r.base + i] : K(0);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        if (i0 + u * 256 < r.valid) {
+#pragma unroll
+          for (int p = 0; p < ND; ++p)
+            atomicAdd(&h[p * 256 + static_cast<uint32_t>((x[u] >> (shift0 + 8 * p)) & 255u)], 1u);
+        }
+      }
     }
     __syncthreads();
     for (uint32_t i = t; i < ND * 256; i += 256)
@@ -370,14 +384,15 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   }
 }
 
-// One workgroup sorts one segment [lo, lo + len) (len <= BLOCK * I) by the bits below its
-// 16-bit prefix in LDS, in place: 8-bit rounds of lane-ordered returning LDS adds, as the pass
-// ranks (2 rounds for u32 keys, 6 for u64).  C16: 16-bit wave counters (two per word), so that
-// two 18K-key workgroups share a CU's LDS.
-template <typename K, bool PAIRS, int BLOCK, int I, bool C16>
+// One workgroup sorts one segment [lo, lo + len) (len <= BLOCK * I) by its low 8 * rounds bits
+// in LDS (rounds <= RMAX; the MSD sort: the bits below the 16-bit prefix, 2 rounds for u32 keys,
+// 6 for u64), read from kin / vin and written to kout / vout (the same arrays: in place): 8-bit
+// rounds of lane-ordered returning LDS adds, as the pass ranks.  C16: 16-bit wave counters (two
+// per word), so that two 18K-key workgroups share a CU's LDS.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, int RMAX = (8 * static_cast<int>(sizeof(K)) - 16) / 8>
 struct LocalSort {
   static constexpr uint32_t W = BLOCK / GRS_WAVE, SMAX = BLOCK * I;
-  static constexpr int ROUNDS = (8 * static_cast<int>(sizeof(K)) - 16) / 8;
+  static constexpr int ROUNDS = RMAX;
   static_assert(W <= 16 && BLOCK >= 256, "digit threads: waves 0..3");
   static_assert(!C16 || SMAX < 65536, "16-bit positions");
   struct Smem {
@@ -388,7 +403,11 @@ struct LocalSort {
     uint32_t slot;
   };
   __device__ __forceinline__ static void run(Smem& sm, K* __restrict__ keys, uint32_t* __restrict__ vals,
-                             uint32_t lo, uint32_t len) {
+                                             uint32_t lo, uint32_t len) {
+    run(sm, keys, vals, keys, vals, lo, len, ROUNDS);
+  }
+  __device__ __forceinline__ static void run(Smem& sm, const K* kin, const uint32_t* vin, K* kout,
+                                             uint32_t* vout, uint32_t lo, uint32_t len, int rounds) {
     uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
     auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return sm.cnt[a]; };
     auto cst = [&](uint32_t a, uint32_t v) {
@@ -400,11 +419,12 @@ struct LocalSort {
 #pragma unroll
     for (uint32_t j = 0; j < I; ++j) {
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      k[j] = i < len ? keys[lo + i] : K(0);
-      if constexpr (PAIRS) v[j] = i < len ? vals[lo + i] : 0u;
+      k[j] = i < len ? kin[lo + i] : K(0);
+      if constexpr (PAIRS) v[j] = i < len ? vin[lo + i] : 0u;
     }
 #pragma unroll
     for (int pass = 0; pass < ROUNDS; ++pass) {
+      if (pass >= rounds) break;   // uniform
       const int shift = 8 * pass;
       auto digit = [&](K x) { return static_cast<uint32_t>(x >> shift) & 255u; };
       for (uint32_t c = t; c < W * 256 / (C16 ? 2 : 1); c += BLOCK) sm.cnt[c] = 0;
@@ -454,7 +474,7 @@ struct LocalSort {
         }
       }
       __syncthreads();
-      if (pass + 1 < ROUNDS) {
+      if (pass + 1 < rounds) {
 #pragma unroll
         for (uint32_t j = 0; j < I; ++j) {
           const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
@@ -466,8 +486,8 @@ struct LocalSort {
       }
     }
     for (uint32_t i = t; i < len; i += BLOCK) {
-      keys[lo + i] = sm.sk[i];
-      if constexpr (PAIRS) vals[lo + i] = sm.sv[i];
+      kout[lo + i] = sm.sk[i];
+      if constexpr (PAIRS) vout[lo + i] = sm.sv[i];
     }
   }
 };
@@ -533,6 +553,127 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict_
   for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
     LS::run(sm, keys, vals, mid[2 + 2 * e], mid[3 + 2 * e]);
     __syncthreads();   // every LDS read of this segment before the next one's
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// segmented sort of long segments (grs_sort_segmented): one stable scatter by the top byte
+// inside every segment (grs_onesweep_seg over a kSegOffsetsAll plan; each segment's first tile
+// writes its 256 run starts to ds[seg * 256 + d]), then every run sorted by the bits below the
+// top byte in LDS, from the second buffer back into the caller's arrays
+// ---------------------------------------------------------------------------------------
+// The runs of segment blockIdx.x as work lists.  Consecutive runs merge greedily into entries
+// of at most CP keys (sorted by the whole key: the runs keep their order); a longer run is an
+// entry of its own.  Entries of up to CP keys go to the primary list (prim), up to CL to the mid list, longer
+// ones to the big list (bstart / blen / brow) for a segmented LSD on the bits below the top
+// byte.  cnt (zeroed by the caller): [0] primary entries, [1] mid entries, [2] big entries,
+// [3] big entries longer than one fallback tile of TILEF keys, which get a histogram row of ND
+// digits (zeroed here).  prim / mid: (start, length | merged << 31) per entry.
+template <uint32_t CP, uint32_t CL, uint32_t TILEF, int ND>
+__global__ __launch_bounds__(256) void grs_seg_runs(const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ ds, uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ prim, uint32_t* __restrict__ mid,
+                                                    uint32_t* __restrict__ bstart,
+                                                    uint32_t* __restrict__ blen, uint32_t* __restrict__ brow,
+                                                    uint32_t* __restrict__ rows) {
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  __shared__ uint32_t es[257], eb[257], rl[256], wsum[3 * 4], base[3];
+  const uint32_t s = blockIdx.x, t = threadIdx.x;
+  const uint32_t lo = off[s], hi = off[s + 1];
+  if (hi <= lo) return;   // uniform: an empty segment (its run starts were never written)
+  const uint32_t st = ds[static_cast<size_t>(s) * 256 + t];
+  const uint32_t en = t < 255u ? ds[static_cast<size_t>(s) * 256 + t + 1] : hi;
+  rl[t] = en - st;
+  __syncthreads();
+  // greedy packing by wave 0 on the scalar unit (lane j of quarter q holds run 64 q + j): run d
+  // opens an entry when it is the first, longer than CP, or would overfill the open one; rl[d]
+  // becomes the flag
+  if (t < GRS_WAVE) {
+    uint32_t cur = CP + 1;
+    uint32_t q4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) q4[q] = rl[q * GRS_WAVE + t];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint64_t m = 0;
+#pragma unroll
+      for (int j = 0; j < GRS_WAVE; ++j) {
+        const uint32_t l = __builtin_amdgcn_readlane(q4[q], j);
+        const bool open = cur > CP || l > CP - cur;
+        cur = open ? l : cur + l;
+        if (l > CP) cur = CP + 1;
+        m |= static_cast<uint64_t>(open) << j;
+      }
+      rl[q * GRS_WAVE + t] = static_cast<uint32_t>(m >> t) & 1u;
+    }
+  }
+  __syncthreads();
+  uint32_t f[1] = {rl[t]}, ne[1];
+  const uint32_t is_first = f[0];
+  block_scan<256, 1>(f, wsum, ne);
+  const uint32_t E = ne[0];
+  if (is_first) {
+    es[f[0]] = st;
+    eb[f[0]] = t;
+  }
+  if (t == 0) {
+    es[E] = hi;
+    eb[E] = 256;
+  }
+  __syncthreads();
+  uint32_t s0 = 0, l = 0, nb = 0;
+  if (t < E) {
+    s0 = es[t];
+    l = es[t + 1] - s0;
+    nb = eb[t + 1] - eb[t];
+  }
+  uint32_t cls[3] = {l != 0u && l <= CP ? 1u : 0u, l > CP && l <= CL ? 1u : 0u, l > CL ? 1u : 0u}, tot[3];
+  const uint32_t k0 = cls[0], k1 = cls[1], k2 = cls[2];
+  block_scan<256, 3>(cls, wsum, tot);
+  if (t == 0) {
+    base[0] = tot[0] ? atomicAdd(&cnt[0], tot[0]) : 0u;
+    base[1] = tot[1] ? atomicAdd(&cnt[1], tot[1]) : 0u;
+    base[2] = tot[2] ? atomicAdd(&cnt[2], tot[2]) : 0u;
+  }
+  __syncthreads();
+  const uint32_t lw = l | (nb > 1u ? 0x80000000u : 0u);
+  if (k0) {
+    const uint32_t e = base[0] + cls[0];
+    prim[2 * e] = s0;
+    prim[2 * e + 1] = lw;
+  } else if (k1) {
+    const uint32_t e = base[1] + cls[1];
+    mid[2 * e] = s0;
+    mid[2 * e + 1] = lw;
+  } else if (k2) {
+    const uint32_t e = base[2] + cls[2];
+    const uint32_t row = l > TILEF ? atomicAdd(&cnt[3], 1u) : NONE;
+    bstart[e] = s0;
+    blen[e] = l;
+    brow[e] = row;
+    if (row != NONE)
+      for (uint32_t i = 0; i < ND * 256; ++i) rows[static_cast<size_t>(row) * ND * 256 + i] = 0;
+  }
+}
+
+// The *count entries of a list of grs_seg_runs sorted in LDS from kin / vin into kout / vout: a
+// run by the bits below the top byte, a merged entry by the whole key (persistent grid; leaves
+// at once when the list is empty).
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_seg_local_list(const K* __restrict__ kin,
+                                                                  const uint32_t* __restrict__ vin,
+                                                                  K* __restrict__ kout,
+                                                                  uint32_t* __restrict__ vout,
+                                                                  const uint32_t* __restrict__ count_p,
+                                                                  const uint32_t* __restrict__ list) {
+  constexpr int KR = static_cast<int>(sizeof(K));   // 8-bit rounds of the whole key
+  using LS = LocalSort<K, PAIRS, BLOCK, I, C16, KR>;
+  __shared__ typename LS::Smem sm;
+  const uint32_t count = *count_p;
+  for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
+    const uint32_t lw = list[2 * e + 1];
+    LS::run(sm, kin, vin, kout, vout, list[2 * e], lw & 0x7FFFFFFFu, (lw >> 31) ? KR : KR - 1);
+    __syncthreads();   // every LDS read of this entry before the next one's
   }
 }
 

@@ -208,6 +208,78 @@ def test_segmented_sort_short_segment_bound(gpu, kb, lengths, rank):
     s.close()
 
 
+# tile of the segmented onesweep pass (grs_capi.hip BigTile: 1024 threads x ITEMS) per
+# (key bits, payload); look-back groups are GRS_LB_GROUP = 8 tiles
+SEG_TILE = {(32, True): 1024 * 17, (32, False): 1024 * 36, (64, True): 1024 * 22, (64, False): 1024 * 17}
+
+
+@pytest.mark.parametrize("path", ["default", "lsd"])
+@pytest.mark.parametrize("pairs", [True, False], ids=["pairs", "keys"])
+@pytest.mark.parametrize("kb", [32, 64])
+@pytest.mark.parametrize("case", ["tile_edges", "group_edges", "one_long_many_short", "two_segments",
+                                  "skewed_runs"])
+def test_segmented_sort_long_segments(gpu, kb, pairs, case, path):
+    """Segments longer than the LDS sorts take: lengths at the 16K LDS bound, one tile (solo,
+    no look-back) and one past it, two tiles, at and around a look-back group of 8 tiles,
+    empty segments between, against oracle.segmented_sort_np; full-range keys with a
+    heavy-tie subset so every byte and the stability matter.  Path "default": segments of 4K
+    keys and more on average take the top-byte scatter + LDS sorts (grs_seg_runs: merged
+    runs, the primary and mid shapes, the segmented-LSD fallback for runs past LDS, which
+    "skewed_runs" reaches with a 200K-key run); "lsd" (GRS_OPT_MSD = never): the segmented LSD
+    (grs_seg_plan, grs_seg_hist, one grs_onesweep_seg launch per byte)."""
+    import gpuradixsort_amd as grs
+
+    T = SEG_TILE[(kb, pairs)]
+    dt = np.uint32 if kb == 32 else np.uint64
+    top = dt(kb - 8)
+    skew = None
+    if case == "tile_edges":
+        lengths = [16384, 16385, T - 1, T, 0, T + 1, 2 * T, 2 * T + 1, 1, 0, 3 * T - 7]
+    elif case == "group_edges":
+        lengths = [8 * T - 1, 8 * T, 0, 8 * T + 1, 9 * T + 5, 17 * T + 3]
+    elif case == "one_long_many_short":
+        lengths = [3] * 20000 + [5 * T + 11] + [0, 1, 2] * 3000
+    elif case == "two_segments":
+        lengths = [1, 40 * T + 99]
+    else:
+        # top bytes per segment: six runs of 10000 (the mid shape), one run of 200000 (the
+        # fallback, several tiles), uniform (merged runs), two runs of 15000
+        lengths = [60000, 200000, 5000, 30000]
+        skew = [np.repeat(np.arange(6), 10000), np.full(200000, 0x41), None, np.repeat([0x80, 0x81], 15000)]
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.uint32)
+    n = int(off[-1])
+    rng = np.random.default_rng(n + kb + pairs)
+    keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+    ties = rng.random(n) < 0.4
+    keys[ties] = rng.integers(0, 16, int(ties.sum())).astype(dt) * (np.iinfo(dt).max // dt(15))
+    if skew is not None:
+        for i, tb in enumerate(skew):
+            if tb is not None:
+                seg = slice(int(off[i]), int(off[i + 1]))
+                low = keys[seg] & ((dt(1) << top) - dt(1))
+                keys[seg] = (rng.permutation(tb).astype(dt) << top) | low
+    vals = np.arange(n, dtype=np.uint32)
+    want_k, want_v = oracle.segmented_sort_np(keys, off, vals)
+    s = grs.RadixSorter(n, key_bits=kb, pairs=True)
+    if path == "lsd":
+        s.set_option("msd", "never")
+    k = torch.from_numpy(keys.view(np.int32 if kb == 32 else np.int64).copy()).to(gpu)
+    v = torch.from_numpy(vals.view(np.int32).copy()).to(gpu) if pairs else None
+    o = torch.from_numpy(off.view(np.int32)).to(gpu)
+    for rep in range(2):                 # the second call reuses the planner's scratch
+        if rep:
+            k.copy_(torch.from_numpy(keys.view(np.int32 if kb == 32 else np.int64).copy()))
+            if pairs:
+                v.copy_(torch.from_numpy(vals.view(np.int32).copy()))
+        s.sort_segmented(k, o, v)
+        torch.cuda.synchronize()
+        s.check_error()
+        assert np.array_equal(k.cpu().numpy().view(dt), want_k), (case, rep)
+        if pairs:
+            assert np.array_equal(v.cpu().numpy().view(np.uint32), want_v), (case, rep)
+    s.close()
+
+
 def test_segmented_sort_needs_payload_sorter(gpu):
     import gpuradixsort_amd as grs
 

@@ -79,11 +79,15 @@ def main():
     k = torch.empty_like(k0)
     v = torch.empty_like(k0)
     ms_copy = timed(lambda: k.copy_(k0), a.reps)
-    # 1K-item segments (256-thread LDS sort), 16K-item segments (1024-thread LDS sort), 64
-    # segments of 1M items (the composite (segment, key) sort) and 4 of 16M (key sort + one
-    # partition pass by segment)
-    for segs in (1 << 16, 1 << 12, 1 << 6, 4):
-        off = torch.arange(0, m + 1, m // segs, dtype=torch.int32, device=dev)
+    # 1K-item segments (256-thread LDS sort), 16K-item segments (1024-thread LDS sort); 128K,
+    # 1M and 16M-item segments and 64 ragged ones (the segmented LSD: one planner block, one
+    # histogram, 4 segmented onesweep passes)
+    import numpy as np
+    rng = np.random.default_rng(3)
+    cuts = np.sort(rng.integers(0, m + 1, 63))
+    ragged = torch.from_numpy(np.concatenate([[0], cuts, [m]]).astype(np.int32)).to(dev)
+    for segs in (1 << 16, 1 << 12, 1 << 9, 1 << 6, 4, "ragged64"):
+        off = ragged if segs == "ragged64" else torch.arange(0, m + 1, m // segs, dtype=torch.int32, device=dev)
 
         def seg():
             k.copy_(k0)
