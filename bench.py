@@ -349,9 +349,13 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
                       for i, nm in enumerate(names)}
         dom = max(("p1_scatter_top_byte", "p2_scatter_byte2", "p3_local_sort"), key=msd_phases.get)
         mean_pass_ms = msd_phases[dom]
+    elif tims[0].get("kind") == "fused":
+        # every pass in one launch (grs_onesweep_fused): pass_ms[0] is that launch
+        mean_pass_ms = sum(t["pass_ms"][0] for t in tims) / len(tims)
     else:
         pass_ms = [p for t in tims for p in t["pass_ms"]]
         mean_pass_ms = sum(pass_ms) / len(pass_ms)
+    fused = tims[0].get("kind") == "fused"
     # the exchange grs_sort_sharded took (include/grs.h): presorted = local sort of the shard
     # first, then the encoded exchange and a merge; partition-first = local sort of the received
     # run.  Its phases of the last step, with the xGMI bytes and rate of this rank
@@ -364,7 +368,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     if msd:
         kernel_name = {"p1_scatter_top_byte": "grs_onesweep_region", "p2_scatter_byte2": "grs_onesweep_seg",
                        "p3_local_sort": "grs_msd_local"}[dom]
-    alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0))
+    alg_bytes = n_sorted_local * 2 * (kb // 8 + (4 if pairs else 0)) * (kb // rb if fused else 1)
     achieved = alg_bytes / (mean_pass_ms * 1e-3) / 1e9
     # SURVEY §8d credits P_cfg = key bits / digit bits passes, whatever schedule ran
     passes = kb // rb
@@ -416,7 +420,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         "cpu_baseline": cpu,
         "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
                       "sort_total_gpu": round(sort_ms, 5)},
-        "schedule": "msd" if msd else "lsd",
+        "schedule": "msd" if msd else "lsd-fused" if fused else "lsd",
         "check": {"inversions_last_step": inversions},
     }
     if msd:

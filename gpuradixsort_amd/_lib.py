@@ -56,7 +56,7 @@ GRS_EXTRACT_FIELD, GRS_EXTRACT_MORTON3 = 0, 1
 OPTIONS = {
     "tile": (1, {"size": -1, "small": 0, "big": 1}),
     "xl": (2, {"size": -1, "never": 0, "always": 1}),
-    "pass": (3, {"auto": 0, "v4": 4, "v6": 6}),
+    "pass": (3, {"auto": 0, "v4": 4, "v6": 6, "fused": 8}),
     "records": (4, {"arrays": 0, "scratch": 1, "split": 2}),
     "rank": (5, {"probe": 0, "match": 1}),
     "sharded_path": (6, {"auto": 0, "general": 1}),

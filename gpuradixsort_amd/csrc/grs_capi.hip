@@ -295,7 +295,8 @@ struct grs_sorter {
   int x_presorted = 0;
   uint64_t x_region_redo = 0;      // sharded partitions redone into contiguous buckets (spills)
   int tile_mode = -1;              // GRS_OPT_TILE: -1 by size, 0 small, 1 big
-  int pass_mode = 0;               // GRS_OPT_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6
+  int pass_mode = 0;               // GRS_OPT_PASS: 0 auto, 4 = grs_onesweep_v4, 6 = grs_onesweep_v6,
+                                   // 8 = grs_onesweep_fused
   bool sharded_general = false;    // GRS_OPT_SHARDED_PATH: one rank takes the G-rank path too
   int sharded_send = 0;            // GRS_OPT_SHARDED_SEND: 0 regions, 1 histogram + contiguous
                                    // buckets, 2 test: regions of n / (2G) (full buckets spill)
@@ -377,7 +378,7 @@ bool use_big_tiles(const grs_sorter* s, size_t n, size_t big_tile) {
 // tools/ab_pass.sh, Gkeys/s v6 vs v4: C2 49.8 vs 45.3; C4 119.3 vs 124.2, C3 56.5 vs 61.1,
 // C5 32.5 vs 34.3.
 bool use_persistent(const grs_sorter* s, size_t tiles, int rb) {
-  if (s->pass_mode != 0) return s->pass_mode == 6;
+  if (s->pass_mode != 0) return s->pass_mode == 6 || s->pass_mode == 8;
   return rb == 4 || tiles <= 4u * static_cast<size_t>(std::max(1, s->cus));
 }
 
@@ -508,7 +509,7 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       s->xl_mode = value == -1 ? 0 : value == 1 ? 1 : 2;
       break;
     case GRS_OPT_PASS:
-      if (value != 0 && value != 4 && value != 6) return bad();
+      if (value != 0 && value != 4 && value != 6 && value != 8) return bad();
       s->pass_mode = value;
       break;
     case GRS_OPT_RECORDS:
@@ -859,6 +860,38 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
     return p < passes - 1 && rec_split ? 4 : 2;
   };
   using Dig = grs::RadixDigit<K>;
+  // every pass in one launch (grs_onesweep_fused, GRS_OPT_PASS = 8): the persistent big-tile
+  // pass, full-width digits, in place.  Not the default: its grid barrier costs more than a
+  // kernel boundary (C2 0.47 vs 0.29 ms a sort, tools/barrier_probe.py)
+  const bool fused = persist && big && !rec && !src_in && s->rank_mode == 0 && (end_bit - begin_bit) % RB == 0 &&
+                     s->pass_mode == 8;
+  if constexpr (!Big::TWO_ROUNDS) {
+    if (fused) {
+      auto kern = grs::grs_onesweep_fused<K, PAIRS, RB, Big::BLOCK, Big::ITEMS, Big::MINW, kBig>;
+      static const int per_cu = [&] {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, Big::BLOCK, 0) != hipSuccess) b = 0;
+        return b;
+      }();
+      if (per_cu < 1) return set_err(GRS_EHIP, "internal: fused pass kernel does not fit a CU");
+      const uint32_t grid = std::min<uint32_t>(tiles, static_cast<uint32_t>(per_cu * std::max(1, s->cus)));
+      K* const alt = static_cast<K*>(s->alt_keys);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(Big::BLOCK), 0, stream, keys, alt, vals, s->alt_vals, n, begin_bit,
+                         passes, hist, tickets, tickets + 1, st0, st1, s->ctrl + GRS_CTRL_ERROR);
+      GRS_HIP(hipGetLastError());
+      if ((r = mark()) != GRS_OK) return r;
+      if ((passes & 1) != 0) {   // odd: the result sits in the scratch
+        GRS_HIP(hipMemcpyAsync(keys, alt, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToDevice, stream));
+        if (PAIRS) GRS_HIP(hipMemcpyAsync(vals, s->alt_vals, static_cast<size_t>(n) * 4, hipMemcpyDeviceToDevice, stream));
+        if ((r = mark()) != GRS_OK) return r;
+      }
+      if (evs) {
+        s->info[s->calls % s->ring] = {ev, 1, (passes & 1) != 0, 2};
+        ++s->calls;
+      }
+      return GRS_OK;
+    }
+  }
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
     const int bits = std::min(RB, end_bit - shift);
@@ -3075,8 +3108,10 @@ const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
   if (!s || n == 0) return "";
   auto pick = [&](size_t big_tile, bool two_rounds = false) -> const char* {
     if (s->rank_mode != 0 || !use_big_tiles(s, n, big_tile) || two_rounds) return "grs_onesweep_v4";
-    return use_persistent(s, (n + big_tile - 1) / big_tile, s->radix_bits) ? "grs_onesweep_v6"
-                                                                              : "grs_onesweep_v4";
+    if (!use_persistent(s, (n + big_tile - 1) / big_tile, s->radix_bits)) return "grs_onesweep_v4";
+    const bool rec = s->key_type == GRS_KEY_U32 && s->pairs && s->radix_bits == 8 && s->rec_mode != 0;
+    const bool fused = !rec && s->pass_mode == 8;
+    return fused ? "grs_onesweep_fused" : "grs_onesweep_v6";
   };
   const bool u32 = s->key_type == GRS_KEY_U32;
   if (s->radix_bits == 4)

@@ -735,6 +735,81 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
 }
 
 // ---------------------------------------------------------------------------------------
+// every pass of a sort in one launch
+// ---------------------------------------------------------------------------------------
+// Grid barrier of a launch whose workgroups are all resident: every wave waits for its stores
+// (the workgroup barrier alone does not: one CU's waves share its L1), then the workgroup adds 1
+// to *bar with release semantics at agent scope (its XCD's L2 written back: the next pass reads
+// on other XCDs) and waits until `target` have arrived (acquire: L1 / L2 invalidated).  The wait
+// is bounded like a look-back spin: past it the error word is set and the workgroup goes on.
+// Measured (tools/barrier_probe.py, 256 workgroups storing 16 MB a round): 27 us a round against
+// 5 us for a kernel boundary (11 us with no fences at all) -- hence not the default.
+__device__ __forceinline__ void grid_barrier(uint32_t* bar, uint32_t target, uint32_t* error_word,
+                                             uint32_t limit) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    while (ld_status(bar) < target) {
+      if (++spins > limit) {
+        atomicOr(error_word, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// The P passes of an LSD sort (digit p = bits [shift0 + RB p, + RB)) in ONE launch (option
+// GRS_OPT_PASS = 8; measured slower than one launch per pass): grid = the
+// resident workgroups (the host checks the occupancy: the barrier needs every one running),
+// each running grs_onesweep_v6's ticket loop over pass p's tiles, then a grid barrier before
+// pass p + 1 reads what pass p wrote.  Pass p reads (keys_a, vals_a) when p is even and
+// (keys_b, vals_b) when odd and writes the other pair; status buffers alternate as in separate
+// launches (pass p zeroes its tiles' words of pass p + 1's buffer).  bar: zero at launch.
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_fused(
+    K* keys_a, K* keys_b, uint32_t* vals_a, uint32_t* vals_b, uint32_t n, int shift0, int passes,
+    const uint32_t* __restrict__ hist, uint32_t* __restrict__ tickets, uint32_t* __restrict__ bar,
+    uint32_t* status0, uint32_t* status1, uint32_t* __restrict__ error_word) {
+  using Dig = RadixDigit<K>;
+  using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, Dig>;
+  __shared__ SM sm;
+  const uint32_t t = threadIdx.x;
+  const PassDebug dbg = PassDebug::read(error_word);
+  const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
+  for (int p = 0; p < passes; ++p) {
+    const bool odd = (p & 1) != 0;
+    K* const kin = odd ? keys_b : keys_a;
+    K* const kout = odd ? keys_a : keys_b;
+    uint32_t* const vin = odd ? vals_b : vals_a;
+    uint32_t* const vout = odd ? vals_a : vals_b;
+    uint32_t* const ticket = tickets + p * GRS_XCDS;
+    if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+    for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+    const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? hist[p * GRS_HIST_PASS_STRIDE + t] : 0u;
+    __syncthreads();
+    const Dig dig{shift0 + RB * p, (1u << RB) - 1u};
+    uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+    K key[ITEMS];
+    uint32_t val[ITEMS];
+    if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, kin, vin, n, tile, t);
+    while (tile < tiles) {
+      tile = onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, true>(
+          sm, TileSpan::whole(tile, n, SM::TILE), key, val, kin, kout, vin, vout, n, dig, gh, ticket,
+          odd ? status1 : status0, odd ? status0 : status1, error_word, dbg);
+      lds_barrier();
+      for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+      lds_barrier();
+    }
+    if (p + 1 < passes) grid_barrier(bar, static_cast<uint32_t>(p + 1) * gridDim.x, error_word, dbg.spin_limit);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // segmented pass: every segment of a table sorted by one digit on its own
 // ---------------------------------------------------------------------------------------
 // MSD sort and segmented sorts (grs_capi.hip): the same tile code as grs_onesweep_v4, over the

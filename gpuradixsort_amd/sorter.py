@@ -210,7 +210,7 @@ class RadixSorter:
         check(lib().grs_timing_history(self._h, int(k), ctypes.byref(t)), "grs_timing_history")
         return {"passes": t.passes, "total_ms": t.total_ms, "hist_ms": t.hist_ms,
                 "pass_ms": list(t.pass_ms)[: t.passes], "copy_ms": t.copy_ms,
-                "kind": "msd" if t.kind == 1 else "lsd"}
+                "kind": {1: "msd", 2: "fused"}.get(t.kind, "lsd")}
 
     def check_error(self, stream: Optional[torch.cuda.Stream] = None, device_wide: bool = False) -> None:
         """Raise GrsError(GRS_ETIMEOUT) if a look-back spin of an earlier call gave up.

@@ -71,9 +71,11 @@ typedef struct grs_timing {
   float pass_ms[16];         /* one onesweep launch per digit */
   float copy_ms;             /* final copy for an odd pass count (0 otherwise) */
   int kind;                  /* 0: LSD passes; 1: the MSD sort (GRS_OPT_MSD): hist_ms = the top
-                                byte's histogram, pass_ms[0..4] = the top-byte scatter, the
-                                per-bucket byte-2 histogram, the byte-2 scatter, the LDS sort of
-                                the 16-bit segments, the fallback of the longer ones */
+                                byte's sampled histogram, pass_ms[0..5] = the top-byte scatter, its
+                                redo (empty unless a run outgrew its region), the per-bucket
+                                byte-2 histogram, the byte-2 scatter, the LDS sort of the 16-bit
+                                segments, the fallback of the longer ones; 2: every LSD pass in
+                                one launch (GRS_OPT_PASS = 8): pass_ms[0] = that launch */
 } grs_timing;
 
 /* Library version (GRS_VERSION) and the last error message of this host thread. */
@@ -118,7 +120,10 @@ typedef enum grs_option {
   GRS_OPT_XL = 2,            /* -1 by size (default), 0 never, 1 XL two-round tiles wherever big
                                 tiles run (8-bit digits) */
   GRS_OPT_PASS = 3,          /* 0 by size (default), 4 one tile per workgroup (grs_onesweep_v4),
-                                6 persistent workgroups with next-tile prefetch (grs_onesweep_v6) */
+                                6 persistent workgroups with next-tile prefetch (grs_onesweep_v6),
+                                8 every pass in one launch of those workgroups, a grid barrier
+                                between passes (grs_onesweep_fused; slower than a kernel boundary
+                                per pass on MI355X, never chosen by size) */
   GRS_OPT_RECORDS = 4,       /* u32 pairs at 8-bit digits: 0 two arrays every pass, 1 8-byte
                                 (key, value) records in the sorter's scratch, 2 (default) also
                                 split over the caller's arrays (even n, 8-byte aligned) */

@@ -28,6 +28,7 @@ SHAPES = [
     (32, True, 8, {"tile": "big"}),                   # u32 pairs, record passes
     (64, False, 8, {"tile": "big"}),                  # u64 keys
     (32, False, 4, {"tile": "big"}),                  # 4-bit digits (C2's kernel)
+    (32, False, 4, {"tile": "big", "pass": "fused"}),  # 4-bit digits, every pass in one launch
     (32, False, 8, {"rank": "match", "tile": "big"}),  # ballot-match fallback
 ]
 

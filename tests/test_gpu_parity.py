@@ -320,14 +320,17 @@ def test_ballot_match_fallback(gpu, monkeypatch):
             s.close()
 
 
+@pytest.mark.parametrize("pass_kernel", ["v6", "fused"])
 @pytest.mark.parametrize("kb,pairs,rb", [(32, False, 8), (32, True, 8), (64, False, 8),
                                           (64, True, 8), (32, False, 4), (64, True, 4)])
-def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb):
+def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb, pass_kernel):
     """Option pass=v6: the persistent big-tile pass (grs_onesweep_v6: resident workgroups loop
     over tickets, the next tile's loads issued behind the reorder) gives the same bit-exact
     results across tile edges, for every key/payload type and both digit widths (u64 pairs at
     8-bit digits keep the two-round v4 pass, whose second round needs the registers the
-    prefetch would take)."""
+    prefetch would take).  pass=fused: every pass in one launch of those workgroups with a grid
+    barrier between passes (grs_onesweep_fused; u32 pairs at 8-bit digits keep v6 and their
+    record passes)."""
     import gpuradixsort_amd as grs
 
     rng = np.random.default_rng(11 + kb + pairs + rb)
@@ -338,7 +341,9 @@ def test_persistent_pass(gpu, monkeypatch, kb, pairs, rb):
         keys[1::13] = 3
         perm = oracle.stable_argsort(keys)
         s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb,
-                            options={"pass": "v6", "tile": "big"})
+                            options={"pass": pass_kernel, "tile": "big"})
+        if pass_kernel == "fused" and not (kb == 64 and pairs and rb == 8) and not (kb == 32 and pairs and rb == 8):
+            assert s.pass_kernel_for(max(n, 2)) in ("grs_onesweep_fused", "grs_onesweep_v4"), n
         k = to_dev(keys, gpu)
         v = to_dev(np.arange(n, dtype=np.uint32), gpu) if pairs else None
         s.sort(k, v)
