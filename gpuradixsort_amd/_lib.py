@@ -91,6 +91,8 @@ SIGNATURES = [
                               c_int, c_void_p, c_void_p]),
     ("grs_partition_ranges", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                      c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("grs_partition_regions", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                      c_void_p, c_void_p, c_int, c_size_t, c_void_p, c_void_p]),
     ("grs_sort_sharded", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                  c_size_t, POINTER(c_size_t), c_void_p, c_void_p]),
     ("grs_sharded_last_timing", c_int, [c_void_p, POINTER(grs_sharded_timing)]),

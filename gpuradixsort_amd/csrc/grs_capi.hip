@@ -103,14 +103,16 @@ struct MatchTile {
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr bool TWO_ROUNDS = false;
 };
-// Partition pass (key-range buckets for the multi-GPU exchange): the big tiles (its digit
-// needs the element index, so the store phase reads a position's digit off the tile-local
-// digit starts instead of the key).  36K-key tiles: 2^27 keys into 8 buckets 0.38 -> 0.xx ms
-// against round 1's 24K tiles with one digit byte per key in LDS.
+// Partition pass (key-range buckets for the multi-GPU exchange): big tiles (its digit needs
+// the element index, so the store phase reads a position's digit off the tile-local digit
+// starts instead of the key).  u32 keys: 1024 x 32, not x 36 -- the composite splitter compares
+// push the 36-key tile to 128 VGPRs and scratch spills (tools/lab6.py, 2^27 keys into 8
+// buckets: 0.304-0.311 vs 0.341 ms a pass; a 12-bit bucket table in LDS instead of the compares
+// 0.329-0.360, 32-bit compares with a branch for keys equal to a splitter 0.331).
 template <typename K, bool PAIRS>
 struct PartTile {
   static constexpr int BLOCK = 1024, MINW = 1;
-  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 36) : (PAIRS ? 11 : 17);
+  static constexpr int ITEMS = sizeof(K) == 4 ? (PAIRS ? 17 : 32) : (PAIRS ? 11 : 17);
   static constexpr int TILE = BLOCK * ITEMS;
   static constexpr bool TWO_ROUNDS = false;
 };
@@ -1185,14 +1187,15 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
   const size_t words = status_words_for(tiles, 16);
   if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
   uint32_t* hist = s->ctrl;
-  GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = true;   // run_sort's block may be this one (sorter.cb_i)
   if (region) {
     // "digit counts" of `region` each: the pass's digit-start scan yields b * region
-    GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(hist), static_cast<int>(region),
-                              count + 1, stream));
-    GRS_HIP(hipMemsetAsync(s->status, 0, words * 4, stream));
+    hipLaunchKernelGGL(grs::grs_part_init, dim3(std::max<uint32_t>(1u, std::min<uint32_t>(256u, static_cast<uint32_t>(words / 1024 + 1)))),
+                       dim3(256), 0, stream, hist, static_cast<uint32_t>(GRS_CTRL_ERROR), region,
+                       static_cast<uint32_t>(count + 1), s->status, static_cast<uint32_t>(words));
+    GRS_HIP(hipGetLastError());
   } else {
+    GRS_HIP(hipMemsetAsync(s->ctrl, 0, GRS_CTRL_ERROR * 4, stream));
     // one resident wave of workgroups (grid-stride loop): 2048 blocks at 6 per CU (76 VGPRs)
     // ran as 1536 + 512, a second, mostly empty round (tools/prof_partition.py)
     static const int per_cu = [] {
@@ -1219,7 +1222,7 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
   if (r != GRS_OK) return r;
   if (region) {
     const uint32_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
-    hipLaunchKernelGGL(grs::grs_lb_totals, dim3(1), dim3(64), 0, stream,
+    hipLaunchKernelGGL(grs::grs_lb_totals, dim3(1), dim3(256), 0, stream,
                        s->status + static_cast<size_t>(tiles) * 16, groups, 16u,
                        static_cast<uint32_t>(count + 1), d_counts);
     GRS_HIP(hipGetLastError());
@@ -1233,7 +1236,7 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
 template <typename K, bool PAIRS>
 grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* keys_out,
                          uint32_t* vals_out, uint32_t n, const K* splitters, const uint32_t* th,
-                         int count, uint32_t* d_counts, hipStream_t stream) {
+                         int count, uint32_t* d_counts, hipStream_t stream, uint32_t region = 0) {
   auto go = [&](auto nconst) {
     constexpr int N = decltype(nconst)::value;
     grs::SplitterIdxDigit<K, N> d{};
@@ -1244,7 +1247,7 @@ grs_status run_partition(grs_sorter* s, const K* keys, const uint32_t* vals, K* 
       d.th[i] = i < count ? (th ? th[i] : 0u) : 0xFFFFFFFFu;
     }
     return run_partition_n<K, PAIRS, N>(s, keys, vals, keys_out, vals_out, n, d, nullptr, count,
-                                        d_counts, stream);
+                                        d_counts, stream, region);
   };
   if (count <= 1) return go(std::integral_constant<int, 1>{});
   if (count <= 3) return go(std::integral_constant<int, 3>{});
@@ -1259,7 +1262,8 @@ extern "C" {
 static grs_status partition_impl(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
                                  void* d_keys_out, uint32_t* d_vals_out, size_t n,
                                  const void* splitters, const uint32_t* thresholds,
-                                 int n_splitters, uint32_t* d_counts, void* stream) {
+                                 int n_splitters, uint32_t* d_counts, void* stream,
+                                 uint32_t region = 0) {
   if (!s) return set_err(GRS_EINVAL, "grs_partition: NULL sorter");
   if (n_splitters < 0 || n_splitters > GRS_MAX_SPLITTERS || (n_splitters > 0 && !splitters))
     return set_err(GRS_EINVAL, "grs_partition: 0..15 splitters required");
@@ -1282,20 +1286,20 @@ static grs_status partition_impl(grs_sorter* s, const void* d_keys, const uint32
     if (s->pairs)
       r = run_partition<uint32_t, true>(s, (const uint32_t*)d_keys, d_vals, (uint32_t*)d_keys_out,
                                         d_vals_out, n32, (const uint32_t*)splitters, thresholds,
-                                        n_splitters, d_counts, st);
+                                        n_splitters, d_counts, st, region);
     else
       r = run_partition<uint32_t, false>(s, (const uint32_t*)d_keys, nullptr, (uint32_t*)d_keys_out,
                                          nullptr, n32, (const uint32_t*)splitters, thresholds,
-                                         n_splitters, d_counts, st);
+                                         n_splitters, d_counts, st, region);
   } else {
     if (s->pairs)
       r = run_partition<uint64_t, true>(s, (const uint64_t*)d_keys, d_vals, (uint64_t*)d_keys_out,
                                         d_vals_out, n32, (const uint64_t*)splitters, thresholds,
-                                        n_splitters, d_counts, st);
+                                        n_splitters, d_counts, st, region);
     else
       r = run_partition<uint64_t, false>(s, (const uint64_t*)d_keys, nullptr, (uint64_t*)d_keys_out,
                                          nullptr, n32, (const uint64_t*)splitters, thresholds,
-                                         n_splitters, d_counts, st);
+                                         n_splitters, d_counts, st, region);
   }
   if (prev != s->device) (void)hipSetDevice(prev);
   return r;
@@ -1317,6 +1321,18 @@ grs_status grs_partition_ranges(grs_sorter* s, const void* d_keys, const uint32_
     return set_err(GRS_EINVAL, "grs_partition_ranges: thresholds are NULL");
   return partition_impl(s, d_keys, d_vals, d_keys_out, d_vals_out, n, splitters, thresholds,
                         n_splitters, d_counts, stream);
+}
+
+grs_status grs_partition_regions(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                                 void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                                 const void* splitters, const uint32_t* thresholds,
+                                 int n_splitters, size_t region, uint32_t* d_counts, void* stream) {
+  if (n_splitters > 0 && !thresholds)
+    return set_err(GRS_EINVAL, "grs_partition_regions: thresholds are NULL");
+  if (n > 0 && (region == 0 || static_cast<uint64_t>(n_splitters + 1) * region >= (uint64_t(1) << 32)))
+    return set_err(GRS_EINVAL, "grs_partition_regions: need 0 < region and (n_splitters + 1) * region < 2^32");
+  return partition_impl(s, d_keys, d_vals, d_keys_out, d_vals_out, n, splitters, thresholds,
+                        n_splitters, d_counts, stream, static_cast<uint32_t>(region));
 }
 
 grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n, int begin_bit,

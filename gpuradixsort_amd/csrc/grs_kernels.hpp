@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "grs_config.h"
 
 namespace grs {
@@ -356,14 +358,36 @@ __global__ __launch_bounds__(Hist2Layout<K>::BLOCK) void grs_upfront_hist2(
 
 // Per-digit totals of a finished pass from its look-back status: every tile added its count to
 // its group's accumulator ((arrivals << 24) | sum), so a digit's total is the sum over groups.
-// One thread per digit (radix <= 16: the partition's buckets).
-__global__ void grs_lb_totals(const uint32_t* __restrict__ gacc, uint32_t groups, uint32_t radix,
-                              uint32_t count, uint32_t* __restrict__ totals) {
-  const uint32_t d = threadIdx.x;
-  if (d >= count) return;
+// One block of 256 threads: digit d (radix <= 16: the partition's buckets) summed by 16 threads
+// over every 16th group, then added up in LDS.
+__global__ __launch_bounds__(256) void grs_lb_totals(const uint32_t* __restrict__ gacc, uint32_t groups,
+                                                     uint32_t radix, uint32_t count,
+                                                     uint32_t* __restrict__ totals) {
+  __shared__ uint32_t part[256];
+  const uint32_t d = threadIdx.x & 15u, q = threadIdx.x >> 4;
   uint32_t sum = 0;
-  for (uint32_t g = 0; g < groups; ++g) sum += gacc[static_cast<size_t>(g) * radix + d] & 0xFFFFFFu;
-  totals[d] = sum;
+  if (d < count)
+    for (uint32_t g = q; g < groups; g += 16) sum += gacc[static_cast<size_t>(g) * radix + d] & 0xFFFFFFu;
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x < count) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tot += part[k * 16 + threadIdx.x];
+    totals[threadIdx.x] = tot;
+  }
+}
+
+// Control block and look-back status of a region-mode partition pass, in one launch instead of
+// three memsets: ctrl[0, ctrl_words) = 0 (digit counts, tickets), then the count + 1 digit
+// "counts" = region (the pass's digit-start scan yields b * region), status[0, words) = 0.
+__global__ __launch_bounds__(256) void grs_part_init(uint32_t* __restrict__ ctrl, uint32_t ctrl_words,
+                                                     uint32_t region, uint32_t count,
+                                                     uint32_t* __restrict__ status, uint32_t words) {
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < ctrl_words; i += stride)
+    ctrl[i] = i < count ? region : 0u;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < words; i += stride) status[i] = 0;
 }
 
 // Digit of key k at shard-local index i, for plain and indexed digit functors.

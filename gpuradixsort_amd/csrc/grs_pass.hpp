@@ -214,8 +214,10 @@ struct V4Smem {
   alignas(16) K keys[LTILE];
   uint32_t vals[PAIRS ? LTILE : 1];
   // indexed digits (partition): tile-local start of every digit, from which the store phase
-  // reads off the digit of a reordered position (the key alone does not determine it)
+  // reads off the digit of a reordered position (the key alone does not determine it), and per
+  // 64-position chunk the digits of its first and last position (first | last << 8)
   uint32_t lstart[IDX ? RADIX + 1 : 1];
+  uint16_t cdig[IDX ? TILE / GRS_WAVE : 1];
 };
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int OPT, typename DigitF>
 using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::kIndexed,
@@ -459,6 +461,18 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   }
   lds_barrier();  // B3
 
+  if constexpr (IDX) {   // the chunk digits (read in the store phase, after B4)
+    for (uint32_t c = t; c < static_cast<uint32_t>(TILE / GRS_WAVE); c += BLOCK) {
+      uint32_t d0 = 0, d1 = 0;
+#pragma unroll
+      for (int b = 1; b < RADIX; ++b) {
+        const uint32_t ls = sm.lstart[b];
+        d0 += ls <= c * GRS_WAVE;
+        d1 += ls <= c * GRS_WAVE + GRS_WAVE - 1;
+      }
+      sm.cdig[c] = static_cast<uint16_t>(d0 | (d1 << 8));
+    }
+  }
   // ---- reorder the tile in LDS by (digit, input order) ----
   // the digits are recomputed from the keys (1 VALU each) instead of being kept live since
   // the ranking: the empty asm hides the earlier values from common-subexpression elimination
@@ -529,7 +543,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // digit of reordered position i.  Indexed digits: a thread visits increasing positions, so
   // its digit only moves forward through the tile-local digit starts (at most RADIX - 1 steps
   // per tile, over empty digits too).
-  uint32_t dcur = 0;
   auto put = [&](uint32_t dst, K kk, uint32_t i) {
     if constexpr ((OPT & 8192) != 0) {
       static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
@@ -548,8 +561,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   };
   auto dig_at = [&](uint32_t i, K kk) -> uint32_t {
     if constexpr (IDX) {
-      while (i >= sm.lstart[dcur + 1]) ++dcur;
-      return dcur;
+      // the digits at the ends of i's 64-position chunk (one wave-instruction's positions: a
+      // broadcast read); a walk over the digit starts only where a run starts inside the chunk
+      const uint32_t c = sm.cdig[i >> 6];
+      uint32_t d = c & 255u;
+      if (d != (c >> 8))
+        while (i >= sm.lstart[d + 1]) ++d;
+      return d;
     } else {
       return dig(kk);
     }
@@ -621,12 +639,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   uint32_t val[ITEMS];
   if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+  // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
+  const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   __syncthreads();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
   tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
-  // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
-  const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, TileSpan::whole(tile, n, SM::TILE), key, val,
                                                  keys_in, keys_out, vals_in,
                                                  vals_out, n, dg, gh, ticket, status, status_next,
@@ -715,8 +733,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   const PassDebug dbg = PassDebug::read(error_word);
-  __syncthreads();
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
+  __syncthreads();
   const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
   uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
   K key[ITEMS];

@@ -158,6 +158,37 @@ class RadixSorter:
                                   ctypes.c_void_p(sp.ctypes.data), int(sp.size), _ptr(counts),
                                   _stream_ptr(stream)), "grs_partition")
 
+    def partition_regions(self, keys: torch.Tensor, keys_out: torch.Tensor, splitters, counts: torch.Tensor,
+                          region: int, thresholds=None, vals: Optional[torch.Tensor] = None,
+                          vals_out: Optional[torch.Tensor] = None, n: Optional[int] = None,
+                          stream: Optional[torch.cuda.Stream] = None) -> None:
+        """The same partition into regions (grs_partition_regions, the exchange's send step):
+        bucket b from keys_out[b * region] on, no bucket histogram; keys_out (and vals_out) hold
+        len(splitters) * region + n items; a count > region means that bucket ran on into the
+        next region.  thresholds: shard-local index thresholds (ties by position), default 0."""
+        import numpy as np
+
+        self._check_keys(keys, vals)
+        n = keys.numel() if n is None else int(n)
+        sp = np.ascontiguousarray(np.asarray(splitters, dtype=np.uint32 if self.key_bits == 32
+                                             else np.uint64))
+        th = np.ascontiguousarray(np.zeros(sp.size, np.uint32) if thresholds is None
+                                  else np.asarray(thresholds, dtype=np.uint32))
+        need = sp.size * int(region) + n
+        if (not keys_out.is_cuda or not keys_out.is_contiguous() or keys_out.numel() < need
+                or keys_out.element_size() != keys.element_size()):
+            raise ValueError(f"keys_out must be a contiguous device tensor of >= {need} keys")
+        if self.pairs and (vals_out is None or vals_out.numel() < need or not vals_out.is_contiguous()):
+            raise ValueError(f"pairs partition needs a contiguous vals_out of >= {need} items")
+        if counts.numel() < sp.size + 1 or counts.element_size() != 4:
+            raise ValueError("counts needs len(splitters) + 1 32-bit entries")
+        vp = _ptr(vals) if vals is not None else ctypes.c_void_p(0)
+        vo = _ptr(vals_out) if vals_out is not None else ctypes.c_void_p(0)
+        check(lib().grs_partition_regions(self._h, _ptr(keys), vp, _ptr(keys_out), vo, n,
+                                          ctypes.c_void_p(sp.ctypes.data), ctypes.c_void_p(th.ctypes.data),
+                                          int(sp.size), int(region), _ptr(counts), _stream_ptr(stream)),
+              "grs_partition_regions")
+
     def sort_host(self, keys, vals=None, stream: Optional[torch.cuda.Stream] = None) -> None:
         """Sort host numpy arrays in place through device staging (grs_sort_host; BASELINE C1
         plumbing, PCIe both ways).  keys: uint32/uint64 numpy array; vals: uint32 or None."""

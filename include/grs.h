@@ -210,6 +210,18 @@ grs_status grs_partition_ranges(grs_sorter* s, const void* d_keys, const uint32_
                                 const void* splitters, const uint32_t* thresholds,
                                 int n_splitters, uint32_t* d_counts, void* stream);
 
+/* The same partition into REGIONS instead of back-to-back buckets (the multi-GPU exchange's
+ * send step, grs_sort_sharded): bucket b is written from d_keys_out[b * region] on (and
+ * d_vals_out), so no bucket histogram (a read of the keys) precedes the pass; the bucket sizes
+ * still go to d_counts.  The output arrays hold n_splitters * region + n items: a bucket larger
+ * than `region` runs on into the next region (the later buckets are then wrong) but never past
+ * the arrays -- a count > region says so, and grs_partition_ranges is the fallback.  Requires
+ * 0 < region and (n_splitters + 1) * region < 2^32. */
+grs_status grs_partition_regions(grs_sorter* s, const void* d_keys, const uint32_t* d_vals,
+                                 void* d_keys_out, uint32_t* d_vals_out, size_t n,
+                                 const void* splitters, const uint32_t* thresholds,
+                                 int n_splitters, size_t region, uint32_t* d_counts, void* stream);
+
 /* ---- multi-GPU: one process per GPU, RCCL over xGMI ----
  * The reference has no multi-device path; this is BASELINE config C4's exchange.  Rank r's
  * input is the global range that follows ranks < r; on return rank r holds a contiguous,

@@ -536,3 +536,61 @@ def test_partition_is_stable_range_split(gpu, kb, pairs):
         assert np.array_equal(ko.cpu().numpy(), keys[perm])
         if pairs:
             assert np.array_equal(vo.cpu().numpy(), perm)
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+@pytest.mark.parametrize("pairs", [False, True])
+def test_partition_regions_with_ties(gpu, kb, pairs):
+    """grs_partition_regions (the exchange's send step): bucket b at keys_out[b * region], no
+    bucket histogram; splitters with index thresholds split runs of equal keys, and splitter
+    keys sharing a 12-bit prefix exercise the compares behind the LDS bucket table
+    (SplitterIdxDigit::fill_lut).  Then a region too small: the count shows the spill."""
+    import gpuradixsort_amd as grs
+
+    rng = np.random.default_rng(100 + kb + pairs)
+    dt = np.uint32 if kb == 32 else np.uint64
+    sh = dt(kb - 12)
+    for n, nsplit in ((1, 1), (5000, 3), (300_007, 7), (777_777, 15)):
+        keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        keys[::11] = keys[0]                              # a run of equal keys across buckets
+        keys[1::17] = (dt(5) << sh) | dt(3)               # many keys in one shared prefix
+        cand = np.concatenate([keys[:1], [(dt(5) << sh) | dt(3), (dt(5) << sh) | dt(1)],
+                               rng.choice(keys, 16)]).astype(dt)
+        sp = np.sort(rng.choice(cand, nsplit))
+        th = rng.integers(0, n + 1, nsplit).astype(np.uint32)
+        idx = np.arange(n, dtype=np.uint64)
+        bucket = np.zeros(n, np.int64)
+        for b in range(nsplit):
+            bucket += (sp[b] < keys) | ((sp[b] == keys) & (th[b] <= idx))
+        counts = np.bincount(bucket, minlength=nsplit + 1)
+        region = int(counts.max()) + 64
+        s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=8)
+        k = to_dev(keys, gpu)
+        ko = torch.empty(nsplit * region + n, dtype=k.dtype, device=gpu)
+        v = vo = None
+        if pairs:
+            v = to_dev(np.arange(n, dtype=np.uint32), gpu)
+            vo = torch.empty(nsplit * region + n, dtype=torch.uint32, device=gpu)
+        cnt = torch.zeros(nsplit + 1, dtype=torch.uint32, device=gpu)
+        s.partition_regions(k, ko, sp, cnt, region, thresholds=th, vals=v, vals_out=vo)
+        torch.cuda.synchronize()
+        s.check_error()
+        assert np.array_equal(cnt.cpu().numpy(), counts), n
+        ko_h = ko.cpu().numpy()
+        vo_h = vo.cpu().numpy() if pairs else None
+        for b in range(nsplit + 1):
+            sel = np.nonzero(bucket == b)[0]
+            got = ko_h[b * region: b * region + sel.size]
+            assert np.array_equal(got, keys[sel]), (n, b)
+            if pairs:
+                assert np.array_equal(vo_h[b * region: b * region + sel.size], sel.astype(np.uint32)), (n, b)
+        if n > 1000:   # a region smaller than the largest bucket: its count says so
+            small = int(counts.max()) - 1
+            ko2 = torch.empty(nsplit * small + n, dtype=k.dtype, device=gpu)
+            vo2 = torch.empty(nsplit * small + n, dtype=torch.uint32, device=gpu) if pairs else None
+            s.partition_regions(k, ko2, sp, cnt, small, thresholds=th, vals=v, vals_out=vo2)
+            torch.cuda.synchronize()
+            s.check_error()
+            c2 = cnt.cpu().numpy()
+            assert np.array_equal(c2, counts) and int(c2.max()) > small
+        s.close()

@@ -5,6 +5,8 @@ per rank).
 python tools/bench_sharded_steps.py [--ranks 8] [--reps 10]
 Prints one JSON line per step:
   partition      grs_partition_ranges of one rank's shard into N buckets with tie-breaking
+  partition_regions  the same into the exchange's region send buffer (grs_partition_regions:
+                 no bucket histogram; what grs_sort_sharded runs)
                  splitters (the splitters of rank 0, from the host twin over all ranks' samples)
   local_sort     grs_sort of the received run (2^30 / N keys), full-range keys and (the
                  realistic case) keys of one of the N key ranges
@@ -85,6 +87,21 @@ def main():
     s.check_error()
     print(json.dumps({"step": "partition", "ranks": G, "n_local": n, "ms": round(ms, 4),
                       "GB/s": round(n * 8 / ms / 1e6, 1)}), flush=True)
+    # what grs_sort_sharded runs: the region send buffer (no bucket histogram), the region being
+    # the even share + 25 % + 64K items
+    region = min(n, n * 5 // 4 // G + 65536)
+    xout = torch.empty((G - 1) * region + n, dtype=shard.dtype, device=dev)
+
+    def part_regions():
+        check(L.grs_partition_regions(s._h, ctypes.c_void_p(shard.data_ptr()), None,
+                                      ctypes.c_void_p(xout.data_ptr()), None, n, spl.ctypes.data,
+                                      th.ctypes.data, G - 1, region, ctypes.c_void_p(cnt.data_ptr()), sp),
+              "partition_regions")
+    ms = timed(part_regions, a.reps)
+    s.check_error()
+    print(json.dumps({"step": "partition_regions", "ranks": G, "n_local": n, "ms": round(ms, 4),
+                      "GB/s": round(n * 8 / ms / 1e6, 1)}), flush=True)
+    del xout
 
     bufs = [torch.empty_like(shard) for _ in range(a.reps + 1)]
     for b in bufs:
