@@ -146,11 +146,14 @@ typedef enum grs_option {
                                 polls, so the later tiles of its look-back group time out: the
                                 sort's output is wrong and GRS_ETIMEOUT surfaces through
                                 grs_check_error / grs_stream_check_error (the error path's test) */
-  GRS_OPT_MSD = 11           /* u32 keys without payload, 8-bit digits, the whole key: -1 by size
-                                (default), 0 never, 1 always -- the MSD-first sort (two stable
-                                scatters by the top two bytes into 65536 segments, each finished
-                                in LDS by one workgroup; segments too long for LDS sorted by a
-                                segmented LSD on their low 16 bits) instead of 4 LSD passes */
+  GRS_OPT_MSD = 11           /* u32 keys, u32 keys + u32 payload, u64 keys; 8-bit digits, the
+                                whole key: -1 by size (default: from 48M keys), 0 never, 1 always
+                                -- the MSD-first sort (two stable scatters by the top two bytes
+                                into 65536 segments, each finished in LDS by one workgroup;
+                                segments too long for LDS sorted by a segmented LSD on the bits
+                                below their 16-bit prefix) instead of the LSD passes.  Also
+                                grs_sort_segmented's long segments: 0 keeps them on the segmented
+                                LSD instead of the top-byte scatter + LDS sorts */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);
