@@ -1079,15 +1079,19 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // histogram per top-byte bucket over alt; zeroes P2's status
   {
     uint32_t* const tab = mb + L.tab;
+    // H2 chunks: ~8 rounds of the resident blocks (2 per CU), 32K to 256K keys
+    uint32_t chunk = GRS_H2_CHUNK;
+    while (chunk > 32768u && static_cast<uint64_t>(n) / chunk < 16u * static_cast<uint64_t>(std::max(1, s->cus)))
+      chunk >>= 1;
     if (xl)
       hipLaunchKernelGGL((grs::grs_msd_plan2<XL::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
-                         totals, exact, tab, rec2, hdr2);
+                         totals, exact, chunk, tab, rec2, hdr2);
     else
       hipLaunchKernelGGL((grs::grs_msd_plan2<Big::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
-                         totals, exact, tab, rec2, hdr2);
+                         totals, exact, chunk, tab, rec2, hdr2);
     GRS_HIP(hipGetLastError());
-    hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / GRS_H2_CHUNK + 257), dim3(1024), 0, stream, alt,
-                       h2, st[1], static_cast<uint32_t>(words2), tab);
+    hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
+                       h2, st[1], static_cast<uint32_t>(words2), tab, chunk);
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;

@@ -269,13 +269,13 @@ __global__ __launch_bounds__(256) void grs_msd_sample(const K* __restrict__ keys
 }
 
 // The top-byte bucket table after P1: in[s] = where bucket s's keys lie in alt, len[s] = its
-// keys, out[s] = where its sorted keys go, cpre[s] = H2 chunks before bucket s (cpre[256] =
-// all).  P1's regions when no run outgrew its region (totals[256] == 0), the redone exact
+// keys, out[s] = where its sorted keys go, cpre[s] = H2 chunks of `chunk` keys before bucket s
+// (cpre[256] = all).  P1's regions when no run outgrew its region (totals[256] == 0), the redone exact
 // layout otherwise.  One block computes it into LDS (in, len, out, cpre: 4 x 257 words).
 __device__ void msd_bucket_table(const uint32_t* __restrict__ samp, unsigned long long mult,
                                  uint32_t pad, const uint32_t* __restrict__ totals,
-                                 const uint32_t* __restrict__ exact, uint32_t* in, uint32_t* len,
-                                 uint32_t* out, uint32_t* cpre, uint32_t* wsum) {
+                                 const uint32_t* __restrict__ exact, uint32_t chunk, uint32_t* in,
+                                 uint32_t* len, uint32_t* out, uint32_t* cpre, uint32_t* wsum) {
   const uint32_t t = threadIdx.x;   // blockDim == 1024
   const bool redo = totals[256] != 0u;
   uint32_t v[3] = {0, 0, 0}, tot[3];
@@ -284,7 +284,7 @@ __device__ void msd_bucket_table(const uint32_t* __restrict__ samp, unsigned lon
     const uint32_t r = redo ? l : static_cast<uint32_t>((static_cast<unsigned long long>(samp[t]) * mult) >> 20) + pad;
     v[0] = l;
     v[1] = r;
-    v[2] = (l + GRS_H2_CHUNK - 1) / GRS_H2_CHUNK;
+    v[2] = (l + chunk - 1) / chunk;
     len[t] = l;
   }
   block_scan<1024, 3>(v, wsum, tot);
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
                                                       unsigned long long mult, uint32_t pad,
                                                       const uint32_t* __restrict__ totals,
                                                       const uint32_t* __restrict__ exact,
-                                                      uint32_t* __restrict__ tab,
+                                                      uint32_t chunk, uint32_t* __restrict__ tab,
                                                       SegTile* __restrict__ rec2,
                                                       uint32_t* __restrict__ hdr2) {
   __shared__ uint32_t lds[GRS_PLAN_LDS_WORDS + 4 * 257 + 64];
@@ -313,20 +313,21 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
   uint32_t* const out = len + 257;
   uint32_t* const cpre = out + 257;
   uint32_t* const wsum = cpre + 257;
-  msd_bucket_table(samp, mult, pad, totals, exact, in, len, out, cpre, wsum);
+  msd_bucket_table(samp, mult, pad, totals, exact, chunk, in, len, out, cpre, wsum);
   for (uint32_t i = threadIdx.x; i < 4 * 257; i += 1024) tab[i] = in[i];
   seg_plan_block<TILE2, 1024, kSegMoved>(in, len, out, 256u, nullptr, rec2, hdr2, lds);
 }
 
-// H2: h2[(top byte) * 256 + byte 2] over P1's output, one 256K-key chunk of one bucket per
-// block (grid >= n / chunk + 256; tab from grs_msd_plan2); zeroes `zero_words` of `zero` (P2's
-// status).  Two 1024-thread blocks per CU (8 waves per SIMD).
+// H2: h2[(top byte) * 256 + byte 2] over P1's output, one chunk of one bucket per block (grid
+// >= n / chunk + 256; tab from grs_msd_plan2 with the same chunk: 256K keys at 2^30, fewer
+// below so the grid is several resident rounds, not 2.5 with a tail); zeroes `zero_words` of
+// `zero` (P2's status).  Two 1024-thread blocks per CU (8 waves per SIMD).
 template <typename K>
 __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ keys,
                                                          uint32_t* __restrict__ h2,
                                                          uint32_t* __restrict__ zero,
                                                          uint32_t zero_words,
-                                                         const uint32_t* __restrict__ tab) {
+                                                         const uint32_t* __restrict__ tab, uint32_t chunk) {
   constexpr uint32_t B = 1024;
   constexpr uint32_t LW = 256 * GRS_H2_COPIES;
   __shared__ __attribute__((aligned(16))) uint32_t h[LW];
@@ -344,8 +345,8 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
     if (cpre[mid] <= b) lo = mid; else hi = mid;
   }
   const uint32_t s = lo, j = b - cpre[s];
-  const uint32_t c0 = tab[s] + j * GRS_H2_CHUNK;
-  const uint32_t cl = min(static_cast<uint32_t>(GRS_H2_CHUNK), tab[257 + s] - j * GRS_H2_CHUNK);
+  const uint32_t c0 = tab[s] + j * chunk;
+  const uint32_t cl = min(chunk, tab[257 + s] - j * chunk);
   uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
   constexpr int SH = 8 * static_cast<int>(sizeof(K)) - 16;   // the second byte from the top
   auto count = [&](K k) {
