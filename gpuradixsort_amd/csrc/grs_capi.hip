@@ -123,7 +123,7 @@ struct PartTile {
 constexpr uint32_t kBig4Opt = 0;
 constexpr uint32_t kSmallOpt = 16;
 constexpr uint32_t kMatchOpt = 512 | 16;               // ballot-match ranking (fallback)
-// (XCD ranges stay a lab option, tools/lab_pass.hpp: they need the digit counts of every
+// (XCD ranges were a lab option, git show 729d494:tools/lab_pass.hpp: they need the digit counts of every
 // range for every pass, and a range of pass p > 0 holds the keys pass p - 1 scattered there,
 // which no upfront histogram of the input positions gives)
 

@@ -403,26 +403,39 @@ struct LocalSort {
     uint32_t wtot[4];
     uint32_t slot;
   };
+  using Vals = uint32_t[PAIRS ? I : 1];
   __device__ __forceinline__ static void run(Smem& sm, K* __restrict__ keys, uint32_t* __restrict__ vals,
                                              uint32_t lo, uint32_t len) {
     run(sm, keys, vals, keys, vals, lo, len, ROUNDS);
   }
   __device__ __forceinline__ static void run(Smem& sm, const K* kin, const uint32_t* vin, K* kout,
                                              uint32_t* vout, uint32_t lo, uint32_t len, int rounds) {
-    uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
-    auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return sm.cnt[a]; };
-    auto cst = [&](uint32_t a, uint32_t v) {
-      if constexpr (C16) c16[a] = static_cast<uint16_t>(v); else sm.cnt[a] = v;
-    };
-    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
     K k[I];
-    uint32_t v[PAIRS ? I : 1];
+    Vals v;
+    load(k, v, kin, vin, lo, len);
+    sort_rounds(sm, k, v, len, rounds);
+    store(sm, kout, vout, lo, len);
+  }
+  // the segment's keys (and payload) into registers, wave-striped (item j of lane l of wave w is
+  // key w*64*I + j*64 + l)
+  __device__ __forceinline__ static void load(K (&k)[I], Vals& v, const K* kin, const uint32_t* vin,
+                                              uint32_t lo, uint32_t len) {
+    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
 #pragma unroll
     for (uint32_t j = 0; j < I; ++j) {
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
       k[j] = i < len ? kin[lo + i] : K(0);
       if constexpr (PAIRS) v[j] = i < len ? vin[lo + i] : 0u;
     }
+  }
+  // `rounds` stable 8-bit rounds from the registers; the sorted segment is left in sm.sk / sm.sv
+  __device__ __forceinline__ static void sort_rounds(Smem& sm, K (&k)[I], Vals& v, uint32_t len, int rounds) {
+    uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
+    auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return sm.cnt[a]; };
+    auto cst = [&](uint32_t a, uint32_t x) {
+      if constexpr (C16) c16[a] = static_cast<uint16_t>(x); else sm.cnt[a] = x;
+    };
+    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
 #pragma unroll
     for (int pass = 0; pass < ROUNDS; ++pass) {
       if (pass >= rounds) break;   // uniform
@@ -486,7 +499,10 @@ struct LocalSort {
         }
       }
     }
-    for (uint32_t i = t; i < len; i += BLOCK) {
+  }
+  // the sorted segment from LDS to HBM, consecutive threads on consecutive keys
+  __device__ __forceinline__ static void store(Smem& sm, K* kout, uint32_t* vout, uint32_t lo, uint32_t len) {
+    for (uint32_t i = threadIdx.x; i < len; i += BLOCK) {
       kout[lo + i] = sm.sk[i];
       if constexpr (PAIRS) vout[lo + i] = sm.sv[i];
     }

@@ -23,7 +23,8 @@
 //
 // The variants measured and rejected in rounds 2-3 (XCD ranges, wide look-back, aligned or
 // nontemporal stores, ticketless tiles, other persistent schedules, phase stamps) live in
-// tools/lab_pass.hpp, which tools/lab2.hip builds; this file holds what libgrs launches.
+// the round 2-4 lab fork (git show 729d494:tools/lab_pass.hpp, removed in round 5); this file holds
+// what libgrs launches.
 #pragma once
 
 #include <type_traits>

@@ -1,11 +1,36 @@
-// lab2.hip — round-2 kernel laboratory (not part of libgrs): the v4 pass (grs_pass.hpp) at
-// several tile shapes / occupancies, the round-1 ar pass, and streaming-copy ceilings.
+// lab2.hip — kernel laboratory (not part of libgrs): memory-pattern replays and emulations of
+// the pass, LDS-atomic rates, streaming-copy ceilings, the one-pass scan.  The pass kernel
+// itself is timed from the shipped source (tools/lab4.hip includes grs_pass.hpp: lab2.py's "p4"
+// variants).  The round 2-4 fork of the pass with its rejected variants (tools/lab_pass.hpp)
+// was removed in round 5; `git show 729d494:tools/lab_pass.hpp` has it.
 // Built by tools/Makefile into tools/liblab2.so; driven by tools/lab2.py on the GPU box.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
 
-#include "lab_pass.hpp"
+#include "../gpuradixsort_amd/csrc/grs_kernels.hpp"
+
+namespace grs_lab {
+// XCC id of the calling wave: HW_REG_XCC_ID (hwreg 20 on gfx940+), bits [3:0]
+__device__ __forceinline__ uint32_t xcc_id() {
+  return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (GRS_XCDS - 1);
+}
+// Per-XCD ticket heads (round 4's rejected schedule, kept for the replay's X8 mode): tile ids
+// 8 j + c are handed out by counter c in increasing j; a workgroup draws from its own XCD's
+// counter and, once that is exhausted, from the others in turn.
+__device__ __forceinline__ uint32_t draw_ticket_x8(uint32_t* ticket, uint32_t tiles) {
+  const uint32_t x = xcc_id();
+  for (uint32_t k = 0; k < GRS_XCDS; ++k) {
+    const uint32_t c = (x + k) & (GRS_XCDS - 1);
+    if (c >= tiles) continue;
+    const uint32_t cnt = (tiles - c + GRS_XCDS - 1) / GRS_XCDS;   // tiles with id = c mod 8
+    const uint32_t v = atomicAdd(ticket + c, 1u);
+    if (v < cnt) return v * GRS_XCDS + c;
+  }
+  return 0xFFFFFFFFu;   // every tile drawn
+}
+}  // namespace grs_lab
+
 
 namespace {
 
@@ -473,186 +498,6 @@ int lab2_emu_pairs(int block, int items, int aos, int lds, const void* kin, cons
   void* args[] = {&a, &b, &c, &d, &n};
   if (hipLaunchKernel(k, dim3(tiles), dim3(block), args, lds, s) != hipSuccess) return -2;
   return 0;
-}
-
-// v4 pass: kb, pairs, block, items, minw, opt
-int lab2_v4(int kb, int pairs, int block, int items, int minw, int opt, const void* in, void* out,
-            const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
-            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
-            uint32_t hist_stride, uint32_t range_tiles) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000000L + opt;
-  switch (code) {
-#define V(KB, P, B, I, M, O)                                                                   \
-  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000000L + O: {             \
-    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                               \
-    const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
-    hipLaunchKernelGGL((grs_lab::grs_onesweep_v4<KT, P != 0, 8, B, I, M, O>), dim3(tiles), dim3(B), \
-                       0, s, (const KT*)in, (KT*)out, vin, vout, n,                            \
-                       grs::RadixDigit<KT>{shift, 255u}, hist, ticket, st, st2, err,           \
-                       (const grs::RadixDigit<KT>*)nullptr, hist_stride, range_tiles);        \
-  } break;
-    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 32, 1, 528) V(32, 0, 1024, 36, 1, 304)
-    V(32, 0, 1024, 36, 1, 336) V(32, 0, 1024, 36, 1, 368) V(32, 0, 1024, 40, 1, 1296)
-    V(32, 0, 1024, 44, 1, 1296) V(32, 0, 1024, 40, 1, 1040)
-    V(32, 0, 1024, 48, 1, 1296) V(32, 0, 1024, 56, 1, 1296) V(32, 0, 1024, 62, 1, 1296)
-    V(32, 0, 768, 64, 1, 1296) V(32, 0, 768, 80, 1, 1296) V(32, 0, 512, 96, 1, 1296)
-    V(32, 0, 512, 120, 1, 1296) V(32, 0, 1024, 48, 1, 1040) V(32, 0, 1024, 48, 1, 1280)
-    V(64, 1, 1024, 11, 1, 272) V(32, 1, 1024, 17, 1, 272) V(64, 0, 1024, 17, 1, 272)
-    V(32, 1, 1024, 34, 1, 1040) V(64, 0, 1024, 34, 1, 1040) V(64, 1, 1024, 22, 1, 1040)
-    V(32, 1, 1024, 30, 1, 1040) V(64, 0, 1024, 30, 1, 1040) V(64, 1, 1024, 20, 1, 1040)
-    V(64, 1, 1024, 11, 1, 16) V(64, 0, 1024, 32, 1, 1040)
-    V(64, 0, 1024, 28, 1, 1040) V(32, 1, 1024, 26, 1, 1040) V(64, 1, 1024, 22, 1, 1024)
-    V(32, 0, 512, 96, 1, 1040) V(32, 0, 512, 112, 1, 1040) V(32, 0, 768, 64, 1, 1040)
-    V(32, 0, 768, 72, 1, 1040) V(32, 0, 512, 72, 1, 16) V(32, 0, 768, 48, 1, 16)
-    V(32, 0, 768, 56, 1, 1040) V(32, 0, 768, 60, 1, 1040) V(32, 0, 768, 64, 1, 1024)
-    V(32, 0, 640, 72, 1, 1040) V(32, 0, 896, 56, 1, 1040) V(32, 0, 768, 68, 1, 1040)
-    V(32, 1, 768, 40, 1, 1040) V(32, 1, 768, 44, 1, 1040) V(32, 1, 768, 48, 1, 1040)
-    V(32, 0, 768, 66, 1, 1040) V(32, 0, 768, 62, 1, 1040) V(32, 0, 768, 64, 1, 1048)
-    V(32, 0, 1024, 36, 1, 280)
-    V(64, 0, 768, 40, 1, 1040) V(64, 0, 768, 44, 1, 1040) V(64, 1, 768, 28, 1, 1040)
-    V(32, 0, 1024, 36, 1, 65808) V(32, 0, 1024, 36, 1, 65816) V(32, 0, 768, 64, 1, 66576)
-    V(32, 0, 768, 64, 1, 66584) V(32, 1, 1024, 17, 1, 65808) V(32, 1, 768, 40, 1, 66576)
-    V(64, 0, 1024, 17, 1, 65808) V(64, 0, 768, 44, 1, 66576)
-    V(32, 0, 1024, 36, 1, 131344) V(32, 0, 1024, 36, 1, 131352) V(32, 0, 768, 64, 1, 132112)
-    V(32, 0, 768, 64, 1, 132120) V(32, 1, 1024, 17, 1, 131344) V(64, 0, 1024, 17, 1, 131344)
-    V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1048856) V(32, 0, 768, 64, 1, 1049616)
-    V(32, 0, 768, 64, 1, 1049624) V(32, 1, 1024, 17, 1, 1048848) V(64, 0, 1024, 17, 1, 1048848)
-    V(32, 1, 768, 40, 1, 1049616)
-    V(32, 0, 1024, 48, 1, 1049872) V(32, 0, 1024, 40, 1, 1049872) V(32, 0, 768, 56, 1, 1049616)
-    V(32, 0, 768, 60, 1, 1049616) V(32, 0, 768, 48, 1, 1049616) V(32, 0, 768, 48, 1, 1040)
-    V(64, 0, 768, 44, 1, 1049616) V(64, 1, 768, 28, 1, 1049616)
-    V(32, 0, 1024, 36, 1, 256) V(32, 0, 768, 64, 1, 1032)
-    V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 2097424) V(32, 0, 1024, 36, 1, 2097432)
-    V(32, 0, 768, 64, 1, 2098192) V(32, 0, 768, 64, 1, 2098200) V(32, 1, 768, 40, 1, 2098192)
-    V(64, 0, 1024, 17, 1, 2097424)
-
-    V(32, 0, 1024, 36, 1, 1073742096) V(32, 0, 1024, 36, 1, 1073742104) V(32, 0, 768, 64, 1, 1073742864)
-    V(32, 0, 768, 64, 1, 1073742872) V(32, 1, 768, 40, 1, 1073742864) V(64, 0, 768, 44, 1, 1073742864)
-    V(32, 0, 512, 36, 2, 272) V(32, 0, 512, 32, 2, 272) V(32, 0, 512, 48, 2, 1040)
-    V(32, 0, 512, 56, 2, 1040) V(32, 0, 512, 64, 2, 1040) V(32, 0, 512, 36, 2, 280)
-    V(32, 0, 1024, 36, 1, 16777488) V(32, 0, 1024, 36, 1, 33554704) V(32, 0, 768, 64, 1, 16778256)
-    V(32, 0, 768, 64, 1, 33555472) V(32, 1, 768, 40, 1, 16778256) V(32, 1, 768, 40, 1, 33555472)
-    V(64, 0, 768, 44, 1, 16778256) V(64, 0, 768, 44, 1, 33555472)
-    V(32, 0, 1024, 36, 1, 134217984 + 16) V(32, 0, 1024, 36, 1, 134217984 + 24)
-    V(32, 0, 768, 64, 1, 134217728 + 1040) V(32, 0, 768, 64, 1, 134217728 + 1048)
-    V(32, 0, 1024, 36, 1, 4194576) V(32, 0, 1024, 36, 1, 4194584) V(32, 0, 768, 64, 1, 4195344)
-    V(32, 0, 768, 64, 1, 4195352) V(32, 1, 768, 40, 1, 4195344) V(64, 0, 768, 44, 1, 4195344)
-    V(32, 0, 1024, 36, 1, 276) V(32, 0, 1024, 36, 1, 284)
-#undef V
-    default:
-      return -1;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// v6 (persistent, next-tile prefetch): kb, pairs, block, items, minw, opt, grid
-int lab2_v6(int kb, int pairs, int block, int items, int minw, int opt, int grid, const void* in,
-            void* out, const uint32_t* vin, uint32_t* vout, uint32_t n, const uint32_t* hist,
-            uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err, int shift, void* stream,
-            uint32_t hist_stride, uint32_t range_tiles) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = (((((long)kb * 2 + pairs) * 10000 + block) * 1000 + items) * 10 + minw) * 10000000L + opt;
-  switch (code) {
-#define V(KB, P, B, I, M, O)                                                                    \
-  case (((((long)KB * 2 + P) * 10000 + B) * 1000 + I) * 10 + M) * 10000000L + O: {              \
-    using KT = std::conditional_t<KB == 32, uint32_t, uint64_t>;                                \
-    const uint32_t tiles = (n + B * I - 1) / (B * I);                                           \
-    const uint32_t g = std::min<uint32_t>(tiles, grid > 0 ? grid : 256);                        \
-    hipLaunchKernelGGL((grs_lab::grs_onesweep_v6<KT, P != 0, 8, B, I, M, O>), dim3(g), dim3(B), 0,   \
-                       s, (const KT*)in, (KT*)out, vin, vout, n, grs::RadixDigit<KT>{shift, 255u}, \
-                       hist, ticket, st, st2, err, (const grs::RadixDigit<KT>*)nullptr,         \
-                       hist_stride, range_tiles);                                               \
-  } break;
-    V(32, 0, 1024, 36, 1, 256) V(32, 0, 1024, 36, 1, 264) V(32, 0, 1024, 36, 1, 288)
-    V(64, 1, 1024, 11, 1, 256) V(32, 1, 1024, 17, 1, 256) V(64, 0, 1024, 17, 1, 256)
-    V(32, 0, 768, 64, 1, 1040) V(32, 0, 768, 64, 1, 1048) V(32, 0, 768, 64, 1, 1024)
-    V(32, 0, 768, 60, 1, 1040) V(32, 0, 1024, 36, 1, 65792)
-    V(32, 0, 1024, 36, 1, 272) V(32, 0, 1024, 36, 1, 280) V(32, 0, 1024, 36, 1, 262416)
-    V(32, 0, 1024, 36, 1, 262424) V(32, 0, 1024, 36, 1, 524560) V(32, 0, 1024, 36, 1, 524568)
-    V(32, 0, 1024, 36, 1, 1048848) V(32, 0, 1024, 36, 1, 1573136) V(32, 0, 1024, 36, 1, 2097424)
-    V(32, 0, 768, 64, 1, 525328) V(32, 1, 1024, 17, 1, 524560) V(64, 0, 1024, 17, 1, 524560)
-    V(32, 0, 1024, 36, 1, 524544) V(32, 0, 1024, 36, 1, 524552)
-    V(32, 0, 1024, 36, 1, 277086480) V(32, 0, 1024, 36, 1, 277086488) V(32, 0, 768, 64, 1, 277087248)
-    V(32, 0, 1024, 36, 1, 8388880) V(32, 0, 1024, 36, 1, 8388888) V(32, 0, 768, 64, 1, 8389648)
-    V(32, 0, 768, 64, 1, 8389656)
-    V(32, 0, 1024, 36, 1, 526608) V(32, 0, 1024, 36, 1, 526616)
-    V(32, 0, 1024, 36, 1, 260) V(32, 0, 1024, 36, 1, 268)
-#undef V
-    default:
-      return -1;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// v6 pass at 4-bit digits: block, items, minw, opt, grid
-int lab2_v6rb4(int block, int items, int minw, int opt, int grid, const void* in, void* out,
-               uint32_t n, const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2,
-               uint32_t* err, void* stream, uint32_t hist_stride, uint32_t range_tiles) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = ((block * 1000L + items) * 10 + minw) * 100000000L + opt;
-  switch (code) {
-#define V(B, I, M, O)                                                                          \
-  case ((B * 1000L + I) * 10 + M) * 100000000L + O: {                                          \
-    const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
-    const uint32_t g = std::min<uint32_t>(tiles, grid);                                        \
-    if ((O & 2) != 0) {   /* static tiles: a cooperative launch (every workgroup resident) */   \
-      const uint32_t* a_in = (const uint32_t*)in; uint32_t* a_out = (uint32_t*)out;           \
-      const uint32_t* a_vin = nullptr; uint32_t* a_vout = nullptr; uint32_t a_n = n;          \
-      grs::RadixDigit<uint32_t> a_dig{0, 15u};                                                 \
-      const grs::RadixDigit<uint32_t>* a_dd = nullptr;                                         \
-      void* args[] = {&a_in, &a_out, &a_vin, &a_vout, &a_n, &a_dig, &hist, &ticket, &st, &st2, \
-                      &err, &a_dd, &hist_stride, &range_tiles};                                \
-      if (hipLaunchCooperativeKernel(                                                          \
-              reinterpret_cast<const void*>(&grs_lab::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), \
-              dim3(g), dim3(B), args, 0, s) != hipSuccess)                                     \
-        return -3;                                                                             \
-    } else {                                                                                   \
-      hipLaunchKernelGGL((grs_lab::grs_onesweep_v6<uint32_t, false, 4, B, I, M, O>), dim3(g),       \
-                         dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
-                         grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,        \
-                         (const grs::RadixDigit<uint32_t>*)nullptr, hist_stride, range_tiles); \
-    }                                                                                          \
-  } break;
-    V(1024, 32, 1, 0) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(512, 16, 2, 0) V(256, 32, 4, 0)
-    V(1024, 32, 1, 8) V(1024, 32, 1, 512) V(1024, 32, 1, 520) V(1024, 32, 1, 528)
-    V(1024, 32, 1, 2097152) V(1024, 32, 1, 2097160) V(1024, 32, 1, 2097168)
-    V(1024, 32, 1, 1048576) V(1024, 32, 1, 1048584)
-    V(1024, 32, 1, 524288) V(1024, 32, 1, 524296) V(512, 32, 2, 524288) V(512, 32, 2, 8)
-    V(1024, 32, 1, 64) V(1024, 32, 1, 72) V(1024, 32, 1, 16777216) V(1024, 32, 1, 33554432)
-    V(1024, 32, 1, 134217728) V(1024, 32, 1, 134217736) V(1024, 32, 1, 2) V(1024, 32, 1, 10)
-    V(1024, 32, 1, 67108864) V(1024, 32, 1, 67108872) V(1024, 32, 1, 67108880)
-#undef V
-    default:
-      return -1;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// v4 pass at 4-bit digits (BASELINE C2): block, items, minw, opt
-int lab2_v4rb4(int block, int items, int minw, int opt, const void* in, void* out, uint32_t n,
-               const uint32_t* hist, uint32_t* ticket, uint32_t* st, uint32_t* st2, uint32_t* err,
-               void* stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const long code = ((block * 1000L + items) * 10 + minw) * 1000 + opt;
-  switch (code) {
-#define V(B, I, M, O)                                                                          \
-  case ((B * 1000L + I) * 10 + M) * 1000 + O: {                                                \
-    const uint32_t tiles = (n + B * I - 1) / (B * I);                                          \
-    hipLaunchKernelGGL((grs_lab::grs_onesweep_v4<uint32_t, false, 4, B, I, M, O>), dim3(tiles),     \
-                       dim3(B), 0, s, (const uint32_t*)in, (uint32_t*)out, nullptr, nullptr, n, \
-                       grs::RadixDigit<uint32_t>{0, 15u}, hist, ticket, st, st2, err,          \
-                       (const grs::RadixDigit<uint32_t>*)nullptr);                             \
-  } break;
-    V(1024, 32, 1, 0) V(1024, 32, 1, 16) V(512, 32, 2, 0) V(1024, 16, 1, 0) V(1024, 32, 1, 8)
-    V(1024, 32, 1, 24) V(1024, 32, 1, 64) V(1024, 32, 1, 72)
-    V(1024, 64, 1, 1024) V(1024, 64, 1, 1040) V(1024, 64, 1, 1032) V(768, 84, 1, 1024)
-    V(512, 128, 1, 1024) V(512, 128, 1, 1040) V(512, 128, 1, 1032)
-#undef V
-    default:
-      return -1;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // copy / read ceilings: kind 0 = copy, 1 = read; unroll 1/4/8; grid

@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 27)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--variants", default="v4:32:0:256:72:2:0")
+    ap.add_argument("--variants", default="p4:32:0:1024:36:1:272")
     ap.add_argument("--copy", action="store_true")
     ap.add_argument("--lds-atomic", action="store_true", help="returning ds_add rate by address multiplicity")
     ap.add_argument("--rot", type=int, default=0, help="OPT 2048 store-sweep rotation per tile (keys)")
@@ -92,6 +92,9 @@ def main():
             stride = 256
         args = (P(keys), P(out), P(vin), P(vout), ctypes.c_uint32(n), P(hist), P(ticket), P(st),
                 P(st2), P(err), 0, sp, ctypes.c_uint32(stride), ctypes.c_uint32(rtiles))
+        if kind in ("r4", "r6", "v4", "v6"):
+            raise SystemExit(f"variant kind {kind}: the lab fork of the pass was removed in round 5 "
+                             "(git show 729d494:tools/lab_pass.hpp); p4 = the shipped kernel")
         if kind == "r4":   # r4:32:0:block:items:minw:opt  (4-bit digits, low nibble)
             rc = L.lab2_v4rb4(block, items, v[5], v[6], P(keys), P(out), ctypes.c_uint32(n),
                               P(hist4[kb]), P(ticket), P(st), P(st2), P(err), sp)

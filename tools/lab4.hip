@@ -1,6 +1,6 @@
 // lab4.hip — round-4 laboratory for the SHIPPED pass kernel (gpuradixsort_amd/csrc/grs_pass.hpp):
-// the library's tile shapes with candidate OPT bits, timed by tools/lab2.py ("p4" variants)
-// beside the round-3 lab copy (tools/lab_pass.hpp via lab2.hip).  Not part of libgrs.
+// the library's tile shapes with candidate OPT bits, timed by tools/lab2.py ("p4" variants).
+// Not part of libgrs.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
