@@ -64,7 +64,7 @@ OPTIONS = {
     "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
     "merge": (9, {"rounds": 0, "kway": 1}),
     "fault_tile": (10, {"off": -1}),   # test hook: tile v of every pass never publishes
-    "msd": (11, {"size": -1, "never": 0, "always": 1}),
+    "msd": (11, {"size": -1, "never": 0, "always": 1, "exact_p2": 2}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares

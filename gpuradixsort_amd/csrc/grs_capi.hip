@@ -305,8 +305,11 @@ struct grs_sorter {
   int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
-  int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies
+  int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
+                                   // 2 = 1 with P2's regions refused (test hook: the exact redo)
   void* msd_buf = nullptr;         // the MSD sort's tables (u32 keys without payload, 8-bit)
+  void* alt2_keys = nullptr;       // the MSD sort's P2 regions (keys | payload)
+  uint32_t* alt2_vals = nullptr;
   size_t msd_bytes = 0;
 };
 
@@ -352,6 +355,7 @@ void grs_destroy(grs_sorter* s) {
   if (s->xrbuf) (void)hipFree(s->xrbuf);
   if (s->codec_buf) (void)hipFree(s->codec_buf);
   if (s->msd_buf) (void)hipFree(s->msd_buf);
+  if (s->alt2_keys) (void)hipFree(s->alt2_keys);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   for (hipEvent_t e : s->xev)
@@ -412,7 +416,8 @@ static_assert(BigTile<uint32_t, true>::TILE == kMsdTileMin && BigTile<uint64_t, 
               BigTile<uint32_t, false>::TILE > kMsdTileMin, "MSD table sizing");
 
 struct MsdLayout {   // word offsets into msd_buf
-  size_t h2, big, mid, dstart, tab, hdr2, rec2, hdrf, recf, bstart, blen, brow, rows, spill, words;
+  size_t h2, h2x, h2s, big, spill2, mid, clear, dstart, reg, room, len2, in2, out2, tab, hdr2, rec2, hdr2r, rec2r,
+      hdrf, recf, bin, bstart, blen, brow, rows, spill, words;
   size_t r2, rf, bl, mr;   // capacities: P2 records, fallback records, big list, histogram rows
   // nd: digits of the fallback (2 for u32 keys, 6 for u64)
   static MsdLayout of(size_t cap, size_t nd) {
@@ -424,16 +429,29 @@ struct MsdLayout {   // word offsets into msd_buf
     L.rf = cap / kMsdTileMin + L.bl + 1;
     size_t o = 0;
     auto take = [&](size_t w) { const size_t at = o; o += (w + 63) & ~static_cast<size_t>(63); return at; };
-    // h2 | big counters | mid list (its count zeroed with h2 by the sample kernel)
-    L.h2 = take(65536 + 64 + 2 + 2 * 65536);
-    L.big = L.h2 + 65536;
-    L.mid = L.h2 + 65536 + 64;
+    // h2 (P2's digit totals) | h2x (exact counts, after a P2 spill) | h2s (sampled counts) |
+    // big counters, P2's spill flag | mid list: the first `clear` words zeroed by the sample kernel
+    L.h2 = take(3 * 65536 + 64 + 2 + 3 * 65536);
+    L.h2x = L.h2 + 65536;
+    L.h2s = L.h2 + 2 * 65536;
+    L.big = L.h2 + 3 * 65536;
+    L.spill2 = L.big + 8;
+    L.mid = L.big + 64;
+    L.clear = 3 * 65536 + 64 + 2;
     L.dstart = take(65536);
+    L.reg = take(65536);
+    L.room = take(256);
+    L.len2 = take(65536);
+    L.in2 = take(65536);
+    L.out2 = take(65536);
     L.tab = take(4 * 257);
     L.hdr2 = take(4);
     L.rec2 = take(L.r2 * 8);
+    L.hdr2r = take(4);
+    L.rec2r = take(L.r2 * 8);
     L.hdrf = take(4);
     L.recf = take(L.rf * 8);
+    L.bin = take(L.bl);
     L.bstart = take(L.bl);
     L.blen = take(L.bl);
     L.brow = take(L.bl);
@@ -456,6 +474,9 @@ struct MsdLayout {   // word offsets into msd_buf
 // Elements of the sorter's second buffer (per array) for an MSD sorter: P1 writes its runs
 // into sampled regions (n + n/8 + 256 x 4096 + 256 elements at most, grs_msd.hpp).
 size_t msd_alt_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 8 + 256 * 4096 + 1024; }
+// Elements of the third buffer (per array): P2 writes its runs into regions sized from a sample
+// of P1's output (grs_msd_plan3: at most this many, else the exact path runs).
+size_t msd_alt2_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 4 + 65536 * 64 + 1024; }
 
 bool msd_type(const grs_sorter* s) {
   return s->radix_bits == 8 && !(s->key_type == GRS_KEY_U64 && s->pairs);
@@ -553,7 +574,7 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       s->merge_mode = value;
       break;
     case GRS_OPT_MSD:
-      if (value < -1 || value > 1) return bad();
+      if (value < -1 || value > 2) return bad();
       s->msd_mode = value;
       break;
 
@@ -657,6 +678,9 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   if (msd_type(s)) {
     s->msd_bytes = MsdLayout::of(cap, msd_digits(s)).words * 4;
     alloc(&s->msd_buf, s->msd_bytes);
+    const size_t w2 = msd_alt2_words(cap);
+    alloc(&s->alt2_keys, w2 * (kb + (s->pairs ? 4 : 0)));
+    if (st == GRS_OK && s->pairs) s->alt2_vals = reinterpret_cast<uint32_t*>(static_cast<char*>(s->alt2_keys) + w2 * kb);
   }
   alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
   alloc(reinterpret_cast<void**>(&s->ctrl2), GRS_CTRL_ERROR * 4);
@@ -967,7 +991,7 @@ bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
   const int kbits = s->key_type == GRS_KEY_U64 ? 64 : 32;
   const size_t elem = kbits / 8 + (s->pairs ? 4 : 0);
   if (begin_bit != 0 || end_bit != kbits || msd_local_shape(n, elem) == 0) return false;
-  return s->msd_mode == 1 || n >= kMsdMinN;
+  return s->msd_mode >= 1 || n >= kMsdMinN;
 }
 
 // sample -> P1 (regions) -> [redo] -> P2's plan -> H2 -> P2 -> P3 -> fallback (plan,
@@ -1043,7 +1067,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // sample: the top byte's histogram; zeroes P1's status, the next call's control block, h2
   // and the big-segment counters
   hipLaunchKernelGGL((grs::grs_msd_sample<K>), dim3(1024), dim3(256), 0, stream, src, n, samp, st[0],
-                     static_cast<uint32_t>(words1), hist_next, h2, 65536u + 64u + 2u);
+                     static_cast<uint32_t>(words1), hist_next, h2, static_cast<uint32_t>(L.clear));
   GRS_HIP(hipGetLastError());
   s->cb_i ^= 1;
   if ((r = mark()) != GRS_OK) return r;
@@ -1075,14 +1099,28 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
                      exact, 256u, tickets + 15 * GRS_XCDS, st[0], st[1], err, nullptr);
   GRS_HIP(hipGetLastError());
   if ((r = mark()) != GRS_OK) return r;
-  // P2's plan (the bucket table: P1's regions, or the redo's exact layout), then H2: byte-2
-  // histogram per top-byte bucket over alt; zeroes P2's status
+  // P2's plans (the bucket table: P1's regions, or the redo's exact layout): the exact one for
+  // the rare redo below, then H2 over a 1/2^k sample of P1's output and the region plan from it
+  // (grs_msd_plan3); zeroes P2's status
+  uint32_t* const tab = mb + L.tab;
+  uint32_t* const spill2 = mb + L.spill2;
+  uint32_t* const h2x = mb + L.h2x;
+  uint32_t* const reg = mb + L.reg;
+  uint32_t* const hdr2r = mb + L.hdr2r;
+  auto* const rec2r = reinterpret_cast<grs::SegTile*>(mb + L.rec2r);
+  K* const rk = static_cast<K*>(s->alt2_keys);
+  uint32_t* const rv = PAIRS ? s->alt2_vals : nullptr;
+  // H2 chunks: ~8 rounds of the resident blocks (2 per CU), 32K to 256K keys; the sample: one
+  // 64-key piece in 2^k, k so that a uniform 16-bit bin still gets ~1000 sampled keys
+  uint32_t chunk = GRS_H2_CHUNK;
+  while (chunk > 32768u && static_cast<uint64_t>(n) / chunk < 16u * static_cast<uint64_t>(std::max(1, s->cus)))
+    chunk >>= 1;
+  uint32_t shift = 0;
+  while (shift < 3 && (static_cast<uint64_t>(n) >> (shift + 1)) >= 65536ull * 1024) ++shift;
+  chunk = std::min<uint32_t>(chunk << shift, 1u << 20);   // sampled: about as many keys a block
+  // the region buffer's room (option msd = 2, a test hook: none, so the exact redo runs)
+  const uint64_t cap2 = s->msd_mode == 2 ? 0 : static_cast<uint64_t>(msd_alt2_words(s->capacity));
   {
-    uint32_t* const tab = mb + L.tab;
-    // H2 chunks: ~8 rounds of the resident blocks (2 per CU), 32K to 256K keys
-    uint32_t chunk = GRS_H2_CHUNK;
-    while (chunk > 32768u && static_cast<uint64_t>(n) / chunk < 16u * static_cast<uint64_t>(std::max(1, s->cus)))
-      chunk >>= 1;
     if (xl)
       hipLaunchKernelGGL((grs::grs_msd_plan2<XL::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
                          totals, exact, chunk, tab, rec2, hdr2);
@@ -1091,43 +1129,85 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
                          totals, exact, chunk, tab, rec2, hdr2);
     GRS_HIP(hipGetLastError());
     hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
-                       h2, st[1], static_cast<uint32_t>(words2), tab, chunk);
+                       shift ? mb + L.h2s : h2x, st[1], static_cast<uint32_t>(words2), tab, chunk, shift,
+                       (const uint32_t*)nullptr);
     GRS_HIP(hipGetLastError());
+    if (shift) {
+      uint32_t* const room = mb + L.room;
+      hipLaunchKernelGGL(grs::grs_msd_regions, dim3(256), dim3(256), 0, stream, tab, mb + L.h2s, reg, room);
+      GRS_HIP(hipGetLastError());
+      if (xl)
+        hipLaunchKernelGGL((grs::grs_msd_plan3<XL::TILE>), dim3(1), dim3(1024), 0, stream, tab, room, cap2,
+                           rec2r, hdr2r, spill2);
+      else
+        hipLaunchKernelGGL((grs::grs_msd_plan3<Big::TILE>), dim3(1), dim3(1024), 0, stream, tab, room, cap2,
+                           rec2r, hdr2r, spill2);
+      GRS_HIP(hipGetLastError());
+    }
   }
   if ((r = mark()) != GRS_OK) return r;
-  // P2: stable scatter by the second byte inside each top-byte bucket, alt -> keys; each
-  // bucket's first tile writes where its 256 16-bit segments start (dstart)
+  // P2: stable scatter by the second byte inside each top-byte bucket.  With a sample (large
+  // sorts): alt -> the region buffer, each 16-bit segment in its region, its first tile writing
+  // the region starts (dstart) and its last the totals (h2) and the spill flag; after a spill
+  // (or for small sorts, always) the exact pass alt -> keys from H2's exact counts (h2x).
   {
     const Dig d2{KB - 16, 255u};
     const dim3 grid(static_cast<uint32_t>(t2));
-    if (xl)
-      hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, XL::BLOCK, XL::ITEMS, XL::MINW, XL::OPT, false>),
-                         grid, dim3(XL::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2,
-                         256u, tickets + GRS_XCDS, st[1], st[0], err, dstart);
-    else
-      hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, Big::BLOCK, Big::ITEMS, Big::MINW, Big::OPT, false>),
-                         grid, dim3(Big::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2,
-                         256u, tickets + GRS_XCDS, st[1], st[0], err, dstart);
+    constexpr uint32_t RG = 131072;
+    auto go = [&](auto tshape) {
+      using T = decltype(tshape);
+      if (shift) {
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RG, false>),
+                           grid, dim3(T::BLOCK), 0, stream, alt, rk, valt, rv, d2, rec2r, hdr2r, reg, 256u,
+                           tickets + GRS_XCDS, st[1], st[0], err, dstart, h2, spill2, (const uint32_t*)nullptr);
+        GRS_HIP(hipGetLastError());
+        // the redo: exact counts, then the exact pass in place (persistent, gated by the flag)
+        hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
+                           st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2);
+        GRS_HIP(hipGetLastError());
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, true>),
+                           dim3(s->cus), dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x,
+                           256u, tickets + 14 * GRS_XCDS, st[0], st[1], err, (uint32_t*)nullptr,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, spill2);
+        GRS_HIP(hipGetLastError());
+      } else {
+        // no sample: the exact pass straight away (the flag says so to P3: in place)
+        GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(spill2), 1, 1, stream));
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, false>), grid,
+                           dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x, 256u,
+                           tickets + GRS_XCDS, st[1], st[0], err, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                           (uint32_t*)nullptr, (const uint32_t*)nullptr);
+        GRS_HIP(hipGetLastError());
+      }
+    };
+    if (xl) go(XL{});
+    else go(Big{});
+    hipLaunchKernelGGL(grs::grs_msd_starts, dim3(256), dim3(256), 0, stream, spill2, tab, h2, h2x, dstart,
+                       mb + L.len2, mb + L.in2, mb + L.out2);
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
-  // P3: every 16-bit segment sorted by the bits below its prefix in LDS, in place; longer
-  // ones listed: up to the largest LDS shape's capacity for its persistent kernel (inputs
-  // narrower than the key, e.g. a rank's range after the multi-GPU exchange), beyond that for
-  // the fallback
+  // P3: every 16-bit segment sorted by the bits below its prefix in LDS, from its region (in
+  // place after a spill) to its sorted place in keys; longer ones listed: up to the largest LDS
+  // shape's capacity for its persistent kernel (inputs narrower than the key, e.g. a rank's
+  // range after the multi-GPU exchange), beyond that for the fallback (moved to their place
+  // first: grs_msd_copy_big)
   using P3L = std::conditional_t<sizeof(K) == 4 && !PAIRS, MsdLocalC, MsdLocalB>;
   const uint32_t mid_max = P3L::SMAX > P3C::SMAX ? P3L::SMAX : P3C::SMAX;
   hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
-                     dim3(P3C::BLOCK), 0, stream, keys, vals, h2, dstart, mid_max, mb + L.mid, bigc,
-                     mb + L.bstart, mb + L.blen, mb + L.brow, rows);
+                     dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
+                     mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows);
   GRS_HIP(hipGetLastError());
   if (P3L::SMAX > P3C::SMAX) {
     constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
     constexpr int minw = per_cu * P3L::BLOCK / GRS_WAVE / 4;
     hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw>),
-                       dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, mb + L.mid);
+                       dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.mid);
     GRS_HIP(hipGetLastError());
   }
+  hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
+                     spill2, bigc, mb + L.bin, mb + L.bstart, mb + L.blen);
+  GRS_HIP(hipGetLastError());
   if ((r = mark()) != GRS_OK) return r;
   // fallback: the listed segments by a segmented LSD on the bits below the prefix
   // (keys -> alt -> ... -> keys: ND is even)

@@ -80,13 +80,15 @@ __device__ __forceinline__ void block_scan(uint32_t (&v)[NV], uint32_t* wsum, ui
 // the segment's place among the segments of several tiles: solo segments need none);
 // kSegMoved a = where each segment's keys are read, b = lengths, c = where its sorted runs go
 // (histogram row = segment index).  hdr[0] = tiles, hdr[1] = groups, hdr[2] =
-// status rows.
+// status rows.  room (nullable): the records' seg_len = room[i] instead of the segment's length
+// (a region pass: the room its runs may take).
 // lds: GRS_PLAN_LDS_WORDS words.
 template <uint32_t TILE, int BLOCK, int SRC>
 __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                                const uint32_t* __restrict__ c, uint32_t nseg,
                                uint32_t* __restrict__ spill, SegTile* __restrict__ rec,
-                               uint32_t* __restrict__ hdr, uint32_t* lds) {
+                               uint32_t* __restrict__ hdr, uint32_t* lds,
+                               const uint32_t* __restrict__ room = nullptr) {
   constexpr uint32_t G = GRS_LB_GROUP;
   const uint32_t t = threadIdx.x;
   const bool in_lds = nseg < GRS_PLAN_LDS_SEGS;
@@ -142,10 +144,11 @@ __device__ void seg_plan_block(const uint32_t* __restrict__ a, const uint32_t* _
     const uint32_t tl = tpre[lo + 1] - tpre[lo];
     const uint32_t len = sln[lo];
     const uint32_t q = j / G;
-    const uint32_t flags = (j % G) | (min(G, tl - q * G) << 4) | ((tl == 1 ? 1u : 0u) << 8) | (q << 9);
+    const uint32_t flags = (j % G) | (min(G, tl - q * G) << 4) | ((tl == 1 ? 1u : 0u) << 8) | (q << 9) |
+                           (j + 1 == tl ? 0x80000000u : 0u);
     const uint32_t out = SRC == kSegMoved ? shr[lo] : sst[lo];
     rec[tk] = SegTile{rpre[lo] + j, gpre[lo] + q, flags, sst[lo] + j * TILE, min(TILE, len - j * TILE),
-                      out, len, SRC == kSegMoved ? lo : shr[lo]};
+                      out, room != nullptr ? room[lo] : len, SRC == kSegMoved ? lo : shr[lo]};
   }
   if (t == 0) {
     hdr[0] = tiles;
@@ -327,12 +330,15 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
                                                          uint32_t* __restrict__ h2,
                                                          uint32_t* __restrict__ zero,
                                                          uint32_t zero_words,
-                                                         const uint32_t* __restrict__ tab, uint32_t chunk) {
+                                                         const uint32_t* __restrict__ tab, uint32_t chunk,
+                                                         uint32_t sample_shift = 0,
+                                                         const uint32_t* __restrict__ gate = nullptr) {
   constexpr uint32_t B = 1024;
   constexpr uint32_t LW = 256 * GRS_H2_COPIES;
   __shared__ __attribute__((aligned(16))) uint32_t h[LW];
   __shared__ uint32_t cpre[257];
   const uint32_t t = threadIdx.x;
+  if (gate != nullptr && __builtin_amdgcn_readfirstlane(*gate) == 0u) return;   // (the exact redo)
   for (uint32_t i = blockIdx.x * B + t; i < zero_words; i += gridDim.x * B) zero[i] = 0;
   for (uint32_t i = t; i < LW; i += B) h[i] = 0;
   if (t < 257) cpre[t] = tab[3 * 257 + t];
@@ -357,7 +363,6 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   // 16-B loads from the first aligned key on
   const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(kc) & 15u) / sizeof(K);
   const uint32_t head = min(cl, (VEC - mis) % VEC);
-  if (t < head) count(kc[t]);
   const uint32_t nv = (cl - head) / VEC;
   const uint4* kv = reinterpret_cast<const uint4*>(kc + head);
   auto count4 = [&](const uint4& x) {
@@ -365,6 +370,27 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
 #pragma unroll
     for (uint32_t q = 0; q < VEC; ++q) count(e[q]);
   };
+  if (sample_shift != 0) {
+    // a sample: the first of every 2^sample_shift 64-key pieces (whatever the input order, the
+    // pieces cover the chunk evenly); the bucket's scale is its length over its sampled keys
+    constexpr uint32_t PU = 64 / VEC;   // 16-B loads per piece
+    const uint32_t np = (nv + PU - 1) / PU;
+    const uint32_t ns = ((np + (1u << sample_shift) - 1) >> sample_shift) * PU;
+    for (uint32_t m = t; m < ns; m += B) {
+      const uint32_t v = ((m / PU) << sample_shift) * PU + m % PU;
+      if (v < nv) count4(kv[v]);
+    }
+    __syncthreads();
+    if (t < 256) {
+      const uint32_t* row = h + t * GRS_H2_COPIES;
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
+      if (c != 0) atomicAdd(&h2[s * 256 + t], c);
+    }
+    return;
+  }
+  if (t < head) count(kc[t]);
   uint32_t i = t;
   for (; i + 3 * B < nv; i += 4 * B) {
     uint4 x[4];
@@ -382,6 +408,133 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
 #pragma unroll
     for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
     if (c != 0) atomicAdd(&h2[s * 256 + t], c);
+  }
+}
+
+// The regions of P2 (one block of 256 per top-byte bucket s, a thread per byte-2 bin b), from
+// the sampled byte-2 counts hs (H2 with a sample_shift) so that P2 needs no counting read of
+// P1's output: the region of bin (s, b) holds its estimate c * scale (scale = the bucket's
+// length over its sampled keys) + 6 standard errors (scale * sqrt(c + 1)) + 64, at most the
+// bucket's length (a bucket with no sampled key: every bin its length).  reg[s * 256 + b] = the
+// region (P2's "histogram" rows), room[s] = the bucket's total.
+__global__ __launch_bounds__(256) void grs_msd_regions(const uint32_t* __restrict__ tab,
+                                                       const uint32_t* __restrict__ hs,
+                                                       uint32_t* __restrict__ reg, uint32_t* __restrict__ room) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t s = blockIdx.x, t = threadIdx.x;
+  const uint32_t c = hs[s * 256 + t];
+  uint32_t v[1] = {c}, ts[1];
+  block_scan<256, 1>(v, wsum, ts);
+  const uint32_t L = tab[257 + s];
+  uint32_t r = L;
+  if (ts[0] != 0u) {
+    const float scale = static_cast<float>(L) / static_cast<float>(ts[0]);
+    const float e = static_cast<float>(c) * scale + 6.0f * scale * sqrtf(static_cast<float>(c) + 1.0f) + 64.0f;
+    r = e < static_cast<float>(L) ? static_cast<uint32_t>(e) : L;
+  }
+  reg[s * 256 + t] = r;
+  // the bucket's total in 64 bits: past 2^31 it is reported as 2^32 - 1, which no region buffer
+  // holds, so the exact path runs (each region stays below 2^32, and so does every prefix P2's
+  // tiles take over a bucket's regions)
+  __shared__ uint64_t part[4];
+  uint64_t r64 = r;
+  for (int o = 32; o > 0; o >>= 1) r64 += __shfl_xor(r64, o);
+  if ((t & 63u) == 0) part[t >> 6] = r64;
+  __syncthreads();
+  if (t == 0) {
+    const uint64_t all = part[0] + part[1] + part[2] + part[3];
+    room[s] = all >= (uint64_t(1) << 31) ? 0xFFFFFFFFu : static_cast<uint32_t>(all);
+  }
+}
+
+// The region plan of P2 (one block): the regions laid out bucket by bucket in the region buffer
+// (cap2 elements) and P2's tiles planned with seg_len = room[s] (rec / hdr).  Regions past cap2:
+// no tiles (hdr[0] = 0) and *spill = 1, so the exact path runs instead.
+template <uint32_t TILE2>
+__global__ __launch_bounds__(1024) void grs_msd_plan3(const uint32_t* __restrict__ tab,
+                                                      const uint32_t* __restrict__ room_g, uint64_t cap2,
+                                                      SegTile* __restrict__ rec, uint32_t* __restrict__ hdr,
+                                                      uint32_t* __restrict__ spill) {
+  __shared__ uint32_t lds[GRS_PLAN_LDS_WORDS + 4 * 257 + 64];
+  uint32_t* const in = lds + GRS_PLAN_LDS_WORDS;
+  uint32_t* const len = in + 257;
+  uint32_t* const out = len + 257;
+  uint32_t* const room = out + 257;
+  uint32_t* const wsum = room + 257;
+  const uint32_t t = threadIdx.x;
+  uint64_t r64 = 0;
+  if (t < 256) {
+    in[t] = tab[t];
+    len[t] = tab[257 + t];
+    room[t] = room_g[t];
+    r64 = room[t];
+  }
+  // the layout's total in 64 bits (a wave sum per wave, then thread 0)
+  for (int o = 32; o > 0; o >>= 1) r64 += __shfl_xor(r64, o);
+  __shared__ uint64_t wtot[16];
+  if ((t & 63u) == 0) wtot[t >> 6] = r64;
+  uint32_t v[1] = {t < 256 ? room[t] : 0u}, tot[1];
+  block_scan<1024, 1>(v, wsum, tot);
+  if (t < 256) out[t] = v[0];
+  uint64_t all = 0;
+  for (int k = 0; k < 16; ++k) all += wtot[k];
+  __syncthreads();
+  if (all > cap2 || all >= (uint64_t(1) << 32)) {
+    if (t == 0) {
+      hdr[0] = 0;
+      hdr[1] = 0;
+      hdr[2] = 0;
+      *spill = 1u;
+    }
+    return;
+  }
+  seg_plan_block<TILE2, 1024, kSegMoved>(in, len, out, 256u, nullptr, rec, hdr, lds, room);
+}
+
+// The 16-bit segments for P3 after P2: without a spill (*spill == 0) the lengths are the
+// region P2's digit totals (rtot) and each segment is read from its region start (rstart, in
+// the region buffer); after a spill, the exact pass's counts (xcnt), in place.  out = where each
+// sorted segment goes: its bucket's exact start (tab's out, grs_msd_plan2) + the lengths of
+// the bucket's earlier segments.  One block of 256 per top-byte bucket.
+__global__ __launch_bounds__(256) void grs_msd_starts(const uint32_t* __restrict__ spill,
+                                                      const uint32_t* __restrict__ tab,
+                                                      const uint32_t* __restrict__ rtot,
+                                                      const uint32_t* __restrict__ xcnt,
+                                                      const uint32_t* __restrict__ rstart,
+                                                      uint32_t* __restrict__ len2, uint32_t* __restrict__ in2,
+                                                      uint32_t* __restrict__ out2) {
+  __shared__ uint32_t wsum[4];
+  const bool sp = *spill != 0u;
+  const uint32_t s = blockIdx.x, t = threadIdx.x, b = s * 256 + t;
+  const uint32_t l = sp ? xcnt[b] : rtot[b];
+  uint32_t v[1] = {l}, tot[1];
+  block_scan<256, 1>(v, wsum, tot);
+  const uint32_t o = tab[2 * 257 + s] + v[0];
+  len2[b] = l;
+  out2[b] = o;
+  in2[b] = sp ? o : rstart[b];
+}
+
+// The big-list segments of P3 (longer than any LDS shape) from the region buffer into the
+// caller's arrays at their sorted place, for the in-place fallback (persistent grid, every
+// block on every entry; leaves at once without entries or after a spill, whose exact pass
+// already wrote the caller's arrays).
+template <typename K, bool PAIRS>
+__global__ __launch_bounds__(256) void grs_msd_copy_big(const K* __restrict__ rk, const uint32_t* __restrict__ rv,
+                                                        K* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ spill,
+                                                        const uint32_t* __restrict__ big,
+                                                        const uint32_t* __restrict__ big_in,
+                                                        const uint32_t* __restrict__ big_out,
+                                                        const uint32_t* __restrict__ big_len) {
+  if (*spill != 0u) return;
+  const uint32_t count = big[0];
+  for (uint32_t e = 0; e < count; ++e) {
+    const uint32_t a = big_in[e], o = big_out[e], n = big_len[e];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+      keys[o + i] = rk[a + i];
+      if constexpr (PAIRS) vals[o + i] = rv[a + i];
+    }
   }
 }
 
@@ -509,18 +662,25 @@ struct LocalSort {
   }
 };
 
-// P3: one workgroup per 16-bit prefix b (grid 65536): its len = h2[b] keys (and payload) at
-// dstart[b] (P2's digit starts) sorted in LDS (LocalSort).  Longer segments are listed: up to
-// MID keys in the mid list (mid[0] = count, mid_start / mid_len) for grs_msd_local_list's
-// larger shape, longer ones in the big list for the segmented LSD: big[0] counts them, big[1]
-// counts those longer than one fallback tile (TILEF keys), which get a histogram row (ND
-// digits) zeroed here; big_start / big_len / big_row hold (start, length, row) per entry.
+// P3: one workgroup per 16-bit prefix b (grid 65536): its len2[b] keys (and payload), read at
+// in2[b] of the region buffer (rk / rv) -- or, after a P2 spill, of the caller's arrays, in
+// place -- sorted in LDS (LocalSort) and written to out2[b] of the caller's arrays
+// (grs_msd_starts).  Longer segments are listed: up to MID keys in the mid list (mid[0] =
+// count, (in, out, len) from mid[2] on) for grs_msd_local_list's larger shape, longer ones in
+// the big list for the segmented LSD in place (grs_msd_copy_big moves them first): big[0] counts
+// them, big[1] counts those longer than one fallback tile (TILEF keys), which get a histogram
+// row (ND digits) zeroed here; big_in / big_start / big_len / big_row hold (region start,
+// sorted start, length, row) per entry.
 template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF>
 __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                       const uint32_t* __restrict__ h2,
-                                                       const uint32_t* __restrict__ dstart,
+                                                       const K* __restrict__ rk, const uint32_t* __restrict__ rv,
+                                                       const uint32_t* __restrict__ spill,
+                                                       const uint32_t* __restrict__ len2,
+                                                       const uint32_t* __restrict__ in2,
+                                                       const uint32_t* __restrict__ out2,
                                                        uint32_t mid_max, uint32_t* __restrict__ mid,
                                                        uint32_t* __restrict__ big,
+                                                       uint32_t* __restrict__ big_in,
                                                        uint32_t* __restrict__ big_start,
                                                        uint32_t* __restrict__ big_len,
                                                        uint32_t* __restrict__ big_row,
@@ -529,22 +689,34 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
   constexpr uint32_t ND = LS::ROUNDS;   // fallback digits (histogram row of ND x 256 words)
   __shared__ typename LS::Smem sm;
   const uint32_t t = threadIdx.x;
-  const uint32_t len = h2[blockIdx.x];
-  if (len <= 1) return;   // (the start of an empty segment was never written)
-  const uint32_t lo = dstart[blockIdx.x];
+  const uint32_t len = len2[blockIdx.x];
+  if (len == 0u) return;   // (the start of an empty segment was never written)
+  const bool inplace = __builtin_amdgcn_readfirstlane(*spill) != 0u;
+  const uint32_t lo = in2[blockIdx.x], o = out2[blockIdx.x];
+  const K* const kin = inplace ? keys : rk;
+  const uint32_t* const vin = inplace ? vals : rv;
+  if (len == 1u) {
+    if (!inplace && t == 0) {
+      keys[o] = kin[lo];
+      if constexpr (PAIRS) vals[o] = vin[lo];
+    }
+    return;
+  }
   if (len > LS::SMAX) {
     if (len <= mid_max) {   // the mid list (a larger LDS shape)
       if (t == 0) {
         const uint32_t e = atomicAdd(&mid[0], 1u);
-        mid[2 + 2 * e] = lo;
-        mid[3 + 2 * e] = len;
+        mid[2 + 3 * e] = lo;
+        mid[3 + 3 * e] = o;
+        mid[4 + 3 * e] = len;
       }
       return;
     }
     if (t == 0) {
       const uint32_t e = atomicAdd(&big[0], 1u);
       const uint32_t row = len > TILEF ? atomicAdd(&big[1], 1u) : 0xFFFFFFFFu;
-      big_start[e] = lo;
+      big_in[e] = lo;
+      big_start[e] = o;
       big_len[e] = len;
       big_row[e] = row;
       sm.slot = row;
@@ -554,7 +726,7 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
       for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(sm.slot) * ND * 256 + i] = 0;
     return;
   }
-  LS::run(sm, keys, vals, lo, len);
+  LS::run(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, 0u, len, LS::ROUNDS);
 }
 
 // P3's second shape: the mid list's segments (persistent grid, a segment per workgroup in
@@ -563,12 +735,20 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
 template <typename K, bool PAIRS, int BLOCK, int I, bool C16, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict__ keys,
                                                             uint32_t* __restrict__ vals,
+                                                            const K* __restrict__ rk,
+                                                            const uint32_t* __restrict__ rv,
+                                                            const uint32_t* __restrict__ spill,
                                                             const uint32_t* __restrict__ mid) {
   using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
   __shared__ typename LS::Smem sm;
   const uint32_t count = mid[0];
+  if (count == 0u) return;
+  const bool inplace = *spill != 0u;
+  const K* const kin = inplace ? keys : rk;
+  const uint32_t* const vin = inplace ? vals : rv;
   for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
-    LS::run(sm, keys, vals, mid[2 + 2 * e], mid[3 + 2 * e]);
+    const uint32_t lo = mid[2 + 3 * e], o = mid[3 + 3 * e], len = mid[4 + 3 * e];
+    LS::run(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, 0u, len, LS::ROUNDS);
     __syncthreads();   // every LDS read of this segment before the next one's
   }
 }

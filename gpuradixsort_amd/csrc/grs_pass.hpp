@@ -173,16 +173,17 @@ struct TileSpan {
   uint32_t base;       // index of the tile's first key
   uint32_t valid;      // keys in the tile (<= TILE)
   uint32_t seg_start;  // first index of the tile's segment
-  uint32_t seg_len;    // keys in the segment
+  uint32_t seg_len;    // keys in the segment (region passes: the room its runs may take)
   bool solo;           // segmented pass: the segment's only tile -- no status words, no
                        // look-back, its own counts are the segment's
+  bool last;           // the segment's last tile (region passes write the digit totals)
   __device__ __forceinline__ static TileSpan whole(uint32_t tile, uint32_t n, uint32_t TILE) {
     constexpr uint32_t G = GRS_LB_GROUP;
     const uint32_t tiles = n / TILE + (n % TILE != 0u ? 1u : 0u);
     const uint32_t b = tile * TILE;
     const uint32_t g = tile / G;
     return TileSpan{tile, tiles, g, (tiles + G - 1) / G, tile % G, min(G, tiles - g * G), 0u,
-                    b, (n - b) < TILE ? (n - b) : TILE, 0u, n, false};
+                    b, (n - b) < TILE ? (n - b) : TILE, 0u, n, false, tile + 1u == tiles};
   }
 };
 
@@ -191,7 +192,8 @@ struct SegTile {
   uint32_t row;        // tile word row of the status layout (solo tiles: none)
   uint32_t group;      // look-back group of the tile
   uint32_t flags;      // place in the group (bits 0-3) | tiles of the group (4-7) | solo (8)
-                       // | the group's place in its segment (9-31)
+                       // | the group's place in its segment (9-30) | last tile of its
+                       // segment (31)
   uint32_t base;       // first key of the tile
   uint32_t valid;      // keys in the tile
   uint32_t seg_start;  // first key of the segment
@@ -315,7 +317,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF& dig, uint32_t gh,
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
     uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word, PassDebug dbg,
-    uint32_t* __restrict__ digit_starts = nullptr, uint32_t* __restrict__ region_totals = nullptr) {
+    uint32_t* __restrict__ digit_starts = nullptr, uint32_t* __restrict__ region_totals = nullptr,
+    uint32_t* __restrict__ spill_flag = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   constexpr bool C16 = (OPT & 256) != 0;
   constexpr bool MATCH = (OPT & 512) != 0;
@@ -515,13 +518,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(
              : lb.finish(status, gacc, ginc, tile, sp.jg, sp.group, sp.in_group, t, gold, publish,
                          error_word, dbg.spin_limit);
     if constexpr ((OPT & 131072) != 0) {
-      // region pass (grs_onesweep_region): gh is digit t's region, not its count; the last
-      // ticket's look-back covers every other tile, so it knows each digit's total and whether
-      // a run outgrew its region
-      if (tile + 1u == tiles) {
+      // region pass (grs_onesweep_region; grs_onesweep_seg<REGION>): gh is digit t's region,
+      // not its count; the segment's last tile's look-back covers every other tile of it, so it
+      // knows each digit's total and whether a run outgrew its region (a solo tile: its own
+      // counts, never past its region)
+      if (sp.last) {
         const uint32_t tot = prefix + publish;
         region_totals[t] = tot;
-        if (tot > gh) atomicOr(&region_totals[RADIX], 1u);
+        if (tot > gh) atomicOr(spill_flag != nullptr ? spill_flag : &region_totals[RADIX], 1u);
       }
     }
     uint32_t start = gstart + prefix;
@@ -697,7 +701,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
     const uint32_t T = spill ? n / TILEF + (n % TILEF != 0u ? 1u : 0u) : 0u;
     for (uint32_t k = t; k < T; k += BLOCK) {
       const uint32_t q = k / G;
-      const uint32_t flags = (k % G) | (min(G, T - q * G) << 4) | ((T == 1 ? 1u : 0u) << 8) | (q << 9);
+      const uint32_t flags = (k % G) | (min(G, T - q * G) << 4) | ((T == 1 ? 1u : 0u) << 8) | (q << 9) |
+                             (k + 1 == T ? 0x80000000u : 0u);
       redo_rec[k] = SegTile{k, q, flags, k * TILEF, min(TILEF, n - k * TILEF), 0u, n, 0u};
     }
     if (t == 0) {
@@ -846,11 +851,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
     uint32_t* __restrict__ vals_out, const RadixDigit<K> dig, const SegTile* __restrict__ rec,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ hist, uint32_t hist_stride,
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, uint32_t* __restrict__ digit_starts) {
+    uint32_t* __restrict__ error_word, uint32_t* __restrict__ digit_starts,
+    uint32_t* __restrict__ totals = nullptr, uint32_t* __restrict__ spill = nullptr,
+    const uint32_t* __restrict__ gate = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, RadixDigit<K>>;
   static_assert((OPT & (4096 | 8192 | 16384 | 32768)) == 0, "segmented passes move two arrays");
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
+  // gate (nullable): run only when *gate != 0 (a redo that is usually not needed)
+  if (gate != nullptr && __builtin_amdgcn_readfirstlane(*gate) == 0u) return;
   const PassDebug dbg = PassDebug::read(error_word);
   for (;;) {
     if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
@@ -860,8 +869,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
     if (tk >= hdr[0]) return;   // every workgroup leaves once it draws a ticket past the table
     const SegTile r = rec[tk];
     const bool solo = (r.flags >> 8) & 1u;
+    const uint32_t q = (r.flags >> 9) & 0x3FFFFFu;   // the group's place in its segment
     const TileSpan sp{r.row, hdr[2], r.group, hdr[1], r.flags & 15u, (r.flags >> 4) & 15u,
-                      r.group - (r.flags >> 9), r.base, r.valid, r.seg_start, r.seg_len, solo};
+                      r.group - q, r.base, r.valid, r.seg_start, r.seg_len, solo, (r.flags >> 31) != 0u};
     K key[ITEMS];
     uint32_t val[ITEMS];
     uint32_t tt = t;
@@ -871,12 +881,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
                             ? hist[static_cast<size_t>(r.seg) * hist_stride + t] : 0u;
     // the segment's first tile (place 0 of group 0; its keys may be read from elsewhere than
     // its runs go, so base == seg_start does not tell)
-    const bool first = (r.flags & 15u) == 0u && (r.flags >> 9) == 0u;
+    const bool first = (r.flags & 15u) == 0u && q == 0u;
     uint32_t* ds = digit_starts != nullptr && first
                        ? digit_starts + static_cast<size_t>(r.seg) * SM::RADIX : nullptr;
+    // region pass (OPT 131072): hist holds each digit's region, not its count; the segment's last
+    // tile writes the digit totals to totals[seg * RADIX + d] and sets *spill if one outgrew
+    uint32_t* const tot = (OPT & 131072) != 0 ? totals + static_cast<size_t>(r.seg) * SM::RADIX : nullptr;
     onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, false, true>(sm, sp, key, val, keys_in, keys_out, vals_in,
                                                    vals_out, 0u, dig, gh, ticket, status,
-                                                   status_next, error_word, dbg, ds);
+                                                   status_next, error_word, dbg, ds, tot, spill);
     if constexpr (!PERSIST) return;
     lds_barrier();   // every LDS read of the finished tile before the next ticket's reset
   }

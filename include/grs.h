@@ -153,7 +153,9 @@ typedef enum grs_option {
                                 segments too long for LDS sorted by a segmented LSD on the bits
                                 below their 16-bit prefix) instead of the LSD passes.  Also
                                 grs_sort_segmented's long segments: 0 keeps them on the segmented
-                                LSD instead of the top-byte scatter + LDS sorts */
+                                LSD instead of the top-byte scatter + LDS sorts.  2 (test hook):
+                                1, with the byte-2 scatter's sampled regions refused, so its exact
+                                redo runs */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);

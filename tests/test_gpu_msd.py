@@ -27,6 +27,10 @@ def msd_sorter(capacity, mode="always", key_bits=32, pairs=False):
     if s is None or s.capacity < capacity:
         if s is not None:
             s.close()
+            _S.pop(key)
+        for other in list(_S):   # one sorter at a time of the large ones (HBM)
+            if _S[other].capacity >= (1 << 26):
+                _S.pop(other).close()
         s = grs.RadixSorter(max(capacity, 1 << 20), key_bits=key_bits, pairs=pairs, radix_bits=8)
         s.set_option("msd", mode)
         _S[key] = s
@@ -211,6 +215,57 @@ def test_msd_typed_segment_edges_and_spill(gpu, kb, pairs):
     keys[idx] = rng.integers(0, 1 << 24, idx.size).astype(dt)
     gk, gv = run_typed(keys, gpu, pairs)
     perm = oracle.stable_argsort(keys)
+    assert np.array_equal(gk, keys[perm])
+    if pairs:
+        assert np.array_equal(gv, perm.astype(np.uint32))
+
+
+@pytest.mark.parametrize("n", [(1 << 27) + 77, 1 << 28])
+def test_msd_sampled_p2(gpu, n):
+    """Sorts large enough that H2 counts a sample of P1's output (one 64-key piece in 2 / 4) and
+    P2 scatters into regions sized from it (grs_msd_plan3), P3 reading the region buffer:
+    uniform, narrow (few top-byte buckets, long regions), few-unique and sorted keys."""
+    rng = np.random.default_rng(n)
+    cases = (("uniform", rng.integers(0, 1 << 32, n, dtype=np.uint32)),
+             ("narrow_27bit", rng.integers(0, 1 << 27, n, dtype=np.uint32)),
+             ("16_unique", rng.integers(0, 16, n).astype(np.uint32) * np.uint32(0x10001001)),
+             ("sorted", (np.arange(n, dtype=np.uint64) * 15).astype(np.uint32)))
+    for name, keys in cases:
+        k = torch.from_numpy(keys).to(gpu)
+        want = torch.sort(k.view(torch.int32).to(torch.int64) & 0xFFFFFFFF)[0].cpu().numpy()
+        got = run(keys, gpu, "always")
+        assert np.array_equal(got.astype(np.int64), want), name
+        del k
+
+
+def test_msd_p2_region_spill(gpu):
+    """A sample that misses a bin: every key in top-byte bucket 0 and, by 64-key piece of P1's
+    output, byte 2 = 0 in the sampled pieces (even ones: one in two is sampled at 2^27) and 255
+    in the others, so bin (0, 255) outgrows its region: P2's last tiles flag it, the exact
+    histogram and pass run (gated on the flag) and P3 sorts in place -- bit-exact, and the
+    sorter's next sort is too."""
+    n = 1 << 27
+    rng = np.random.default_rng(31)
+    piece = (np.arange(n, dtype=np.int64) // 64) % 2
+    keys = np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)
+    keys |= rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    got = run(keys, gpu, "always")
+    assert np.array_equal(got, np.sort(keys))
+    keys2 = rng.integers(0, 1 << 32, n, dtype=np.uint32)
+    assert np.array_equal(run(keys2, gpu, "always"), np.sort(keys2))
+
+
+@pytest.mark.parametrize("kb,pairs", [(32, False), (32, True), (64, False)])
+def test_msd_exact_p2_hook(gpu, kb, pairs):
+    """Option msd = exact_p2 (a test hook: P2's regions refused) runs the exact redo -- the gated
+    exact histogram and the persistent exact pass in place -- at a sampled size, bit-exact."""
+    n = (1 << 27) + 3
+    rng = np.random.default_rng(kb * 7 + pairs)
+    dt = np.uint32 if kb == 32 else np.uint64
+    keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+    keys[::5] = keys[0]
+    gk, gv = run_typed(keys, gpu, pairs, "exact_p2")
+    perm = np.argsort(keys, kind="stable")
     assert np.array_equal(gk, keys[perm])
     if pairs:
         assert np.array_equal(gv, perm.astype(np.uint32))
