@@ -42,7 +42,8 @@ grs_status set_err(grs_status s, const std::string& msg) {
   do {                                                                                 \
     hipError_t e_ = (call);                                                            \
     if (e_ != hipSuccess)                                                              \
-      return set_err(GRS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+      return set_err(GRS_EHIP, std::string(#call) + " (grs_capi.hip:" +                \
+                                   std::to_string(__LINE__) + "): " + hipGetErrorString(e_)); \
   } while (0)
 
 // Tile shapes of the pass (grs_onesweep_v4, grs_pass.hpp).  Measured on MI355X inside the
@@ -997,8 +998,10 @@ bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
 // sample -> P1 (regions) -> [redo] -> P2's plan -> H2 -> P2 -> P3 -> fallback (plan,
 // histograms, a segmented LSD over the bits below the prefix for the segments P3 left;
 // persistent grids that leave at once when there are none).  src_in / vsrc_in (out of place):
-// the sample and P1 read them; the result lands in keys / vals either way.
-template <typename K, bool PAIRS, typename P3C>
+// the sample and P1 read them; the result lands in keys / vals either way.  REC (u32 pairs,
+// option GRS_OPT_RECORDS != 0): P1 and P2 write 8-byte (key, value) records into the scratch and
+// the region buffer (one run per digit instead of two), H2, P2 and P3 read them.
+template <typename K, bool PAIRS, typename P3C, bool REC = false>
 grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
                    const K* src_in, const uint32_t* vsrc_in) {
   using Big = BigTile<K, PAIRS>;
@@ -1009,6 +1012,8 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   constexpr int KB = 8 * static_cast<int>(sizeof(K));
   constexpr int ND = (KB - 16) / 8;
   static_assert(!Big::TWO_ROUNDS, "u64 pairs take the LSD sort");
+  static_assert(!REC || (PAIRS && sizeof(K) == 4), "records: u32 pairs");
+  constexpr uint32_t RW = REC ? 8192 : 0, RR = REC ? 4096 : 0;   // records written / read
   constexpr uint32_t G = GRS_LB_GROUP;
   const bool big = use_big_tiles(s, n, Big::TILE);
   const bool xl = big && use_xl(s, n, XL::TILE);
@@ -1061,6 +1066,35 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   const uint64_t region_len = static_cast<uint64_t>(n) + n / 8 + 256u * pad + 256u;
   if (region_len > msd_alt_words(s->capacity)) return set_err(GRS_ECAPACITY, "internal: MSD regions");
   grs_status r;
+#ifdef GRS_DIAG
+  // diagnostic builds (tools/diag): the passes' bounds checks, reported per phase on stderr
+  auto diag_set = [&](uint64_t out_lim, uint64_t in_lim) -> grs_status {
+    const uint32_t lim[4] = {static_cast<uint32_t>(std::min<uint64_t>(out_lim, 0xFFFFFFFFu)),
+                             static_cast<uint32_t>(std::min<uint64_t>(in_lim, 0xFFFFFFFFu)),
+                             static_cast<uint32_t>(std::min<size_t>(s->status_words, 0xFFFFFFFFu)), 0u};
+    GRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(grs::diag_lim), lim, sizeof(lim), 0, hipMemcpyHostToDevice, stream));
+    return GRS_OK;
+  };
+  auto diag_check = [&](const char* what) -> grs_status {
+    GRS_HIP(hipStreamSynchronize(stream));
+    uint32_t hit[8];
+    GRS_HIP(hipMemcpyFromSymbol(hit, HIP_SYMBOL(grs::diag_hit), sizeof(hit)));
+    uint32_t host_err[4] = {};
+    GRS_HIP(hipMemcpy(host_err, err, sizeof(host_err), hipMemcpyDeviceToHost));
+    fprintf(stderr, "diag %-12s bad stores %u (max %u)  bad loads %u (max %u)  status %u (tile row %u)  error word %u\n",
+            what, hit[0], hit[1], hit[2], hit[3], hit[4], hit[5], host_err[0]);
+    const uint32_t zero[8] = {};
+    GRS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(grs::diag_hit), zero, sizeof(zero)));
+    const char* stop = getenv("GRS_DIAG_STOP");
+    if (stop != nullptr && strcmp(stop, what) == 0) return set_err(GRS_EINVAL, std::string("diag stop after ") + what);
+    return GRS_OK;
+  };
+#define GRS_DIAG_SET(o, i) if ((r = diag_set(o, i)) != GRS_OK) return r
+#define GRS_DIAG_CHECK(w) if ((r = diag_check(w)) != GRS_OK) return r
+#else
+#define GRS_DIAG_SET(o, i)
+#define GRS_DIAG_CHECK(w)
+#endif
   if ((r = mark()) != GRS_OK) return r;
   if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = false;
@@ -1073,11 +1107,12 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   if ((r = mark()) != GRS_OK) return r;
   // P1: stable scatter by the top byte into the sampled regions, src -> alt (no counting read)
   const Dig d1{KB - 8, 255u};
+  GRS_DIAG_SET(region_len, n);
   {
     const uint32_t tiles = (n + tile1 - 1) / tile1;
     auto go = [&](auto tshape, auto optc) {
       using T = decltype(tshape);
-      constexpr uint32_t opt = decltype(optc)::value;
+      constexpr uint32_t opt = decltype(optc)::value | RW;
       hipLaunchKernelGGL((grs::grs_onesweep_region<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, opt, FT::TILE>),
                          dim3(tiles), dim3(T::BLOCK), 0, stream, src, alt, vsrc, valt, n, d1, samp, mult,
                          pad, static_cast<uint32_t>(region_len), tickets, st[0], st[1], err, totals,
@@ -1094,10 +1129,11 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   hipLaunchKernelGGL((grs::grs_seg_hist<K, 1>), dim3(2 * s->cus), dim3(256), 0, stream, src, recf, hdrf,
                      KB - 8, exact, st[0], 256u);
   GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
+  hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT | RW, true>),
                      dim3(s->cus), dim3(FT::BLOCK), 0, stream, src, alt, vsrc, valt, d1, recf, hdrf,
                      exact, 256u, tickets + 15 * GRS_XCDS, st[0], st[1], err, nullptr);
   GRS_HIP(hipGetLastError());
+  GRS_DIAG_CHECK("P1");
   if ((r = mark()) != GRS_OK) return r;
   // P2's plans (the bucket table: P1's regions, or the redo's exact layout): the exact one for
   // the rare redo below, then H2 over a 1/2^k sample of P1's output and the region plan from it
@@ -1128,7 +1164,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
       hipLaunchKernelGGL((grs::grs_msd_plan2<Big::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
                          totals, exact, chunk, tab, rec2, hdr2);
     GRS_HIP(hipGetLastError());
-    hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
+    hipLaunchKernelGGL((grs::grs_msd_hist2<K, REC>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
                        shift ? mb + L.h2s : h2x, st[1], static_cast<uint32_t>(words2), tab, chunk, shift,
                        (const uint32_t*)nullptr);
     GRS_HIP(hipGetLastError());
@@ -1154,18 +1190,22 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
     const Dig d2{KB - 16, 255u};
     const dim3 grid(static_cast<uint32_t>(t2));
     constexpr uint32_t RG = 131072;
-    auto go = [&](auto tshape) {
+    auto go = [&](auto tshape) -> grs_status {
       using T = decltype(tshape);
       if (shift) {
-        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RG, false>),
+        GRS_DIAG_CHECK("plans");
+        GRS_DIAG_SET(cap2, region_len);
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RG | RR | RW, false>),
                            grid, dim3(T::BLOCK), 0, stream, alt, rk, valt, rv, d2, rec2r, hdr2r, reg, 256u,
                            tickets + GRS_XCDS, st[1], st[0], err, dstart, h2, spill2, (const uint32_t*)nullptr);
         GRS_HIP(hipGetLastError());
+        GRS_DIAG_CHECK("P2region");
+        GRS_DIAG_SET(n, region_len);
         // the redo: exact counts, then the exact pass in place (persistent, gated by the flag)
-        hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
+        hipLaunchKernelGGL((grs::grs_msd_hist2<K, REC>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
                            st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2);
         GRS_HIP(hipGetLastError());
-        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, true>),
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RR, true>),
                            dim3(s->cus), dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x,
                            256u, tickets + 14 * GRS_XCDS, st[0], st[1], err, (uint32_t*)nullptr,
                            (uint32_t*)nullptr, (uint32_t*)nullptr, spill2);
@@ -1173,15 +1213,16 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
       } else {
         // no sample: the exact pass straight away (the flag says so to P3: in place)
         GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(spill2), 1, 1, stream));
-        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, false>), grid,
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RR, false>), grid,
                            dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x, 256u,
                            tickets + GRS_XCDS, st[1], st[0], err, (uint32_t*)nullptr, (uint32_t*)nullptr,
                            (uint32_t*)nullptr, (const uint32_t*)nullptr);
         GRS_HIP(hipGetLastError());
       }
+      return GRS_OK;
     };
-    if (xl) go(XL{});
-    else go(Big{});
+    if ((r = xl ? go(XL{}) : go(Big{})) != GRS_OK) return r;
+    GRS_DIAG_CHECK("P2exact");
     hipLaunchKernelGGL(grs::grs_msd_starts, dim3(256), dim3(256), 0, stream, spill2, tab, h2, h2x, dstart,
                        mb + L.len2, mb + L.in2, mb + L.out2);
     GRS_HIP(hipGetLastError());
@@ -1194,20 +1235,22 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // first: grs_msd_copy_big)
   using P3L = std::conditional_t<sizeof(K) == 4 && !PAIRS, MsdLocalC, MsdLocalB>;
   const uint32_t mid_max = P3L::SMAX > P3C::SMAX ? P3L::SMAX : P3C::SMAX;
-  hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
+  hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE, REC>), dim3(65536),
                      dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
                      mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows);
   GRS_HIP(hipGetLastError());
   if (P3L::SMAX > P3C::SMAX) {
     constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
     constexpr int minw = per_cu * P3L::BLOCK / GRS_WAVE / 4;
-    hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw>),
+    hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw, REC>),
                        dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.mid);
     GRS_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
+  hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS, REC>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
                      spill2, bigc, mb + L.bin, mb + L.bstart, mb + L.blen);
   GRS_HIP(hipGetLastError());
+  GRS_DIAG_CHECK("P3");
+  GRS_DIAG_SET(n, n);
   if ((r = mark()) != GRS_OK) return r;
   // fallback: the listed segments by a segmented LSD on the bits below the prefix
   // (keys -> alt -> ... -> keys: ND is even)
@@ -1229,6 +1272,8 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
                        st[p & 1], st[(p + 1) & 1], err, nullptr);
     GRS_HIP(hipGetLastError());
   }
+  GRS_DIAG_CHECK("fallback");
+  GRS_DIAG_SET(0, 0);
   if ((r = mark()) != GRS_OK) return r;
   if (evs) {
     s->info[s->calls % s->ring] = {ev, 6, false, 1};
@@ -1240,6 +1285,17 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
 template <typename K, bool PAIRS>
 grs_status run_sort_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
                         const K* src_in = nullptr, const uint32_t* vsrc_in = nullptr) {
+  if constexpr (PAIRS && sizeof(K) == 4) {
+    if (s->rec_mode != 0) {
+      switch (msd_local_shape(n, 8)) {
+        case 4: return run_msd<K, PAIRS, MsdLocalS, true>(s, keys, vals, n, stream, src_in, vsrc_in);
+        case 5: return run_msd<K, PAIRS, MsdLocalM, true>(s, keys, vals, n, stream, src_in, vsrc_in);
+        case 1: return run_msd<K, PAIRS, MsdLocalA, true>(s, keys, vals, n, stream, src_in, vsrc_in);
+        case 2: return run_msd<K, PAIRS, MsdLocalB, true>(s, keys, vals, n, stream, src_in, vsrc_in);
+        default: return set_err(GRS_EINVAL, "internal: no MSD shape for this n");
+      }
+    }
+  }
   switch (msd_local_shape(n, sizeof(K) + (PAIRS ? 4 : 0))) {
     case 4: return run_msd<K, PAIRS, MsdLocalS>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 5: return run_msd<K, PAIRS, MsdLocalM>(s, keys, vals, n, stream, src_in, vsrc_in);

@@ -162,6 +162,15 @@ struct Lb3 {
 // Segmented pass (grs_onesweep_seg): tiles never straddle a segment and every segment starts a
 // new group, so its chain restarts at its first group and its digit runs start at the
 // segment's own base.
+#ifdef GRS_DIAG
+// Diagnostic builds only (tools/diag): bounds the host sets before a launch (0 = unchecked) --
+// [0] output elements, [1] input elements, [2] status words -- and what broke them: [0] bad
+// stores, [1] the largest bad store index, [2] bad loads, [3] the largest bad load index, [4]
+// tiles whose status layout passes the bound, [5] 1 + the first such tile row.
+__device__ uint32_t diag_lim[4];
+__device__ uint32_t diag_hit[8];
+#endif
+
 struct TileSpan {
   uint32_t tile;       // tile word row (the ticket)
   uint32_t tiles;      // tile rows of the layout
@@ -269,11 +278,32 @@ __device__ __forceinline__ void tile_load_at(K (&key)[ITEMS], uint32_t (&val)[IT
       const bool in = valid >= TILE || lbase + j * GRS_WAVE < valid;
       const uint32_t idx = wbase + j * GRS_WAVE;
       const bool hi = (OPT & 16384) != 0 && idx >= half;
+#ifdef GRS_DIAG
+      if (in && diag_lim[1] != 0u && idx >= diag_lim[1]) {
+        atomicAdd(&diag_hit[2], 1u);
+        atomicMax(&diag_hit[3], idx);
+        key[j] = static_cast<K>(~0u);
+        val[j] = 0u;
+        continue;
+      }
+#endif
       const uint2 x = !in ? make_uint2(~0u, 0u) : hi ? rec_hi[idx - half] : rec[idx];
       key[j] = static_cast<K>(x.x);
       val[j] = x.y;
     }
   } else if (valid >= TILE) {
+#ifdef GRS_DIAG
+    if (diag_lim[1] != 0u && wbase + (ITEMS - 1) * GRS_WAVE >= diag_lim[1]) {
+      atomicAdd(&diag_hit[2], 1u);
+      atomicMax(&diag_hit[3], wbase + (ITEMS - 1) * GRS_WAVE);
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        key[j] = static_cast<K>(~static_cast<K>(0));
+        val[j] = 0u;
+      }
+      return;
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) key[j] = keys_in[wbase + j * GRS_WAVE];
     if constexpr (PAIRS) {
@@ -355,6 +385,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   const uint32_t dmask = dig.max_digit();
   uint32_t* gacc = status + static_cast<size_t>(tiles) * RADIX;
   uint32_t* ginc = gacc + static_cast<size_t>(groups) * RADIX;
+#ifdef GRS_DIAG
+  if (t == 0 && diag_lim[2] != 0u &&
+      (static_cast<size_t>(tiles + 2 * groups) * RADIX > diag_lim[2] || tile >= tiles || sp.group >= groups)) {
+    atomicAdd(&diag_hit[4], 1u);
+    atomicCAS(&diag_hit[5], 0u, tile + 1u);
+  }
+#endif
 
   // digit of item j (indexed digits: of (key, shard-local index); padding: the largest)
   auto dig_of = [&](int j) -> uint32_t {
@@ -549,6 +586,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   // its digit only moves forward through the tile-local digit starts (at most RADIX - 1 steps
   // per tile, over empty digits too).
   auto put = [&](uint32_t dst, K kk, uint32_t i) {
+#ifdef GRS_DIAG
+    if (diag_lim[0] != 0u && dst >= diag_lim[0]) {
+      atomicAdd(&diag_hit[0], 1u);
+      atomicMax(&diag_hit[1], dst);
+      return;
+    }
+#endif
     if constexpr ((OPT & 8192) != 0) {
       static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
       const uint2 r = make_uint2(static_cast<uint32_t>(kk), sm.vals[i]);
@@ -855,7 +899,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
     uint32_t* __restrict__ totals = nullptr, uint32_t* __restrict__ spill = nullptr,
     const uint32_t* __restrict__ gate = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, RadixDigit<K>>;
-  static_assert((OPT & (4096 | 8192 | 16384 | 32768)) == 0, "segmented passes move two arrays");
+  static_assert((OPT & (16384 | 32768)) == 0, "segmented passes: records in one buffer (n unknown)");
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
   // gate (nullable): run only when *gate != 0 (a redo that is usually not needed)

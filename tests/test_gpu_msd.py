@@ -269,3 +269,38 @@ def test_msd_exact_p2_hook(gpu, kb, pairs):
     assert np.array_equal(gk, keys[perm])
     if pairs:
         assert np.array_equal(gv, perm.astype(np.uint32))
+
+
+@pytest.mark.parametrize("records", ["arrays", "split"])
+def test_msd_pairs_sampled_p2_records(gpu, records):
+    """u32 pairs at a sampled size: with records (the default) P1 and P2 write 8-byte (key,
+    value) records and H2 / P2 / P3 read them; without, two arrays.  Keys and the stable
+    permutation bit-exact both ways, and through a P2 region spill (the exact redo reading
+    records)."""
+    import gpuradixsort_amd as grs
+
+    n = (1 << 27) + 77
+    for other in list(_S):
+        _S.pop(other).close()
+    s = grs.RadixSorter(n, key_bits=32, pairs=True, radix_bits=8)
+    try:
+        s.set_option("msd", "always")
+        s.set_option("records", records)
+        rng = np.random.default_rng(4242)
+        piece = (np.arange(n, dtype=np.int64) // 64) % 2
+        spill = (np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)) | \
+            rng.integers(0, 1 << 16, n, dtype=np.uint32)
+        dup = rng.integers(0, 1 << 32, n, dtype=np.uint32)
+        dup[::3] = dup[1]
+        for name, keys in (("dup", dup), ("p2_spill", spill)):
+            k = torch.from_numpy(keys).to(gpu)
+            v = torch.arange(n, dtype=torch.int32, device=gpu).view(torch.uint32)
+            s.sort(k, v)
+            torch.cuda.synchronize()
+            s.check_error()
+            perm = np.argsort(keys, kind="stable")
+            assert np.array_equal(k.cpu().numpy(), keys[perm]), name
+            assert np.array_equal(v.cpu().numpy(), perm.astype(np.uint32)), name
+            del k, v
+    finally:
+        s.close()
