@@ -1077,13 +1077,17 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   };
   auto diag_check = [&](const char* what) -> grs_status {
     GRS_HIP(hipStreamSynchronize(stream));
-    uint32_t hit[8];
+    uint32_t hit[24];
     GRS_HIP(hipMemcpyFromSymbol(hit, HIP_SYMBOL(grs::diag_hit), sizeof(hit)));
+    if (hit[8] != 0u)
+      fprintf(stderr, "diag %-12s first run past the bound: tile %u digit %u start %u gstart %u prefix %u seg_start %u "
+              "seg_len %u publish %u gh %u base %u valid %u lstart %u\n", what, hit[9], hit[10], hit[11], hit[12],
+              hit[13], hit[14], hit[15], hit[16], hit[17], hit[18], hit[19], hit[20]);
     uint32_t host_err[4] = {};
     GRS_HIP(hipMemcpy(host_err, err, sizeof(host_err), hipMemcpyDeviceToHost));
     fprintf(stderr, "diag %-12s bad stores %u (max %u)  bad loads %u (max %u)  status %u (tile row %u)  error word %u\n",
             what, hit[0], hit[1], hit[2], hit[3], hit[4], hit[5], host_err[0]);
-    const uint32_t zero[8] = {};
+    const uint32_t zero[24] = {};
     GRS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(grs::diag_hit), zero, sizeof(zero)));
     const char* stop = getenv("GRS_DIAG_STOP");
     if (stop != nullptr && strcmp(stop, what) == 0) return set_err(GRS_EINVAL, std::string("diag stop after ") + what);

@@ -168,7 +168,7 @@ struct Lb3 {
 // stores, [1] the largest bad store index, [2] bad loads, [3] the largest bad load index, [4]
 // tiles whose status layout passes the bound, [5] 1 + the first such tile row.
 __device__ uint32_t diag_lim[4];
-__device__ uint32_t diag_hit[8];
+__device__ uint32_t diag_hit[24];   // [8..] the first digit run past the bound: see onesweep_tile
 #endif
 
 struct TileSpan {
@@ -571,9 +571,32 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       // the same sort then reads keys whose digits no longer match the upfront histogram, and
       // a run could pass n.  Keep every run inside its segment, [0, n) for an ordinary pass (a
       // no-op on consistent counts).
-      const uint32_t room = sp.seg_len - publish;
-      start = sp.seg_start + (gstart > room ? room : gstart + min(prefix, room - gstart));
+      // In 64 bits: the 32-bit form (gstart > room ? room : gstart + min(prefix, room - gstart))
+      // came out of this ROCm 7.2 compiler without its first arm (the device IR computes
+      // gstart + min(prefix, room - gstart) unconditionally), so a region run past its room was
+      // not held back -- P2's sampled regions write past the region buffer then (found by the
+      // bounds-checked build, tools/diag).
+      const uint64_t last = sp.seg_len >= publish ? static_cast<uint64_t>(sp.seg_len - publish) : 0u;
+      const uint64_t want = static_cast<uint64_t>(gstart) + static_cast<uint64_t>(prefix);
+      start = sp.seg_start + static_cast<uint32_t>(want < last ? want : last);
     }
+#ifdef GRS_DIAG
+    if (diag_lim[0] != 0u && publish != 0u && start + publish > diag_lim[0] &&
+        atomicCAS(&diag_hit[8], 0u, 1u) == 0u) {
+      diag_hit[9] = tile;
+      diag_hit[10] = t;
+      diag_hit[11] = start;
+      diag_hit[12] = gstart;
+      diag_hit[13] = prefix;
+      diag_hit[14] = sp.seg_start;
+      diag_hit[15] = sp.seg_len;
+      diag_hit[16] = publish;
+      diag_hit[17] = gh;
+      diag_hit[18] = sp.base;
+      diag_hit[19] = sp.valid;
+      diag_hit[20] = lstart;
+    }
+#endif
     // (indexed digits, the partition pass: its one pass per call reads the input as given, so
     // a timed-out look-back there only underestimates its own runs' starts; they stay >= 0 and
     // end before n -- no clamp needed)
