@@ -998,10 +998,10 @@ bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
 // sample -> P1 (regions) -> [redo] -> P2's plan -> H2 -> P2 -> P3 -> fallback (plan,
 // histograms, a segmented LSD over the bits below the prefix for the segments P3 left;
 // persistent grids that leave at once when there are none).  src_in / vsrc_in (out of place):
-// the sample and P1 read them; the result lands in keys / vals either way.  REC (u32 pairs,
-// option GRS_OPT_RECORDS != 0): P1 and P2 write 8-byte (key, value) records into the scratch and
-// the region buffer (one run per digit instead of two), H2, P2 and P3 read them.
-template <typename K, bool PAIRS, typename P3C, bool REC = false>
+// the sample and P1 read them; the result lands in keys / vals either way.  u32 pairs move as
+// two arrays throughout: 8-byte (key, value) records between the passes measured no faster
+// (DESIGN.md §6.R5).
+template <typename K, bool PAIRS, typename P3C>
 grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
                    const K* src_in, const uint32_t* vsrc_in) {
   using Big = BigTile<K, PAIRS>;
@@ -1012,8 +1012,6 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   constexpr int KB = 8 * static_cast<int>(sizeof(K));
   constexpr int ND = (KB - 16) / 8;
   static_assert(!Big::TWO_ROUNDS, "u64 pairs take the LSD sort");
-  static_assert(!REC || (PAIRS && sizeof(K) == 4), "records: u32 pairs");
-  constexpr uint32_t RW = REC ? 8192 : 0, RR = REC ? 4096 : 0;   // records written / read
   constexpr uint32_t G = GRS_LB_GROUP;
   const bool big = use_big_tiles(s, n, Big::TILE);
   const bool xl = big && use_xl(s, n, XL::TILE);
@@ -1116,7 +1114,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
     const uint32_t tiles = (n + tile1 - 1) / tile1;
     auto go = [&](auto tshape, auto optc) {
       using T = decltype(tshape);
-      constexpr uint32_t opt = decltype(optc)::value | RW;
+      constexpr uint32_t opt = decltype(optc)::value;
       hipLaunchKernelGGL((grs::grs_onesweep_region<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, opt, FT::TILE>),
                          dim3(tiles), dim3(T::BLOCK), 0, stream, src, alt, vsrc, valt, n, d1, samp, mult,
                          pad, static_cast<uint32_t>(region_len), tickets, st[0], st[1], err, totals,
@@ -1133,7 +1131,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   hipLaunchKernelGGL((grs::grs_seg_hist<K, 1>), dim3(2 * s->cus), dim3(256), 0, stream, src, recf, hdrf,
                      KB - 8, exact, st[0], 256u);
   GRS_HIP(hipGetLastError());
-  hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT | RW, true>),
+  hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
                      dim3(s->cus), dim3(FT::BLOCK), 0, stream, src, alt, vsrc, valt, d1, recf, hdrf,
                      exact, 256u, tickets + 15 * GRS_XCDS, st[0], st[1], err, nullptr);
   GRS_HIP(hipGetLastError());
@@ -1168,7 +1166,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
       hipLaunchKernelGGL((grs::grs_msd_plan2<Big::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
                          totals, exact, chunk, tab, rec2, hdr2);
     GRS_HIP(hipGetLastError());
-    hipLaunchKernelGGL((grs::grs_msd_hist2<K, REC>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
+    hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
                        shift ? mb + L.h2s : h2x, st[1], static_cast<uint32_t>(words2), tab, chunk, shift,
                        (const uint32_t*)nullptr);
     GRS_HIP(hipGetLastError());
@@ -1199,17 +1197,17 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
       if (shift) {
         GRS_DIAG_CHECK("plans");
         GRS_DIAG_SET(cap2, region_len);
-        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RG | RR | RW, false>),
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RG, false>),
                            grid, dim3(T::BLOCK), 0, stream, alt, rk, valt, rv, d2, rec2r, hdr2r, reg, 256u,
                            tickets + GRS_XCDS, st[1], st[0], err, dstart, h2, spill2, (const uint32_t*)nullptr);
         GRS_HIP(hipGetLastError());
         GRS_DIAG_CHECK("P2region");
         GRS_DIAG_SET(n, region_len);
         // the redo: exact counts, then the exact pass in place (persistent, gated by the flag)
-        hipLaunchKernelGGL((grs::grs_msd_hist2<K, REC>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
+        hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
                            st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2);
         GRS_HIP(hipGetLastError());
-        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RR, true>),
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, true>),
                            dim3(s->cus), dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x,
                            256u, tickets + 14 * GRS_XCDS, st[0], st[1], err, (uint32_t*)nullptr,
                            (uint32_t*)nullptr, (uint32_t*)nullptr, spill2);
@@ -1217,7 +1215,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
       } else {
         // no sample: the exact pass straight away (the flag says so to P3: in place)
         GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(spill2), 1, 1, stream));
-        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RR, false>), grid,
+        hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, false>), grid,
                            dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x, 256u,
                            tickets + GRS_XCDS, st[1], st[0], err, (uint32_t*)nullptr, (uint32_t*)nullptr,
                            (uint32_t*)nullptr, (const uint32_t*)nullptr);
@@ -1239,18 +1237,18 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // first: grs_msd_copy_big)
   using P3L = std::conditional_t<sizeof(K) == 4 && !PAIRS, MsdLocalC, MsdLocalB>;
   const uint32_t mid_max = P3L::SMAX > P3C::SMAX ? P3L::SMAX : P3C::SMAX;
-  hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE, REC>), dim3(65536),
+  hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
                      dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
                      mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows);
   GRS_HIP(hipGetLastError());
   if (P3L::SMAX > P3C::SMAX) {
     constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
     constexpr int minw = per_cu * P3L::BLOCK / GRS_WAVE / 4;
-    hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw, REC>),
+    hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw>),
                        dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.mid);
     GRS_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS, REC>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
+  hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
                      spill2, bigc, mb + L.bin, mb + L.bstart, mb + L.blen);
   GRS_HIP(hipGetLastError());
   GRS_DIAG_CHECK("P3");
@@ -1289,17 +1287,6 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
 template <typename K, bool PAIRS>
 grs_status run_sort_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream_t stream,
                         const K* src_in = nullptr, const uint32_t* vsrc_in = nullptr) {
-  if constexpr (PAIRS && sizeof(K) == 4) {
-    if (s->rec_mode != 0) {
-      switch (msd_local_shape(n, 8)) {
-        case 4: return run_msd<K, PAIRS, MsdLocalS, true>(s, keys, vals, n, stream, src_in, vsrc_in);
-        case 5: return run_msd<K, PAIRS, MsdLocalM, true>(s, keys, vals, n, stream, src_in, vsrc_in);
-        case 1: return run_msd<K, PAIRS, MsdLocalA, true>(s, keys, vals, n, stream, src_in, vsrc_in);
-        case 2: return run_msd<K, PAIRS, MsdLocalB, true>(s, keys, vals, n, stream, src_in, vsrc_in);
-        default: return set_err(GRS_EINVAL, "internal: no MSD shape for this n");
-      }
-    }
-  }
   switch (msd_local_shape(n, sizeof(K) + (PAIRS ? 4 : 0))) {
     case 4: return run_msd<K, PAIRS, MsdLocalS>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 5: return run_msd<K, PAIRS, MsdLocalM>(s, keys, vals, n, stream, src_in, vsrc_in);

@@ -325,8 +325,7 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
 // >= n / chunk + 256; tab from grs_msd_plan2 with the same chunk: 256K keys at 2^30, fewer
 // below so the grid is several resident rounds, not 2.5 with a tail); zeroes `zero_words` of
 // `zero` (P2's status).  Two 1024-thread blocks per CU (8 waves per SIMD).
-// REC: keys holds 8-byte (key, value) records of u32 pairs (P1's output then).
-template <typename K, bool REC = false>
+template <typename K>
 __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ keys,
                                                          uint32_t* __restrict__ h2,
                                                          uint32_t* __restrict__ zero,
@@ -356,29 +355,25 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   const uint32_t cl = min(chunk, tab[257 + s] - j * chunk);
   uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
   constexpr int SH = 8 * static_cast<int>(sizeof(K)) - 16;   // the second byte from the top
-  static_assert(!REC || (sizeof(K) == 4), "records: u32 key + u32 value");
-  using E = std::conditional_t<REC, uint2, K>;   // one element: a key or a record
-  auto count = [&](const E& x) {
-    K k;
-    if constexpr (REC) k = x.x; else k = x;
+  auto count = [&](K k) {
     atomicAdd(base + (static_cast<uint32_t>(k >> SH) & 255u) * GRS_H2_COPIES, 1u);
   };
-  constexpr uint32_t VEC = 16 / sizeof(E);
-  const E* kc = reinterpret_cast<const E*>(keys) + c0;
-  // 16-B loads from the first aligned element on
-  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(kc) & 15u) / sizeof(E);
+  constexpr uint32_t VEC = 16 / sizeof(K);
+  const K* kc = keys + c0;
+  // 16-B loads from the first aligned key on
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(kc) & 15u) / sizeof(K);
   const uint32_t head = min(cl, (VEC - mis) % VEC);
   const uint32_t nv = (cl - head) / VEC;
   const uint4* kv = reinterpret_cast<const uint4*>(kc + head);
   auto count4 = [&](const uint4& x) {
-    const E* e = reinterpret_cast<const E*>(&x);
+    const K* e = reinterpret_cast<const K*>(&x);
 #pragma unroll
     for (uint32_t q = 0; q < VEC; ++q) count(e[q]);
   };
   if (sample_shift != 0) {
     // a sample: the first of every 2^sample_shift 64-key pieces (whatever the input order, the
     // pieces cover the chunk evenly); the bucket's scale is its length over its sampled keys
-    constexpr uint32_t PU = 64 / VEC;   // 16-B loads per piece of 64 elements
+    constexpr uint32_t PU = 64 / VEC;   // 16-B loads per piece
     const uint32_t np = (nv + PU - 1) / PU;
     const uint32_t ns = ((np + (1u << sample_shift) - 1) >> sample_shift) * PU;
     for (uint32_t m = t; m < ns; m += B) {
@@ -523,8 +518,8 @@ __global__ __launch_bounds__(256) void grs_msd_starts(const uint32_t* __restrict
 // The big-list segments of P3 (longer than any LDS shape) from the region buffer into the
 // caller's arrays at their sorted place, for the in-place fallback (persistent grid, every
 // block on every entry; leaves at once without entries or after a spill, whose exact pass
-// already wrote the caller's arrays).  REC: the region buffer holds 8-byte records (rk).
-template <typename K, bool PAIRS, bool REC = false>
+// already wrote the caller's arrays).
+template <typename K, bool PAIRS>
 __global__ __launch_bounds__(256) void grs_msd_copy_big(const K* __restrict__ rk, const uint32_t* __restrict__ rv,
                                                         K* __restrict__ keys, uint32_t* __restrict__ vals,
                                                         const uint32_t* __restrict__ spill,
@@ -537,14 +532,8 @@ __global__ __launch_bounds__(256) void grs_msd_copy_big(const K* __restrict__ rk
   for (uint32_t e = 0; e < count; ++e) {
     const uint32_t a = big_in[e], o = big_out[e], n = big_len[e];
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-      if constexpr (REC) {
-        const uint2 x = reinterpret_cast<const uint2*>(rk)[a + i];
-        keys[o + i] = x.x;
-        vals[o + i] = x.y;
-      } else {
-        keys[o + i] = rk[a + i];
-        if constexpr (PAIRS) vals[o + i] = rv[a + i];
-      }
+      keys[o + i] = rk[a + i];
+      if constexpr (PAIRS) vals[o + i] = rv[a + i];
     }
   }
 }
@@ -590,18 +579,6 @@ struct LocalSort {
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
       k[j] = i < len ? kin[lo + i] : K(0);
       if constexpr (PAIRS) v[j] = i < len ? vin[lo + i] : 0u;
-    }
-  }
-  // the same from 8-byte (key, value) records (u32 pairs)
-  __device__ __forceinline__ static void load_rec(K (&k)[I], Vals& v, const uint2* rin, uint32_t lo, uint32_t len) {
-    static_assert(PAIRS && sizeof(K) == 4, "records: u32 key + u32 value");
-    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-#pragma unroll
-    for (uint32_t j = 0; j < I; ++j) {
-      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      const uint2 x = i < len ? rin[lo + i] : make_uint2(0u, 0u);
-      k[j] = x.x;
-      v[j] = x.y;
     }
   }
   // `rounds` stable 8-bit rounds from the registers; the sorted segment is left in sm.sk / sm.sv
@@ -693,9 +670,8 @@ struct LocalSort {
 // the big list for the segmented LSD in place (grs_msd_copy_big moves them first): big[0] counts
 // them, big[1] counts those longer than one fallback tile (TILEF keys), which get a histogram
 // row (ND digits) zeroed here; big_in / big_start / big_len / big_row hold (region start,
-// sorted start, length, row) per entry.  REC: the region buffer holds 8-byte (key, value)
-// records (u32 pairs; rk, rv unused).
-template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF, bool REC = false>
+// sorted start, length, row) per entry.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF>
 __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uint32_t* __restrict__ vals,
                                                        const K* __restrict__ rk, const uint32_t* __restrict__ rv,
                                                        const uint32_t* __restrict__ spill,
@@ -721,14 +697,8 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
   const uint32_t* const vin = inplace ? vals : rv;
   if (len == 1u) {
     if (!inplace && t == 0) {
-      if constexpr (REC) {
-        const uint2 x = reinterpret_cast<const uint2*>(rk)[lo];
-        keys[o] = x.x;
-        vals[o] = x.y;
-      } else {
-        keys[o] = kin[lo];
-        if constexpr (PAIRS) vals[o] = vin[lo];
-      }
+      keys[o] = kin[lo];
+      if constexpr (PAIRS) vals[o] = vin[lo];
     }
     return;
   }
@@ -756,22 +726,13 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
       for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(sm.slot) * ND * 256 + i] = 0;
     return;
   }
-  K k[I];
-  typename LS::Vals v;
-  if constexpr (REC) {
-    if (!inplace) LS::load_rec(k, v, reinterpret_cast<const uint2*>(rk) + lo, 0u, len);
-    else LS::load(k, v, kin + lo, vin + lo, 0u, len);
-  } else {
-    LS::load(k, v, kin + lo, PAIRS ? vin + lo : nullptr, 0u, len);
-  }
-  LS::sort_rounds(sm, k, v, len, LS::ROUNDS);
-  LS::store(sm, keys + o, PAIRS ? vals + o : nullptr, 0u, len);
+  LS::run(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, 0u, len, LS::ROUNDS);
 }
 
 // P3's second shape: the mid list's segments (persistent grid, a segment per workgroup in
 // turn; leaves at once when the list is empty).  MINW: waves per SIMD to keep the registers
-// of two workgroups per CU where their LDS fits.  REC as grs_msd_local.
-template <typename K, bool PAIRS, int BLOCK, int I, bool C16, int MINW, bool REC = false>
+// of two workgroups per CU where their LDS fits.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict__ keys,
                                                             uint32_t* __restrict__ vals,
                                                             const K* __restrict__ rk,
@@ -787,16 +748,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict_
   const uint32_t* const vin = inplace ? vals : rv;
   for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
     const uint32_t lo = mid[2 + 3 * e], o = mid[3 + 3 * e], len = mid[4 + 3 * e];
-    K k[I];
-    typename LS::Vals v;
-    if constexpr (REC) {
-      if (!inplace) LS::load_rec(k, v, reinterpret_cast<const uint2*>(rk) + lo, 0u, len);
-      else LS::load(k, v, kin + lo, vin + lo, 0u, len);
-    } else {
-      LS::load(k, v, kin + lo, PAIRS ? vin + lo : nullptr, 0u, len);
-    }
-    LS::sort_rounds(sm, k, v, len, LS::ROUNDS);
-    LS::store(sm, keys + o, PAIRS ? vals + o : nullptr, 0u, len);
+    LS::run(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, 0u, len, LS::ROUNDS);
     __syncthreads();   // every LDS read of this segment before the next one's
   }
 }

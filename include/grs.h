@@ -126,8 +126,7 @@ typedef enum grs_option {
                                 per pass on MI355X, never chosen by size) */
   GRS_OPT_RECORDS = 4,       /* u32 pairs at 8-bit digits: 0 two arrays every pass, 1 8-byte
                                 (key, value) records in the sorter's scratch, 2 (default) also
-                                split over the caller's arrays (even n, 8-byte aligned); the
-                                MSD sort's P1 / P2 write records into their scratch when != 0 */
+                                split over the caller's arrays (even n, 8-byte aligned) */
   GRS_OPT_RANK = 5,          /* 0 (default) the device probe's choice, 1 ballot-match ranking */
   GRS_OPT_SHARDED_PATH = 6,  /* grs_sort_sharded on ONE rank: 0 (default) copy + local sort,
                                 1 the G-rank path (a one-GPU rehearsal of the exchange) */

@@ -271,12 +271,10 @@ def test_msd_exact_p2_hook(gpu, kb, pairs):
         assert np.array_equal(gv, perm.astype(np.uint32))
 
 
-@pytest.mark.parametrize("records", ["arrays", "split"])
-def test_msd_pairs_sampled_p2_records(gpu, records):
-    """u32 pairs at a sampled size: with records (the default) P1 and P2 write 8-byte (key,
-    value) records and H2 / P2 / P3 read them; without, two arrays.  Keys and the stable
-    permutation bit-exact both ways, and through a P2 region spill (the exact redo reading
-    records)."""
+def test_msd_pairs_sampled_p2(gpu):
+    """u32 pairs at a sampled size (P2 into sampled regions): keys and the stable permutation
+    bit-exact, also through a P2 region spill -- the case whose runs the region pass must hold
+    inside the region buffer (the run clamp, grs_pass.hpp) before the exact redo."""
     import gpuradixsort_amd as grs
 
     n = (1 << 27) + 77
@@ -285,7 +283,6 @@ def test_msd_pairs_sampled_p2_records(gpu, records):
     s = grs.RadixSorter(n, key_bits=32, pairs=True, radix_bits=8)
     try:
         s.set_option("msd", "always")
-        s.set_option("records", records)
         rng = np.random.default_rng(4242)
         piece = (np.arange(n, dtype=np.int64) // 64) % 2
         spill = (np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)) | \
