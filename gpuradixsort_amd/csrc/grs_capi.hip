@@ -1149,7 +1149,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   K* const rk = static_cast<K*>(s->alt2_keys);
   uint32_t* const rv = PAIRS ? s->alt2_vals : nullptr;
   // H2 chunks: ~8 rounds of the resident blocks (2 per CU), 32K to 256K keys; the sample: one
-  // 64-key piece in 2^k, k so that a uniform 16-bit bin still gets ~1000 sampled keys
+  // GRS_H2_PIECE-key piece in 2^k, k so that a uniform 16-bit bin still gets ~1000 sampled keys
   uint32_t chunk = GRS_H2_CHUNK;
   while (chunk > 32768u && static_cast<uint64_t>(n) / chunk < 16u * static_cast<uint64_t>(std::max(1, s->cus)))
     chunk >>= 1;

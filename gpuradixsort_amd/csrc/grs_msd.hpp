@@ -42,6 +42,7 @@ enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2, kSegMoved =
 // LDS of the planner: 6 words per segment (tile, row and group prefixes, start, length,
 // histogram row); larger tables keep them in global scratch (`spill`, 6 * (nseg + 1) words).
 #define GRS_PLAN_LDS_SEGS 2048
+#define GRS_H2_PIECE 256   // keys of one piece of H2's sample (grs_msd_hist2)
 #define GRS_PLAN_LDS_WORDS (6 * GRS_PLAN_LDS_SEGS + 5 * 16)
 
 // Block exclusive scan of NV values per thread over BLOCK threads (wsum: NV * waves words of
@@ -371,13 +372,29 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
     for (uint32_t q = 0; q < VEC; ++q) count(e[q]);
   };
   if (sample_shift != 0) {
-    // a sample: the first of every 2^sample_shift 64-key pieces (whatever the input order, the
-    // pieces cover the chunk evenly); the bucket's scale is its length over its sampled keys
-    constexpr uint32_t PU = 64 / VEC;   // 16-B loads per piece
+    // a sample: the first of every 2^sample_shift GRS_H2_PIECE-key pieces (whatever the input
+    // order, the pieces cover the chunk evenly); the bucket's scale is its length over its
+    // sampled keys
+    constexpr uint32_t PU = GRS_H2_PIECE / VEC;   // 16-B loads per piece
     const uint32_t np = (nv + PU - 1) / PU;
     const uint32_t ns = ((np + (1u << sample_shift) - 1) >> sample_shift) * PU;
-    for (uint32_t m = t; m < ns; m += B) {
-      const uint32_t v = ((m / PU) << sample_shift) * PU + m % PU;
+    auto at = [&](uint32_t m) { return ((m / PU) << sample_shift) * PU + m % PU; };
+    uint32_t m = t;
+    for (; m + 3 * B < ns; m += 4 * B) {   // four loads in flight (one at a time: latency-bound)
+      uint4 x[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t v = at(m + u * B);
+        ok[u] = v < nv;
+        x[u] = kv[ok[u] ? v : 0u];   // (nv >= 1 here: ns > 0)
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) count4(x[u]);
+    }
+    for (; m < ns; m += B) {
+      const uint32_t v = at(m);
       if (v < nv) count4(kv[v]);
     }
     __syncthreads();

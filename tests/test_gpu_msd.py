@@ -63,6 +63,8 @@ def dists(n, rng):
     yield "narrow_29bit", rng.integers(0, 1 << 29, n, dtype=np.uint32)
 
 
+PIECE = 256   # keys of one piece of H2's sample (GRS_H2_PIECE, grs_msd.hpp)
+
 SIZES = [1, 2, 3, 64, 1000, 4097, 5121, 36865, 65537, 300007, 1 << 20]
 
 
@@ -222,7 +224,7 @@ def test_msd_typed_segment_edges_and_spill(gpu, kb, pairs):
 
 @pytest.mark.parametrize("n", [(1 << 27) + 77, 1 << 28])
 def test_msd_sampled_p2(gpu, n):
-    """Sorts large enough that H2 counts a sample of P1's output (one 64-key piece in 2 / 4) and
+    """Sorts large enough that H2 counts a sample of P1's output (one 256-key piece in 2 / 4) and
     P2 scatters into regions sized from it (grs_msd_plan3), P3 reading the region buffer:
     uniform, narrow (few top-byte buckets, long regions), few-unique and sorted keys."""
     rng = np.random.default_rng(n)
@@ -239,14 +241,14 @@ def test_msd_sampled_p2(gpu, n):
 
 
 def test_msd_p2_region_spill(gpu):
-    """A sample that misses a bin: every key in top-byte bucket 0 and, by 64-key piece of P1's
-    output, byte 2 = 0 in the sampled pieces (even ones: one in two is sampled at 2^27) and 255
+    """A sample that misses a bin: every key in top-byte bucket 0 and, by 256-key piece of P1's
+    output (GRS_H2_PIECE), byte 2 = 0 in the sampled pieces (even ones: one in two is sampled at 2^27) and 255
     in the others, so bin (0, 255) outgrows its region: P2's last tiles flag it, the exact
     histogram and pass run (gated on the flag) and P3 sorts in place -- bit-exact, and the
     sorter's next sort is too."""
     n = 1 << 27
     rng = np.random.default_rng(31)
-    piece = (np.arange(n, dtype=np.int64) // 64) % 2
+    piece = (np.arange(n, dtype=np.int64) // PIECE) % 2
     keys = np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)
     keys |= rng.integers(0, 1 << 16, n, dtype=np.uint32)
     got = run(keys, gpu, "always")
@@ -284,7 +286,7 @@ def test_msd_pairs_sampled_p2(gpu):
     try:
         s.set_option("msd", "always")
         rng = np.random.default_rng(4242)
-        piece = (np.arange(n, dtype=np.int64) // 64) % 2
+        piece = (np.arange(n, dtype=np.int64) // PIECE) % 2
         spill = (np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)) | \
             rng.integers(0, 1 << 16, n, dtype=np.uint32)
         dup = rng.integers(0, 1 << 32, n, dtype=np.uint32)
