@@ -1,18 +1,24 @@
 """bench.py — Gkeys/s of the MI355X radix sort (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5|ns]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5|ns] [--dist uniform|perm]
   (N > 1: torchrun --nproc-per-node N ... bench.py --gpus N ...; one rank per GPU, RCCL)
 
 A step = one complete sort of one batch of synthetic keys already resident in HBM
 (key[i] = splitmix64(seed ^ global_i)).  Every step sorts its OWN unsorted
 buffer (generated before the timed region), so nothing is restored or skipped inside it.
 
-Default workload: BASELINE config C4 itself, 2^30 uniform uint32 keys in total, 8-bit digits,
+Default workload: BASELINE config C4 itself, 2^30 uniform uint32 keys in total, 8-bit digits
+(from 48M keys the MSD-first schedule: two stable scatters by the keys' top two varying bytes,
+then every 16-bit segment sorted in LDS; below, and for 4-bit digits, the LSD passes),
 STRONG scaling: at N = 1 one MI355X sorts all 2^30 keys in one call; at N > 1 rank r holds
 2^30 / N keys and the sort is grs_sort_sharded (gpuradixsort_amd/sharded.py): up to 4 ranks
 the presorted exchange (local sort, bit-packed delta encoding of the buckets, one RCCL send /
 recv per peer over xGMI, decode, merge), beyond that the partition-first one (range partition,
 one RCCL all-to-all, local sort).  `value` = 2^30 keys x steps / wall time.
+
+At N = 1 the default line also carries `north_star` (2^28 uniform u32 keys, BASELINE's
+north-star target) and `reference_input` (the reference's own input, 0..N-1 shuffled,
+main.cpp:119-125, at 2^28 and 2^30: the MSD digits adapt to its 28 / 30-bit span).
 
 Rank 0 prints ONE JSON line with the driver contract plus:
   roofline      dominant kernel (the LSD schedule's pass: grs_onesweep_v4, or v6 on small
@@ -25,6 +31,10 @@ Rank 0 prints ONE JSON line with the driver contract plus:
                 workload + a known-byte calibration copy with the pass's access width, which
                 gives the counters' correction factors), after the timed region (rank 0, N = 1;
                 --no-traffic skips them, null on any failure)
+  moved_roofline  the bytes the schedule that ran actually moves per step (LSD: a histogram
+                read + 2 x per pass; MSD: 3 read+write sweeps + H2's sampled read), over the step
+                time, next to `sort_roofline`'s credited SURVEY §8d bytes (key bits / digit bits
+                passes, whatever schedule ran: an MSD sort can exceed 1 there)
   cpu_baseline  the oracle's host std::sort on a bounded sample (rank 0, N = 1 only)
 """
 from __future__ import annotations
@@ -48,15 +58,19 @@ CONFIGS = {
     # name: (config_id, total keys (c4: strong scaling) or keys per GPU, key_bits, pairs,
     #        radix_bits, description)
     "c4": (4, 1 << 30, 32, False, 8, "C4: 2^30 uint32 keys in total (strong scaling: 2^30 / N per "
-                                     "GPU), 8-bit LSD; N > 1: one RCCL all-to-all over xGMI "
-                                     "(config.exchange)"),
+                                     "GPU), 8-bit digits (MSD schedule at N = 1); N > 1: one RCCL "
+                                     "exchange over xGMI (config.exchange)"),
     "c2": (2, 1 << 24, 32, False, 4, "C2: 16M uint32 keys, 4-bit-digit LSD"),
-    "c3": (3, 1 << 28, 32, True, 8, "C3: 256M uint32 key + uint32 payload, stable"),
-    "c5": (5, 1 << 28, 64, False, 8, "C5: 256M uint64 keys, 8 x 8-bit passes"),
+    "c3": (3, 1 << 28, 32, True, 8, "C3: 256M uint32 key + uint32 payload, stable, 8-bit digits "
+                                    "(MSD schedule)"),
+    "c5": (5, 1 << 28, 64, False, 8, "C5: 256M uint64 keys, 8-bit digits (MSD schedule: 2 scatters + "
+                                     "LDS rounds; 8 passes credited)"),
     # BASELINE.json north_star's own 1-GPU target: >= 60 % of the HBM roofline on 256 M
     # uniform-random uint32 keys (keys only)
-    "ns": (6, 1 << 28, 32, False, 8, "north star: 256M uniform uint32 keys, keys only, 8-bit LSD"),
+    "ns": (6, 1 << 28, 32, False, 8, "north star: 256M uniform uint32 keys, keys only, 8-bit digits "
+                                     "(MSD schedule)"),
 }
+DISTS = ("uniform", "perm")
 
 
 def parse():
@@ -65,6 +79,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--dist", default="uniform", choices=DISTS,
+                    help="uniform: splitmix64 keys; perm: the reference's input, 0..N-1 shuffled "
+                         "(main.cpp:119-125; grs_fill_permutation)")
+    ap.add_argument("--no-reference-input", action="store_true",
+                    help="skip the reference-input legs (0..N-1 shuffled at 2^28 and 2^30)")
     ap.add_argument("--n", type=int, default=0, help="override the total (c4) / per-GPU key count")
     ap.add_argument("--traffic-json", default="", help="tools/bench_pmc.py output of this workload")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC child runs")
@@ -164,7 +183,10 @@ def pmc_probe(a, options):
     v = torch.empty(n, dtype=torch.uint32, device=dev) if pairs else None
     s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb, options=options)
     for i in range(2):
-        grs.fill_splitmix(k, seed, first_index=i * n)
+        if a.dist == "perm":
+            grs.fill_permutation(k, seed + i)
+        else:
+            grs.fill_splitmix(k, seed, first_index=i * n)
         if pairs:
             grs.iota_u32(v)
         s.sort(k, v)
@@ -180,7 +202,7 @@ def pmc_probe(a, options):
     s.check_error()
 
 
-def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
+def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v", dist="uniform"):
     """HBM bytes per launch of the roofline kernel (the pass, or the MSD schedule's dominant
     kernel; names match by prefix) from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM):
     one counter per rocprofv3 run (FETCH_SIZE, then WRITE_SIZE) over a child --pmc-probe run;
@@ -207,7 +229,7 @@ def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
             out = os.path.join(d, ctr)
             cmd = [rp, "--pmc", ctr, "-d", out, "-o", "p", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-probe", "--config", config,
-                   "--n", str(n_local)] + extra
+                   "--n", str(n_local), "--dist", dist] + extra
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
                                  start_new_session=True)
             try:
@@ -221,7 +243,7 @@ def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
             # rows of the roofline kernel by instantiation (its name followed by "<": the MSD
             # schedule launches other instantiations of the same template that usually leave at
             # once, e.g. the gated redo passes): the one reading the most is the roofline kernel
-            vals = {"pass": {}, "cal": []}
+            vals = {"pass": {}, "cal": [], "all": 0.0}
             for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
                     if r["Counter_Name"] != ctr:
@@ -229,8 +251,10 @@ def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
                     name = r["Kernel_Name"]
                     if (kernel + "<") in name:
                         vals["pass"].setdefault(name, []).append(float(r["Counter_Value"]) * 1024.0)   # KiB -> bytes
-                    elif "grs_copy_u32" in name:
+                    if "grs_copy_u32" in name:
                         vals["cal"].append(float(r["Counter_Value"]) * 1024.0)
+                    elif not any(x in name for x in ("grs_fill_", "grs_iota_u32")):
+                        vals["all"] += float(r["Counter_Value"]) * 1024.0   # every kernel of the 2 sorts
             if not vals["pass"] or not vals["cal"]:
                 return None, f"no {ctr} rows for the pass or the calibration copy"
             if chosen is None:
@@ -238,11 +262,13 @@ def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
             rows = vals["pass"].get(chosen)
             if not rows:
                 return None, f"no {ctr} rows for {chosen[:80]}"
-            got[ctr] = (statistics.mean(rows), statistics.mean(vals["cal"]), len(rows))
+            got[ctr] = (statistics.mean(rows), statistics.mean(vals["cal"]), len(rows), vals["all"] / 2)
     known = CAL_WORDS * 4
     fr, fw = known / got["FETCH_SIZE"][1], known / got["WRITE_SIZE"][1]
     rd, wr = fr * got["FETCH_SIZE"][0], fw * got["WRITE_SIZE"][0]
+    sort_bytes = fr * got["FETCH_SIZE"][3] + fw * got["WRITE_SIZE"][3]
     return {"bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
+            "sort_bytes": round(sort_bytes),
             "read_factor": round(fr, 4), "write_factor": round(fw, 4),
             "launches": got["FETCH_SIZE"][2], "instantiation": chosen[:160],
             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one counter per run, over "
@@ -250,8 +276,26 @@ def measure_traffic(a, config, options, n_local, kernel="grs_onesweep_v"):
                       "calibration of known bytes"}, None
 
 
-def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
-    """One workload of CONFIGS, timed per the driver contract; returns rank 0's JSON dict."""
+def moved_bytes(n, kb, pairs, rb, schedule):
+    """HBM bytes the schedule that ran moves per sort of n keys (its algorithmic traffic, rare
+    redo / fallback passes excluded): LSD = the histogram read + a read and a write per pass (+ a
+    copy-back for an odd pass count); MSD (grs_msd.hpp) = the top digit's scatter, the byte-2
+    scatter and the LDS sort each read and write every element once, plus H2's read of a
+    1 / 2^k sample of the keys (k as run_msd picks it) and the 4-MB sample."""
+    e = kb // 8 + (4 if pairs else 0)
+    if schedule == "msd":
+        k = 0
+        while k < 3 and (n >> (k + 1)) >= 65536 * 1024:
+            k += 1
+        return 3 * 2 * n * e + (n * (kb // 8)) // (1 << k) + (4 << 20)
+    passes = -(-kb // rb)
+    return n * (kb // 8) + passes * 2 * n * e + (2 * n * e if passes % 2 else 0)
+
+
+def run_config(a, config, world, rank, local, dev, sharded, steps, warmup, dist="uniform",
+               traffic=True, cpu=True):
+    """One workload of CONFIGS, timed per the driver contract; returns rank 0's JSON dict.
+    dist: "uniform" (splitmix64) or "perm" (the reference's shuffled 0..N-1)."""
     import gpuradixsort_amd as grs
 
     cid, n_cfg, kb, pairs, rb, desc = CONFIGS[config]
@@ -268,12 +312,20 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     step_bytes = n_local * (kb // 8 + (4 if pairs else 0))
     pool = max(1, min(warmup + steps, int(a.pool_gib * 2**30 // step_bytes)))
 
-    # distinct unsorted inputs, one per step (step s uses global indices offset by s * N_total)
+    # distinct unsorted inputs, one per step (step s uses global indices offset by s * N_total;
+    # perm: step s is the seeded permutation seed + s of 0..N_total-1, rank r its slice r)
     n_total = n_local * world
+
+    def fill(k, i):
+        if dist == "perm":
+            grs.fill_permutation(k, seed + i, total=n_total, first_index=rank * n_local)
+        else:
+            grs.fill_splitmix(k, seed, first_index=i * n_total + rank * n_local)
+
     keys_pool, vals_pool = [], []
     for i in range(pool):
         k = torch.empty(n_local, dtype=kdt, device=dev)
-        grs.fill_splitmix(k, seed, first_index=i * n_total + rank * n_local)
+        fill(k, i)
         keys_pool.append(k)
         if pairs:
             v = torch.empty(n_local, dtype=torch.uint32, device=dev)
@@ -286,7 +338,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         def step(i):
             k = keys_pool[i % pool]
             if i >= pool:   # pool exhausted: regenerate inside the step (counted, honest)
-                grs.fill_splitmix(k, seed, first_index=i * n_total)
+                fill(k, i)
             sorter.sort(k, vals_pool[i % pool] if pairs else None)
     else:
         from gpuradixsort_amd.sharded import ShardedSorter
@@ -297,7 +349,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         def step(i):
             k = keys_pool[i % pool]
             if i >= pool:
-                grs.fill_splitmix(k, seed, first_index=i * n_total + rank * n_local)
+                fill(k, i)
             # the exchange synchronises once per call (the counts); the timeout check of the
             # local sort happens after the timed region (bench.py reads the error word below)
             sorter.sort(k, vals_pool[i % pool] if pairs else None, check_error=False)
@@ -336,7 +388,7 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     barrier()
     for i in range(warmup, warmup + nprof):
         # the timed steps sorted these buffers: fresh unsorted inputs of the same workload
-        grs.fill_splitmix(keys_pool[i % pool], seed, first_index=i * n_total + rank * n_local)
+        fill(keys_pool[i % pool], i)
         if pairs:
             grs.iota_u32(vals_pool[i % pool], rank * n_local)
         step(i)
@@ -384,14 +436,14 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
     del keys_pool, vals_pool, sorter
     torch.cuda.empty_cache()
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(min(a.cpu_sample, n_local), kb, pairs, seed)
+    cpu_b = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and cpu:
+        cpu_b = cpu_baseline(min(a.cpu_sample, n_local), kb, pairs, seed)
 
     # PMC bytes per launch: rocprofv3 child runs of this workload (after the timed region)
     traffic, traffic_info = None, None
-    if rank == 0 and world == 1 and not sharded and not a.no_traffic:
-        traffic_info, why = measure_traffic(a, config, options, n_local, kernel_name)
+    if rank == 0 and world == 1 and not sharded and not a.no_traffic and traffic:
+        traffic_info, why = measure_traffic(a, config, options, n_local, kernel_name, dist)
         if traffic_info:
             traffic = traffic_info["bytes_per_launch"]
         else:
@@ -402,6 +454,8 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
             traffic = rec.get("hbm_bytes_per_launch")
 
     sort_alg = n_local * 2 * passes * (kb // 8 + (4 if pairs else 0))
+    schedule = "msd" if msd else "lsd-fused" if fused else "lsd"
+    moved = moved_bytes(n_sorted_local, kb, pairs, rb, "msd" if msd else "lsd")
     if rank != 0:
         return None
     value = n_total * steps / elapsed / 1e9
@@ -410,9 +464,12 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         "steps": steps, "warmup": warmup,
         "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u32" if kb == 32 else "u64",
-        "data": "synthetic: splitmix64(seed ^ global_index) uniform keys, a distinct unsorted "
-                "buffer per step resident in HBM" + ("; payload = global index" if pairs else ""),
-        "config": {"workload": desc, "keys_per_gpu": n_local, "total_keys": n_total,
+        "data": ("synthetic: splitmix64(seed ^ global_index) uniform keys" if dist == "uniform" else
+                 "synthetic: the reference's input, 0..N-1 shuffled by a seeded bijection "
+                 "(grs_fill_permutation; main.cpp:119-125)")
+                + ", a distinct unsorted buffer per step resident in HBM"
+                + ("; payload = global index" if pairs else ""),
+        "config": {"workload": desc, "dist": dist, "keys_per_gpu": n_local, "total_keys": n_total,
                    "key_bits": kb, "payload": "u32" if pairs else None, "radix_bits": rb,
                    "passes": passes, "parallelism": f"range-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -425,11 +482,17 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         # over the whole step (histogram and exchange included)
         "sort_roofline": {"achieved": round(sort_alg / (elapsed / steps) / 1e9, 1),
                           "frac": round(sort_alg / (elapsed / steps) / 1e9 / HBM_PEAK_GBPS, 4),
-                          "alg_bytes_per_step": sort_alg, "unit": "GB/s"},
-        "cpu_baseline": cpu,
+                          "alg_bytes_per_step": sort_alg, "unit": "GB/s",
+                          "credited_passes": passes},
+        # what the schedule that ran actually moves (moved_bytes), over the same step time
+        "moved_roofline": {"bytes_per_step": moved,
+                           "achieved": round(moved / (elapsed / steps) / 1e9, 1),
+                           "frac": round(moved / (elapsed / steps) / 1e9 / HBM_PEAK_GBPS, 4),
+                           "unit": "GB/s", "schedule": schedule},
+        "cpu_baseline": cpu_b,
         "phases_ms": {"hist": round(hist_ms, 5), "pass_mean": round(mean_pass_ms, 5),
                       "sort_total_gpu": round(sort_ms, 5)},
-        "schedule": "msd" if msd else "lsd-fused" if fused else "lsd",
+        "schedule": schedule,
         "check": {"inversions_last_step": inversions},
     }
     if msd:
@@ -439,6 +502,10 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup):
         out["config"]["options"] = options
     if traffic_info:
         out["traffic_pmc"] = traffic_info
+        if traffic_info.get("sort_bytes"):
+            # every kernel of one sort, from the same PMC runs: the bytes HBM really moved
+            out["moved_roofline"]["pmc_bytes_per_step"] = traffic_info["sort_bytes"]
+            out["moved_roofline"]["pmc_over_moved"] = round(traffic_info["sort_bytes"] / moved, 4)
     if sharded:
         out["phases_ms"]["recv_keys_rank0"] = n_sorted_local
         out["config"]["exchange"] = exchange
@@ -476,18 +543,27 @@ def main():
             port = so.getsockname()[1]
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
 
-    out = run_config(a, a.config, world, rank, local, dev, sharded, a.steps, a.warmup)
+    out = run_config(a, a.config, world, rank, local, dev, sharded, a.steps, a.warmup, a.dist)
+    keep = ("value", "unit", "ms_per_step", "steps", "warmup", "roofline", "sort_roofline",
+            "moved_roofline", "phases_ms", "check", "schedule", "config", "traffic_pmc")
+    default_line = world == 1 and not sharded and a.config == "c4" and not a.n and a.dist == "uniform"
     # the north star's own 1-GPU target (BASELINE.json: >= 60 % of the HBM roofline on 256 M
     # uniform uint32 keys) as a second leg of the same driver-timed run, after the headline
-    if world == 1 and not sharded and a.config == "c4" and not a.n and not a.no_north_star:
+    if default_line and not a.no_north_star:
         ns = run_config(a, "ns", world, rank, local, dev, sharded, a.steps, a.warmup)
         if out is not None and ns is not None:
-            out["north_star"] = {k: ns[k] for k in ("value", "unit", "ms_per_step", "steps",
-                                                    "warmup", "roofline", "sort_roofline",
-                                                    "phases_ms", "check", "schedule")}
-            out["north_star"]["config"] = ns["config"]
-            if "traffic_pmc" in ns:
-                out["north_star"]["traffic_pmc"] = ns["traffic_pmc"]
+            out["north_star"] = {k: ns[k] for k in keep if k in ns}
+    # the reference's own input (0..N-1 shuffled, main.cpp:119-125) at the north star's 2^28 and
+    # C4's 2^30 keys, through the default schedule (no PMC child runs, no CPU baseline)
+    if default_line and not a.no_reference_input:
+        legs = {}
+        for cfg in ("ns", "c4"):
+            r = run_config(a, cfg, world, rank, local, dev, sharded, a.steps, a.warmup, "perm",
+                           traffic=False, cpu=False)
+            if r is not None:
+                legs[cfg] = {k: r[k] for k in keep if k in r}
+        if out is not None:
+            out["reference_input"] = legs
     if out is not None:
         print(json.dumps(out), flush=True)
     if sharded:

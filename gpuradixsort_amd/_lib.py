@@ -75,6 +75,7 @@ SIGNATURES = [
     ("grs_create", c_int, [POINTER(c_void_p), c_size_t, c_int, c_int, c_int, c_int]),
     ("grs_destroy", None, [c_void_p]),
     ("grs_scratch_bytes", c_size_t, [c_void_p]),
+    ("grs_debug_check_guards", c_int, [c_void_p, POINTER(c_uint64)]),
     ("grs_rank_mode", c_int, [c_void_p]),
     ("grs_lds_order_check", c_int, [c_int, c_int, c_int, POINTER(c_ulonglong)]),
     ("grs_set_option", c_int, [c_void_p, c_int, c_int]),
@@ -117,6 +118,7 @@ SIGNATURES = [
     ("grs_iota_u32", c_int, [c_void_p, c_size_t, c_uint32, c_void_p]),
     ("grs_gather_records", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
     ("grs_fill_splitmix", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_void_p]),
+    ("grs_fill_permutation", c_int, [c_void_p, c_size_t, c_int, c_uint64, c_uint64, c_uint64, c_void_p]),
     ("grs_count_inversions", c_int, [c_void_p, c_size_t, c_int, POINTER(c_uint64), c_void_p]),
     ("grs_sort_host", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                               c_void_p]),

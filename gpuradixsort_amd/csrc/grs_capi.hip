@@ -18,6 +18,7 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "../../include/grs.h"
 #include "grs_config.h"
@@ -250,8 +251,9 @@ struct grs_sorter {
   bool alt_joint = false;          // u32 pairs: alt_vals lies inside alt_keys' allocation (8n bytes)
   int rec_mode = 2;                // GRS_OPT_RECORDS: 0 two arrays, 1 records in the scratch
                                    // only, 2 also split over the caller's arrays
-  uint32_t* status = nullptr;      // 2 x status_words
+  uint32_t* status = nullptr;      // 2 look-back status buffers: [status_words] | band | [status_words]
   size_t status_words = 0;         // per buffer
+  size_t status_stride = 0;        // words from the first buffer to the second
   uint32_t* ctrl = nullptr;        // GRS_CTRL_WORDS
   // run_sort's histogram + ticket block alternates between ctrl and ctrl2: cb[cb_i] is zero at
   // the start of the next call (each call's histogram kernel zeroes the other one for the
@@ -308,11 +310,84 @@ struct grs_sorter {
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
   int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
                                    // 2 = 1 with P2's regions refused (test hook: the exact redo)
+  // The MSD sort's scratch (msd_scratch): allocated at grs_create from kMsdMinN items of capacity,
+  // by grs_set_option(GRS_OPT_MSD, 1 | 2) below it; released by GRS_OPT_MSD = 0
   void* msd_buf = nullptr;         // the MSD sort's tables (u32 keys without payload, 8-bit)
-  void* alt2_keys = nullptr;       // the MSD sort's P2 regions (keys | payload)
+  void* alt2_keys = nullptr;       // the MSD sort's P2 regions (keys | guard band | payload)
   uint32_t* alt2_vals = nullptr;
   size_t msd_bytes = 0;
+  size_t alt_words = 0;            // elements per array of the second buffer (alt)
+  // Every device scratch allocation ends in a guard band of kGuardBytes (and allocations that
+  // hold several arrays have bands between them), filled with a pattern when allocated and
+  // checked by grs_debug_check_guards: a kernel that writes past a scratch array shows there.
+  struct ScratchBuf {
+    void** owner;                  // the sorter field holding the allocation
+    size_t bytes;                  // allocated bytes (bands included)
+    std::vector<size_t> bands;     // byte offsets of its guard bands
+  };
+  std::vector<ScratchBuf> bufs;
+  size_t alt_inner_band = 0;       // u32 pairs: the band between alt's keys and payload, which
+  bool alt_band_dirty = false;     // the LSD record passes write records across (restored by
+                                   // the next MSD sort or guard check)
 };
+
+namespace {
+
+// ---- scratch allocations with guard bands (grs_debug_check_guards) ----
+constexpr size_t kGuardBytes = 16384;
+constexpr uint32_t kGuardWord = 0x6A7DBA5Eu;
+
+hipError_t fill_band(void* at) {
+  static const std::vector<uint32_t> pattern(kGuardBytes / 4, kGuardWord);
+  return hipMemcpy(at, pattern.data(), kGuardBytes, hipMemcpyHostToDevice);
+}
+
+// Frees *p (if any) and forgets its guard bands.
+void sbuf_free(grs_sorter* s, void** p) {
+  for (size_t i = 0; i < s->bufs.size(); ++i)
+    if (s->bufs[i].owner == p) {
+      s->scratch_bytes -= s->bufs[i].bytes;
+      s->bufs.erase(s->bufs.begin() + static_cast<long>(i));
+      break;
+    }
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+}
+
+// *p = a new allocation (the old one freed first) of `bytes` for the caller followed by a guard
+// band; inner = byte offsets in [0, bytes) of further kGuardBytes bands the caller laid out
+// between its arrays.  On the current device.
+grs_status sbuf_alloc(grs_sorter* s, void** p, size_t bytes, const char* what,
+                      std::vector<size_t> inner = {}) {
+  sbuf_free(s, p);
+  void* d = nullptr;
+  if (hipMalloc(&d, bytes + kGuardBytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(GRS_ENOMEM, std::string(what) + ": hipMalloc of " + std::to_string(bytes + kGuardBytes) +
+                                   " bytes failed");
+  }
+  inner.push_back(bytes);
+  for (size_t o : inner)
+    if (fill_band(static_cast<char*>(d) + o) != hipSuccess) {
+      (void)hipFree(d);
+      return set_err(GRS_EHIP, std::string(what) + ": guard band fill failed");
+    }
+  *p = d;
+  s->bufs.push_back({p, bytes + kGuardBytes, inner});
+  s->scratch_bytes += bytes + kGuardBytes;
+  return GRS_OK;
+}
+
+// Device buffer grown on demand (contents are not kept).
+grs_status grow_buf(grs_sorter* s, void** p, size_t* have, size_t need, const char* what) {
+  if (*have >= need && *p) return GRS_OK;
+  *have = 0;
+  const grs_status r = sbuf_alloc(s, p, need, what);
+  if (r == GRS_OK) *have = need;
+  return r;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -339,24 +414,17 @@ void grs_destroy(grs_sorter* s) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(s->device);
-  if (s->alt_keys) (void)hipFree(s->alt_keys);
-  if (s->alt_vals && !s->alt_joint) (void)hipFree(s->alt_vals);
-  if (s->status) (void)hipFree(s->status);
-  if (s->ctrl) (void)hipFree(s->ctrl);
-  if (s->ctrl2) (void)hipFree(s->ctrl2);
+  // every device scratch allocation (alt, alt2, status, control blocks, tables, the grown
+  // buffers) is registered with its guard bands
+  for (grs_sorter::ScratchBuf& b : s->bufs)
+    if (*b.owner) {
+      (void)hipFree(*b.owner);
+      *b.owner = nullptr;
+    }
+  s->bufs.clear();
   if (s->h_err) (void)hipHostFree(s->h_err);
-  if (s->seg_buf) (void)hipFree(s->seg_buf);
   if (s->seg64) grs_destroy(s->seg64);
-  if (s->host_stage) (void)hipFree(s->host_stage);
-  if (s->shard_buf) (void)hipFree(s->shard_buf);
-  if (s->rec_buf) (void)hipFree(s->rec_buf);
-  if (s->rec_kbuf) (void)hipFree(s->rec_kbuf);
   if (s->shard_host) (void)hipHostFree(s->shard_host);
-  if (s->xbuf) (void)hipFree(s->xbuf);
-  if (s->xrbuf) (void)hipFree(s->xrbuf);
-  if (s->codec_buf) (void)hipFree(s->codec_buf);
-  if (s->msd_buf) (void)hipFree(s->msd_buf);
-  if (s->alt2_keys) (void)hipFree(s->alt2_keys);
   for (int i = 0; s->ev && i < s->ring * grs_sorter::EV_PER_CALL; ++i)
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   for (hipEvent_t e : s->xev)
@@ -420,6 +488,7 @@ struct MsdLayout {   // word offsets into msd_buf
   size_t h2, h2x, h2s, big, spill2, mid, clear, dstart, reg, room, len2, in2, out2, tab, hdr2, rec2, hdr2r, rec2r,
       hdrf, recf, bin, bstart, blen, brow, rows, spill, words;
   size_t r2, rf, bl, mr;   // capacities: P2 records, fallback records, big list, histogram rows
+  std::vector<size_t> bands;   // byte offsets of the guard bands between the tables
   // nd: digits of the fallback (2 for u32 keys, 6 for u64)
   static MsdLayout of(size_t cap, size_t nd) {
     MsdLayout L{};
@@ -429,7 +498,16 @@ struct MsdLayout {   // word offsets into msd_buf
     L.mr = cap / (kMsdTileMin + 1) + 2;
     L.rf = cap / kMsdTileMin + L.bl + 1;
     size_t o = 0;
-    auto take = [&](size_t w) { const size_t at = o; o += (w + 63) & ~static_cast<size_t>(63); return at; };
+    // every table followed by a guard band (the last one's is sbuf_alloc's own)
+    auto take = [&](size_t w) {
+      if (o != 0) {
+        L.bands.push_back(o * 4);
+        o += kGuardBytes / 4;
+      }
+      const size_t at = o;
+      o += (w + 63) & ~static_cast<size_t>(63);
+      return at;
+    };
     // h2 (P2's digit totals) | h2x (exact counts, after a P2 spill) | h2s (sampled counts) |
     // big counters, P2's spill flag | mid list: the first `clear` words zeroed by the sample kernel
     L.h2 = take(3 * 65536 + 64 + 2 + 3 * 65536);
@@ -482,6 +560,9 @@ size_t msd_alt2_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 4 + 
 bool msd_type(const grs_sorter* s) {
   return s->radix_bits == 8 && !(s->key_type == GRS_KEY_U64 && s->pairs);
 }
+// From this many keys the MSD sort is the default (GRS_OPT_MSD = -1), and a sorter of this
+// capacity allocates its scratch at grs_create.
+constexpr size_t kMsdMinN = size_t(3) << 24;   // MSD vs LSD, same box (r5 s12-13): 2^25 84 vs 88, 2^26 106 vs 96 Gkeys/s
 size_t msd_digits(const grs_sorter* s) { return s->key_type == GRS_KEY_U64 ? 6 : 2; }
 
 // Status words one pass of a sort of up to `cap` items can need (largest over the shapes).
@@ -513,6 +594,70 @@ size_t needed_status_words(const grs_sorter* s) {
     w = s->pairs ? max_status_words<uint64_t, true>(s, cap, radix)
                  : max_status_words<uint64_t, false>(s, cap, radix);
   return msd_type(s) ? std::max(w, MsdLayout::status_words(cap)) : w;
+}
+
+// The two look-back status buffers, `words` each, a guard band between them.
+grs_status alloc_status(grs_sorter* s, size_t words) {
+  const size_t stride = words + kGuardBytes / 4;
+  const grs_status r = sbuf_alloc(s, reinterpret_cast<void**>(&s->status), (stride + words) * 4,
+                                  "look-back status buffers", {words * 4});
+  if (r != GRS_OK) return r;
+  s->status_words = words;
+  s->status_stride = stride;
+  return GRS_OK;
+}
+
+// The second buffer: `words` elements per array.  u32 pairs: ONE allocation, keys | guard band |
+// payload (the LSD record passes write n 8-byte records from its start, across the band:
+// alt_band_dirty); otherwise keys, and the payload in an allocation of its own.
+grs_status alloc_alt(grs_sorter* s, size_t words) {
+  const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  grs_status r;
+  if (s->pairs && s->key_type == GRS_KEY_U32) {
+    r = sbuf_alloc(s, &s->alt_keys, (2 * words) * 4 + kGuardBytes, "second buffer", {words * 4});
+    if (r != GRS_OK) return r;
+    s->alt_vals = reinterpret_cast<uint32_t*>(static_cast<char*>(s->alt_keys) + words * 4 + kGuardBytes);
+    s->alt_joint = true;
+    s->alt_inner_band = words * 4;
+    s->alt_band_dirty = false;
+  } else {
+    r = sbuf_alloc(s, &s->alt_keys, words * kb, "second buffer");
+    if (r == GRS_OK && s->pairs) r = sbuf_alloc(s, reinterpret_cast<void**>(&s->alt_vals), words * 4, "second buffer");
+    if (r != GRS_OK) return r;
+  }
+  s->alt_words = words;
+  return GRS_OK;
+}
+
+// The MSD sort's scratch on (alt grown to msd_alt_words(capacity) elements per array, the region
+// buffer alt2 and the tables msd_buf) or off (released, alt back to capacity elements).
+// Synchronises the device when it changes anything.
+grs_status msd_scratch(grs_sorter* s, bool on) {
+  const size_t cap = std::max<size_t>(s->capacity, 1);
+  const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
+  const size_t altw = on ? msd_alt_words(cap) : cap;
+  const bool change = (s->msd_buf != nullptr) != on || s->alt_words != altw;
+  if (!change) return GRS_OK;
+  (void)hipDeviceSynchronize();   // in-flight sorts may still use the buffers replaced here
+  if (!on) {
+    sbuf_free(s, &s->msd_buf);
+    sbuf_free(s, &s->alt2_keys);
+    s->alt2_vals = nullptr;
+    s->msd_bytes = 0;
+    return s->alt_words == cap && s->alt_keys ? GRS_OK : alloc_alt(s, cap);
+  }
+  grs_status r = alloc_alt(s, altw);
+  if (r != GRS_OK) return r;
+  const MsdLayout L = MsdLayout::of(cap, msd_digits(s));
+  s->msd_bytes = L.words * 4;
+  r = sbuf_alloc(s, &s->msd_buf, s->msd_bytes, "MSD tables", L.bands);
+  if (r != GRS_OK) return r;
+  const size_t w2 = msd_alt2_words(cap);
+  r = sbuf_alloc(s, &s->alt2_keys, w2 * kb + kGuardBytes + (s->pairs ? w2 * 4 : 0), "MSD region buffer",
+                 {w2 * kb});
+  if (r != GRS_OK) return r;
+  if (s->pairs) s->alt2_vals = reinterpret_cast<uint32_t*>(static_cast<char*>(s->alt2_keys) + w2 * kb + kGuardBytes);
+  return GRS_OK;
 }
 
 }  // namespace
@@ -588,17 +733,18 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
     int prev = 0;
     GRS_HIP(hipGetDevice(&prev));
     GRS_HIP(hipSetDevice(s->device));
-    uint32_t* st = nullptr;
-    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&st), 2 * words * 4);
+    (void)hipDeviceSynchronize();   // earlier sorts may still use the old buffers
+    const grs_status r = alloc_status(s, words);
     (void)hipSetDevice(prev);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      return set_err(GRS_ENOMEM, "grs_set_option: status buffer allocation failed");
-    }
-    if (s->status) (void)hipFree(s->status);
-    s->scratch_bytes += 2 * (words - s->status_words) * 4;
-    s->status = st;
-    s->status_words = words;
+    if (r != GRS_OK) return r;
+  }
+  if (opt == GRS_OPT_MSD) {   // allocate or release the MSD sort's scratch
+    int prev = 0;
+    GRS_HIP(hipGetDevice(&prev));
+    GRS_HIP(hipSetDevice(s->device));
+    const grs_status r = msd_scratch(s, value != 0 && msd_type(s) && (value != -1 || s->capacity >= kMsdMinN));
+    (void)hipSetDevice(prev);
+    if (r != GRS_OK) return r;
   }
   return GRS_OK;
 }
@@ -651,43 +797,20 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
   (void)hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device);
   const size_t kb = key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t cap = std::max<size_t>(capacity, 1);
-  s->status_words = needed_status_words(s);
-  grs_status st = GRS_OK;
-  auto alloc = [&](void** p, size_t bytes) {
-    if (st != GRS_OK) return;
-    if (hipMalloc(p, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      st = set_err(GRS_ENOMEM, "grs_create: hipMalloc of " + std::to_string(bytes) + " bytes failed");
-      return;
-    }
-    s->scratch_bytes += bytes;
-  };
-  if (s->pairs && key_type == GRS_KEY_U32) {
-    // one allocation: keys | payload, or the same bytes as 8-byte (key, value) records (the
-    // record passes of run_sort); each array with the MSD sort's region slack
-    const size_t half = msd_type(s) ? msd_alt_words(cap) : cap;
-    alloc(&s->alt_keys, half * 8);
-    if (st == GRS_OK) s->alt_vals = static_cast<uint32_t*>(s->alt_keys) + half;
-    s->alt_joint = true;
-  } else if (msd_type(s)) {
-    alloc(&s->alt_keys, msd_alt_words(cap) * kb);   // + the MSD sort's region slack
-  } else {
-    alloc(&s->alt_keys, cap * kb);
-    if (s->pairs) alloc(reinterpret_cast<void**>(&s->alt_vals), cap * 4);
-  }
-  alloc(reinterpret_cast<void**>(&s->status), 2 * s->status_words * 4);
-  if (msd_type(s)) {
-    s->msd_bytes = MsdLayout::of(cap, msd_digits(s)).words * 4;
-    alloc(&s->msd_buf, s->msd_bytes);
-    const size_t w2 = msd_alt2_words(cap);
-    alloc(&s->alt2_keys, w2 * (kb + (s->pairs ? 4 : 0)));
-    if (st == GRS_OK && s->pairs) s->alt2_vals = reinterpret_cast<uint32_t*>(static_cast<char*>(s->alt2_keys) + w2 * kb);
-  }
-  alloc(reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4);
-  alloc(reinterpret_cast<void**>(&s->ctrl2), GRS_CTRL_ERROR * 4);
+  (void)kb;
+  grs_status st = alloc_status(s, needed_status_words(s));
+  if (st == GRS_OK) st = sbuf_alloc(s, reinterpret_cast<void**>(&s->ctrl), GRS_CTRL_WORDS * 4, "grs_create: control block");
+  if (st == GRS_OK) st = sbuf_alloc(s, reinterpret_cast<void**>(&s->ctrl2), GRS_CTRL_ERROR * 4, "grs_create: control block");
   if (st == GRS_OK && (hipMemset(s->ctrl, 0, GRS_CTRL_WORDS * 4) != hipSuccess ||
                        hipMemset(s->ctrl2, 0, GRS_CTRL_ERROR * 4) != hipSuccess))
     st = set_err(GRS_EHIP, "grs_create: hipMemset failed");
+  // the second buffer and, from kMsdMinN items of capacity (where the MSD sort is the default),
+  // the MSD sort's scratch; if that does not fit, the sorter runs the LSD passes (no MSD
+  // scratch: 1 n of elements instead of ~2.4 n)
+  if (st == GRS_OK) {
+    if (msd_type(s) && cap >= kMsdMinN && msd_scratch(s, true) != GRS_OK) (void)msd_scratch(s, false);
+    if (!s->alt_keys) st = alloc_alt(s, cap);
+  }
   if (st == GRS_OK && hipHostMalloc(reinterpret_cast<void**>(&s->h_err), 4, hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     st = set_err(GRS_ENOMEM, "grs_create: hipHostMalloc failed");
@@ -702,6 +825,38 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
 }
 
 size_t grs_scratch_bytes(const grs_sorter* s) { return s ? s->scratch_bytes : 0; }
+
+grs_status grs_debug_check_guards(grs_sorter* s, uint64_t* bad_words) {
+  if (!s || !bad_words) return set_err(GRS_EINVAL, "grs_debug_check_guards: NULL argument");
+  *bad_words = 0;
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  GRS_HIP(hipSetDevice(s->device));
+  grs_status r = GRS_OK;
+  if (hipDeviceSynchronize() != hipSuccess) r = set_err(GRS_EHIP, "grs_debug_check_guards: synchronise");
+  std::vector<uint32_t> h(kGuardBytes / 4);
+  uint64_t bad = 0;
+  for (const grs_sorter::ScratchBuf& b : s->bufs) {
+    if (r != GRS_OK || !*b.owner) continue;
+    for (size_t o : b.bands) {
+      char* at = static_cast<char*>(*b.owner) + o;
+      // alt's inner band after an LSD record sort holds records, legitimately: restored, not counted
+      const bool records = b.owner == &s->alt_keys && o == s->alt_inner_band && s->alt_band_dirty;
+      if (hipMemcpy(h.data(), at, kGuardBytes, hipMemcpyDeviceToHost) != hipSuccess) {
+        r = set_err(GRS_EHIP, "grs_debug_check_guards: read-back");
+        break;
+      }
+      uint64_t c = 0;
+      for (uint32_t w : h) c += w != kGuardWord;
+      if (!records) bad += c;
+      if (c != 0 && fill_band(at) != hipSuccess) r = set_err(GRS_EHIP, "grs_debug_check_guards: restore");
+    }
+  }
+  if (r == GRS_OK) s->alt_band_dirty = false;
+  *bad_words = bad;
+  (void)hipSetDevice(prev);
+  return r;
+}
 
 int grs_rank_mode(const grs_sorter* s) { return s ? s->rank_mode : -1; }
 
@@ -750,7 +905,8 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
                        uint32_t expect_tile = 0) {
   const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
   if (status_words_for(tiles, 1u << RB) > s->status_words)
-    return set_err(GRS_ECAPACITY, "status buffer too small");
+    return set_err(GRS_ECAPACITY, "status buffer too small (pass: " + std::to_string(tiles) + " tiles, have " +
+                                      std::to_string(s->status_words) + " words)");
   if (expect_tile != 0 && expect_tile != static_cast<uint32_t>(Tile::TILE))
     return set_err(GRS_EINVAL, "internal: pass tile differs from the zeroed status layout");
   if constexpr (PERSIST) {
@@ -812,9 +968,11 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   // the persistent pass prefetches into the registers a two-round reorder still needs
   const bool persist = !xl && !Big::TWO_ROUNDS && use_persistent(s, tiles, RB);
   const size_t words = status_words_for(tiles, RADIX);
-  if (words > s->status_words) return set_err(GRS_ECAPACITY, "status buffer too small");
+  if (words > s->status_words)
+    return set_err(GRS_ECAPACITY, "status buffer too small (LSD: n " + std::to_string(n) + ", " +
+                                      std::to_string(words) + " words, have " + std::to_string(s->status_words) + ")");
   uint32_t* st0 = s->status;
-  uint32_t* st1 = s->status + s->status_words;
+  uint32_t* st1 = s->status + s->status_stride;
   uint32_t* const cb[2] = {s->ctrl, s->ctrl2};
   uint32_t* hist = cb[s->cb_i];
   uint32_t* tickets = hist + GRS_CTRL_TICKETS;
@@ -869,6 +1027,7 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
   constexpr bool kRecType = sizeof(K) == 4 && PAIRS && RB == 8;
   const bool rec = kRecType && big && !src_in && (passes & 1) == 0 && s->alt_joint &&
                    s->rec_mode != 0 && s->rank_mode == 0;
+  if (rec) s->alt_band_dirty = true;   // records run across alt's inner guard band
   // even n, 4+ passes: the middle passes also write records, split over the caller's two
   // arrays (records [0, n/2) in keys, [n/2, n) in vals), so every pass but the last writes
   // records.  Pass p's record flags: 0 = none, 1 = write, 2 = read, 3 = read split + write,
@@ -984,8 +1143,6 @@ int msd_local_shape(size_t n, size_t elem) {
   if (elem == 4 && need <= MsdLocalC::SMAX) return 3;
   return 0;
 }
-// From this many keys the MSD sort is the default (GRS_OPT_MSD = -1).
-constexpr size_t kMsdMinN = size_t(3) << 24;   // MSD vs LSD, same box (r5 s12-13): 2^25 84 vs 88, 2^26 106 vs 96 Gkeys/s
 
 bool use_msd(const grs_sorter* s, size_t n, int begin_bit, int end_bit) {
   if (!msd_type(s) || s->msd_mode == 0 || s->msd_buf == nullptr || s->rank_mode != 0) return false;
@@ -1021,7 +1178,9 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   const size_t t2 = n / tile2 + 257;
   const size_t words2 = (t2 + 2 * (t2 / G + 257)) * 256;
   if (words1 > s->status_words || words2 > s->status_words)
-    return set_err(GRS_ECAPACITY, "status buffer too small");
+    return set_err(GRS_ECAPACITY, "status buffer too small (MSD: n " + std::to_string(n) + ", P1 " +
+                                      std::to_string(words1) + " / P2 " + std::to_string(words2) + " words, have " +
+                                      std::to_string(s->status_words) + ")");
   const MsdLayout L = MsdLayout::of(s->capacity, ND);
   if (t2 > L.r2) return set_err(GRS_ECAPACITY, "internal: MSD plan capacity");
   uint32_t* const mb = static_cast<uint32_t*>(s->msd_buf);
@@ -1033,7 +1192,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   uint32_t* const hdrf = mb + L.hdrf;
   auto* const recf = reinterpret_cast<grs::SegTile*>(mb + L.recf);
   uint32_t* const rows = mb + L.rows;
-  uint32_t* const st[2] = {s->status, s->status + s->status_words};
+  uint32_t* const st[2] = {s->status, s->status + s->status_stride};
   uint32_t* const err = s->ctrl + GRS_CTRL_ERROR;
   uint32_t* const cb[2] = {s->ctrl, s->ctrl2};
   uint32_t* const hist = cb[s->cb_i];
@@ -1054,6 +1213,11 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   uint32_t* const samp = hist;
   uint32_t* const exact = hist + 256;
   uint32_t* const totals = hist + 512;
+  // the keys' span and the top digit's shift (grs_msd.hpp GRS_MSD_SPAN): every digit below reads
+  // its shift from span[4] (P1 and its redo: the top digit; H2, P2 and its redo: the byte below
+  // it; P3: the rounds below the 16-bit prefix)
+  uint32_t* const span = hist + GRS_MSD_SPAN;
+  const uint32_t* const top = span + 4;
   // P1's regions: R_d = sample_d * n * 9/8 / sampled + pad (the sample reads every key up to
   // 2^20 keys: exact counts, no pad needed)
   const uint64_t sampled = std::min<uint64_t>(n, uint64_t(GRS_MSD_SAMPLE_CHUNKS) * GRS_WAVE);
@@ -1100,25 +1264,30 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   if ((r = mark()) != GRS_OK) return r;
   if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = false;
+  if (s->alt_band_dirty) {   // an LSD record sort wrote across alt's inner guard band: restore it
+    GRS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(static_cast<char*>(s->alt_keys) + s->alt_inner_band),
+                              static_cast<int>(kGuardWord), kGuardBytes / 4, stream));
+    s->alt_band_dirty = false;
+  }
   // sample: the top byte's histogram; zeroes P1's status, the next call's control block, h2
   // and the big-segment counters
   hipLaunchKernelGGL((grs::grs_msd_sample<K>), dim3(1024), dim3(256), 0, stream, src, n, samp, st[0],
-                     static_cast<uint32_t>(words1), hist_next, h2, static_cast<uint32_t>(L.clear));
+                     static_cast<uint32_t>(words1), hist_next, h2, static_cast<uint32_t>(L.clear), span);
   GRS_HIP(hipGetLastError());
   s->cb_i ^= 1;
   if ((r = mark()) != GRS_OK) return r;
-  // P1: stable scatter by the top byte into the sampled regions, src -> alt (no counting read)
-  const Dig d1{KB - 8, 255u};
+  // P1: stable scatter by the top digit (the sample's guess of it) into the sampled regions,
+  // src -> alt (no counting read); its tiles OR the keys into span[0..3]
+  const Dig d1{0, 255u};   // (+ *top)
   GRS_DIAG_SET(region_len, n);
   {
     const uint32_t tiles = (n + tile1 - 1) / tile1;
     auto go = [&](auto tshape, auto optc) {
       using T = decltype(tshape);
       constexpr uint32_t opt = decltype(optc)::value;
-      hipLaunchKernelGGL((grs::grs_onesweep_region<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, opt, FT::TILE>),
+      hipLaunchKernelGGL((grs::grs_onesweep_region<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, opt>),
                          dim3(tiles), dim3(T::BLOCK), 0, stream, src, alt, vsrc, valt, n, d1, samp, mult,
-                         pad, static_cast<uint32_t>(region_len), tickets, st[0], st[1], err, totals,
-                         recf, hdrf);
+                         pad, static_cast<uint32_t>(region_len), tickets, st[0], st[1], err, totals, span);
     };
     if (xl) go(XL{}, std::integral_constant<uint32_t, XL::OPT>{});
     else if (big) go(Big{}, std::integral_constant<uint32_t, Big::OPT>{});
@@ -1126,14 +1295,18 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
     GRS_HIP(hipGetLastError());
   }
   if ((r = mark()) != GRS_OK) return r;
-  // a run outgrew its region: P1 again into the exact layout (P1's last tile planned it: exact
-  // counts, persistent scatter); without a spill the two launches leave at once
+  // the exact span checks the guessed top digit; a run that outgrew its region or a varying bit
+  // above the guess: P1 again into the exact layout at the exact digit (grs_msd_span plans it:
+  // exact counts, persistent scatter); otherwise the two launches leave at once
+  hipLaunchKernelGGL((grs::grs_msd_span<K, FT::TILE>), dim3(1), dim3(256), 0, stream, n, span, totals, recf, hdrf);
+  GRS_HIP(hipGetLastError());
   hipLaunchKernelGGL((grs::grs_seg_hist<K, 1>), dim3(2 * s->cus), dim3(256), 0, stream, src, recf, hdrf,
-                     KB - 8, exact, st[0], 256u);
+                     0, exact, st[0], 256u, top);
   GRS_HIP(hipGetLastError());
   hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, FT::BLOCK, FT::ITEMS, FT::MINW, FT::OPT, true>),
                      dim3(s->cus), dim3(FT::BLOCK), 0, stream, src, alt, vsrc, valt, d1, recf, hdrf,
-                     exact, 256u, tickets + 15 * GRS_XCDS, st[0], st[1], err, nullptr);
+                     exact, 256u, tickets + 15 * GRS_XCDS, st[0], st[1], err, nullptr, nullptr, nullptr,
+                     nullptr, top);
   GRS_HIP(hipGetLastError());
   GRS_DIAG_CHECK("P1");
   if ((r = mark()) != GRS_OK) return r;
@@ -1168,7 +1341,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
     GRS_HIP(hipGetLastError());
     hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
                        shift ? mb + L.h2s : h2x, st[1], static_cast<uint32_t>(words2), tab, chunk, shift,
-                       (const uint32_t*)nullptr);
+                       (const uint32_t*)nullptr, top);
     GRS_HIP(hipGetLastError());
     if (shift) {
       uint32_t* const room = mb + L.room;
@@ -1189,7 +1362,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // the region starts (dstart) and its last the totals (h2) and the spill flag; after a spill
   // (or for small sorts, always) the exact pass alt -> keys from H2's exact counts (h2x).
   {
-    const Dig d2{KB - 16, 255u};
+    const Dig d2{-8, 255u};   // the byte below the top digit (+ *top)
     const dim3 grid(static_cast<uint32_t>(t2));
     constexpr uint32_t RG = 131072;
     auto go = [&](auto tshape) -> grs_status {
@@ -1199,18 +1372,18 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
         GRS_DIAG_SET(cap2, region_len);
         hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT | RG, false>),
                            grid, dim3(T::BLOCK), 0, stream, alt, rk, valt, rv, d2, rec2r, hdr2r, reg, 256u,
-                           tickets + GRS_XCDS, st[1], st[0], err, dstart, h2, spill2, (const uint32_t*)nullptr);
+                           tickets + GRS_XCDS, st[1], st[0], err, dstart, h2, spill2, (const uint32_t*)nullptr, top);
         GRS_HIP(hipGetLastError());
         GRS_DIAG_CHECK("P2region");
         GRS_DIAG_SET(n, region_len);
         // the redo: exact counts, then the exact pass in place (persistent, gated by the flag)
         hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
-                           st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2);
+                           st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2, top);
         GRS_HIP(hipGetLastError());
         hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, true>),
                            dim3(s->cus), dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x,
                            256u, tickets + 14 * GRS_XCDS, st[0], st[1], err, (uint32_t*)nullptr,
-                           (uint32_t*)nullptr, (uint32_t*)nullptr, spill2);
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, spill2, top);
         GRS_HIP(hipGetLastError());
       } else {
         // no sample: the exact pass straight away (the flag says so to P3: in place)
@@ -1218,7 +1391,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
         hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, false>), grid,
                            dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x, 256u,
                            tickets + GRS_XCDS, st[1], st[0], err, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                           (uint32_t*)nullptr, (const uint32_t*)nullptr);
+                           (uint32_t*)nullptr, (const uint32_t*)nullptr, top);
         GRS_HIP(hipGetLastError());
       }
       return GRS_OK;
@@ -1239,13 +1412,14 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   const uint32_t mid_max = P3L::SMAX > P3C::SMAX ? P3L::SMAX : P3C::SMAX;
   hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
                      dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
-                     mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows);
+                     mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows, top);
   GRS_HIP(hipGetLastError());
   if (P3L::SMAX > P3C::SMAX) {
     constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
     constexpr int minw = per_cu * P3L::BLOCK / GRS_WAVE / 4;
     hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw>),
-                       dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.mid);
+                       dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.mid,
+                       top);
     GRS_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
@@ -1345,11 +1519,11 @@ grs_status run_partition_n(grs_sorter* s, const K* keys, const uint32_t* vals, K
   if (s->rank_mode == 0)
     r = launch_pass<K, PAIRS, 4, T, kSmallOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
                                              s->ctrl + GRS_CTRL_TICKETS, s->status,
-                                             s->status + s->status_words, stream);
+                                             s->status + s->status_stride, stream);
   else
     r = launch_pass<K, PAIRS, 4, T, kMatchOpt>(s, keys, keys_out, vals, vals_out, n, dig, dig_dev, hist,
                                               s->ctrl + GRS_CTRL_TICKETS, s->status,
-                                              s->status + s->status_words, stream);
+                                              s->status + s->status_stride, stream);
   if (r != GRS_OK) return r;
   if (region) {
     const uint32_t groups = (tiles + GRS_LB_GROUP - 1) / GRS_LB_GROUP;
@@ -1641,6 +1815,32 @@ grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t see
   return GRS_OK;
 }
 
+grs_status grs_fill_permutation(void* d_keys, size_t n, int key_bytes, uint64_t total, uint64_t seed,
+                                 uint64_t first_index, void* stream) {
+  if (n == 0) return GRS_OK;
+  if (!d_keys || (key_bytes != 4 && key_bytes != 8) || total == 0 || first_index > total ||
+      n > total - first_index || (key_bytes == 4 && total > (uint64_t(1) << 32)) || total > (uint64_t(1) << 62))
+    return set_err(GRS_EINVAL, "grs_fill_permutation: bad argument");
+  grs::PermParams p{};
+  int b = 1;
+  while (b < 62 && (uint64_t(1) << b) < total) ++b;
+  p.mask = (uint64_t(1) << b) - 1;
+  p.half = b / 2 + 1;
+  for (int r = 0; r < 4; ++r) {
+    p.a[r] = grs::splitmix64(seed + 2 * r) | 1u;
+    p.c[r] = grs::splitmix64(seed + 2 * r + 1);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (key_bytes == 4)
+    hipLaunchKernelGGL(grs::grs_fill_permutation<uint32_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<uint32_t*>(d_keys), static_cast<uint64_t>(n), total, first_index, p);
+  else
+    hipLaunchKernelGGL(grs::grs_fill_permutation<uint64_t>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                       static_cast<uint64_t*>(d_keys), static_cast<uint64_t>(n), total, first_index, p);
+  GRS_HIP(hipGetLastError());
+  return GRS_OK;
+}
+
 grs_status grs_count_inversions(const void* d_keys, size_t n, int key_bytes, uint64_t* out_count,
                                 void* stream) {
   if (!out_count || (key_bytes != 4 && key_bytes != 8))
@@ -1772,17 +1972,8 @@ static grs_status sort_segmented_few(grs_sorter* s, void* d_keys, uint32_t* d_va
   if (hipMemcpyAsync(off, d_offsets, (num_segments + 1) * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     r = set_err(GRS_EHIP, "grs_sort_segmented: offsets");
-  if (r == GRS_OK && !d_vals && s->seg_bytes < n * 4) {   // the keys-only rider
-    if (s->seg_buf) (void)hipFree(s->seg_buf);
-    s->seg_buf = nullptr;
-    s->seg_bytes = 0;
-    if (hipMalloc(&s->seg_buf, n * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      r = set_err(GRS_ENOMEM, "grs_sort_segmented: scratch allocation failed");
-    } else {
-      s->seg_bytes = n * 4;
-    }
-  }
+  if (r == GRS_OK && !d_vals)   // the keys-only rider
+    r = grow_buf(s, &s->seg_buf, &s->seg_bytes, n * 4, "grs_sort_segmented: scratch");
   for (int g = 0; g < num_segments && r == GRS_OK; ++g) {
     const uint32_t lo = off[g], hi = off[g + 1];
     if (hi <= lo + 1) continue;
@@ -1809,18 +2000,7 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
   auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
   const size_t scan_bytes = grs_scan_scratch_bytes(n);
   const size_t need = al(n * 8) + 2 * al(n * 4) + al(scan_bytes);
-  grs_status r = GRS_OK;
-  if (s->seg_bytes < need) {
-    if (s->seg_buf) (void)hipFree(s->seg_buf);
-    s->seg_buf = nullptr;
-    s->seg_bytes = 0;
-    if (hipMalloc(&s->seg_buf, need) != hipSuccess) {
-      (void)hipGetLastError();
-      r = set_err(GRS_ENOMEM, "grs_sort_segmented: scratch allocation failed");
-    } else {
-      s->seg_bytes = need;
-    }
-  }
+  grs_status r = grow_buf(s, &s->seg_buf, &s->seg_bytes, need, "grs_sort_segmented: scratch");
   if (r == GRS_OK && (!s->seg64 || s->seg64->capacity < n)) {
     if (s->seg64) grs_destroy(s->seg64);
     s->seg64 = nullptr;
@@ -1868,7 +2048,6 @@ static grs_status sort_segmented_u32(grs_sorter* s, void* d_keys, uint32_t* d_va
 }  // extern "C"
 
 namespace {
-grs_status grow_buf(void** p, size_t* have, size_t need, const char* what);
 
 // Segments of any length (round 5): a segmented LSD over the segment table -- one planner
 // block (tiles never straddle a segment; a segment of one tile is solo), one histogram launch
@@ -1890,7 +2069,7 @@ grs_status sort_segmented_seg(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n
   auto al = [](size_t w) { return (w + 63) & ~static_cast<size_t>(63); };
   const size_t o_rec = 64, o_rows = o_rec + al(tiles_max * 8), o_st0 = o_rows + al(multi_max * ND * 256);
   const size_t o_st1 = o_st0 + al(sw), o_spill = o_st1 + al(sw), words = o_spill + al(6 * (size_t(nseg) + 1));
-  grs_status r = grow_buf(&s->seg_buf, &s->seg_bytes, words * 4, "grs_sort_segmented");
+  grs_status r = grow_buf(s, &s->seg_buf, &s->seg_bytes, words * 4, "grs_sort_segmented");
   if (r != GRS_OK) return r;
   uint32_t* const b = static_cast<uint32_t*>(s->seg_buf);
   uint32_t* const hdr = b;
@@ -1962,7 +2141,7 @@ grs_status sort_segmented_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n
   const size_t o_rowf = o_brw + al(bcap), o_recf = o_rowf + al(mr * NDF * 256);
   const size_t o_st0 = o_recf + al((n / TF + bcap + 1) * 8), o_st1 = o_st0 + al(sw);
   const size_t o_spill = o_st1 + al(sw), words = o_spill + al(6 * (std::max<size_t>(nseg, bcap) + 1));
-  grs_status r = grow_buf(&s->seg_buf, &s->seg_bytes, words * 4, "grs_sort_segmented");
+  grs_status r = grow_buf(s, &s->seg_buf, &s->seg_bytes, words * 4, "grs_sort_segmented");
   if (r != GRS_OK) return r;
   uint32_t* const b = static_cast<uint32_t*>(s->seg_buf);
   uint32_t* const hdr = b;
@@ -2175,18 +2354,7 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   // perm | pos | vals_out | segment keys (reused for the gathered keys), 256-B aligned parts
   auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
   const size_t need = 3 * al(n * 4) + al(n * kb);
-  grs_status r = GRS_OK;
-  if (s->seg_bytes < need) {
-    if (s->seg_buf) (void)hipFree(s->seg_buf);
-    s->seg_buf = nullptr;
-    s->seg_bytes = 0;
-    if (hipMalloc(&s->seg_buf, need) != hipSuccess) {
-      (void)hipGetLastError();
-      r = set_err(GRS_ENOMEM, "grs_sort_segmented: scratch allocation failed");
-    } else {
-      s->seg_bytes = need;
-    }
-  }
+  grs_status r = grow_buf(s, &s->seg_buf, &s->seg_bytes, need, "grs_sort_segmented: scratch");
   char* b = static_cast<char*>(s->seg_buf);
   uint32_t* perm = reinterpret_cast<uint32_t*>(b);
   uint32_t* pos = reinterpret_cast<uint32_t*>(b + al(n * 4));
@@ -2249,18 +2417,7 @@ grs_status grs_sort_host(grs_sorter* s, const void* h_keys_in, void* h_keys_out,
   const size_t kb = s->key_type == GRS_KEY_U64 ? 8 : 4;
   const size_t kbytes = (n * kb + 255) & ~static_cast<size_t>(255);
   const size_t need = kbytes + (s->pairs ? n * 4 : 0);
-  grs_status r = GRS_OK;
-  if (s->host_stage_bytes < need) {
-    if (s->host_stage) (void)hipFree(s->host_stage);
-    s->host_stage = nullptr;
-    s->host_stage_bytes = 0;
-    if (hipMalloc(&s->host_stage, need) != hipSuccess) {
-      (void)hipGetLastError();
-      r = set_err(GRS_ENOMEM, "grs_sort_host: staging allocation failed");
-    } else {
-      s->host_stage_bytes = need;
-    }
-  }
+  grs_status r = grow_buf(s, &s->host_stage, &s->host_stage_bytes, need, "grs_sort_host: staging");
   char* dk = static_cast<char*>(s->host_stage);
   uint32_t* dv = s->pairs ? reinterpret_cast<uint32_t*>(dk + kbytes) : nullptr;
   if (r == GRS_OK && hipMemcpyAsync(dk, h_keys_in, n * kb, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -2371,15 +2528,9 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   const int W = g + 3;   // words per rank in the count all-gather: counts + verdict
   const size_t need = al(S * sizeof(K)) + al(S * 4) + al(gs * sizeof(K)) + al(gs * 4) + al(4 * W) +
                       al(static_cast<size_t>(g) * W * 4) + al(sizeof(Dig));
-  if (s->shard_bytes < need) {
-    if (s->shard_buf) (void)hipFree(s->shard_buf);
-    s->shard_buf = nullptr;
-    s->shard_bytes = 0;
-    if (hipMalloc(&s->shard_buf, need) != hipSuccess) {
-      (void)hipGetLastError();
-      return set_err(GRS_ENOMEM, "grs_sort_sharded: scratch allocation failed");
-    }
-    s->shard_bytes = need;
+  {
+    const grs_status r = grow_buf(s, &s->shard_buf, &s->shard_bytes, need, "grs_sort_sharded: scratch");
+    if (r != GRS_OK) return r;
   }
   if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), kShardHostWords * 4,
                                       hipHostMallocDefault) != hipSuccess) {
@@ -2437,16 +2588,8 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
   const size_t xitems = static_cast<size_t>(g - 1) * region + n;   // region-mode buffer items
   if (regions) {
     const size_t need = xitems * (sizeof(K) + (PAIRS ? 4 : 0));
-    if (s->xbuf_bytes < need) {
-      if (s->xbuf) (void)hipFree(s->xbuf);
-      s->xbuf = nullptr;
-      s->xbuf_bytes = 0;
-      if (hipMalloc(&s->xbuf, need) != hipSuccess) {
-        (void)hipGetLastError();
-        return set_err(GRS_ENOMEM, "grs_sort_sharded: send buffer allocation failed");
-      }
-      s->xbuf_bytes = need;
-    }
+    const grs_status rx = grow_buf(s, &s->xbuf, &s->xbuf_bytes, need, "grs_sort_sharded: send buffer");
+    if (rx != GRS_OK) return rx;
     send_k = static_cast<K*>(s->xbuf);
     send_v = PAIRS ? reinterpret_cast<uint32_t*>(send_k + xitems) : nullptr;
   }
@@ -2551,19 +2694,6 @@ grs_status run_sharded_n(grs_sorter* s, const K* keys, const uint32_t* vals, uin
 
 // ---- presorted exchange (grs_codec.hpp): sort, encode the buckets, exchange, decode, merge --
 
-// Device buffer grown on demand (contents are not kept).
-grs_status grow_buf(void** p, size_t* have, size_t need, const char* what) {
-  if (*have >= need) return GRS_OK;
-  if (*p) (void)hipFree(*p);
-  *p = nullptr;
-  *have = 0;
-  if (hipMalloc(p, need) != hipSuccess) {
-    (void)hipGetLastError();
-    return set_err(GRS_ENOMEM, std::string(what) + ": allocation failed");
-  }
-  *have = need;
-  return GRS_OK;
-}
 
 size_t codec_blocks_max(size_t n, int g) { return n / grs::kCodecBlock + static_cast<size_t>(g); }
 
@@ -2585,7 +2715,7 @@ grs_status codec_scratch(grs_sorter* s, size_t n_enc, size_t n_merge, int g, Cod
                               ns + 64 + (ns / grs::kMkSPT + 2) * grs::kMkStride);
   const size_t need = al(4 * (2 * g + 2)) + al(4 * 2 * g) + 2 * al(4 * (nb + 1)) + al(8 * nb) +
                       al(scan) + al(4 * cor);
-  const grs_status r = grow_buf(&s->codec_buf, &s->codec_bytes, need, "presorted exchange scratch");
+  const grs_status r = grow_buf(s, &s->codec_buf, &s->codec_bytes, need, "presorted exchange scratch");
   if (r != GRS_OK) return r;
   char* b = static_cast<char*>(s->codec_buf);
   cs->plan = reinterpret_cast<uint32_t*>(b);      b += al(4 * (2 * g + 2));
@@ -2726,7 +2856,7 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   const int W = 2 * g + 3;   // words per rank in the size all-gather: (keys, words) + verdict
   const size_t need = al(S * 4) + al(S * 4) + al(gs * 4) + al(gs * 4) + al(4 * static_cast<size_t>(g) * W) +
                       al(4 * W) + al(sizeof(Dig));
-  grs_status r = grow_buf(&s->shard_buf, &s->shard_bytes, need, "grs_sort_sharded: scratch");
+  grs_status r = grow_buf(s, &s->shard_buf, &s->shard_bytes, need, "grs_sort_sharded: scratch");
   if (r != GRS_OK) return r;
   if (!s->shard_host && hipHostMalloc(reinterpret_cast<void**>(&s->shard_host), kShardHostWords * 4,
                                       hipHostMallocDefault) != hipSuccess) {
@@ -2744,7 +2874,7 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   CodecScratch cs;
   if ((r = codec_scratch(s, n, s->capacity, g, &cs)) != GRS_OK) return r;
   const size_t send_words = n + grs::kCodecDir * codec_blocks_max(n, g);
-  if ((r = grow_buf(&s->xbuf, &s->xbuf_bytes, 4 * send_words, "grs_sort_sharded: send buffer")) != GRS_OK)
+  if ((r = grow_buf(s, &s->xbuf, &s->xbuf_bytes, 4 * send_words, "grs_sort_sharded: send buffer")) != GRS_OK)
     return r;
   uint32_t* send = static_cast<uint32_t*>(s->xbuf);
 
@@ -2795,7 +2925,7 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
     lens[p] = h[p * 2 * g + 2 * me];
     total += lens[p];
   }
-  if ((r = grow_buf(&s->xrbuf, &s->xrbuf_bytes, std::max<size_t>(4 * ro, 4), "grs_sort_sharded: receive buffer")) != GRS_OK)
+  if ((r = grow_buf(s, &s->xrbuf, &s->xrbuf_bytes, std::max<size_t>(4 * ro, 4), "grs_sort_sharded: receive buffer")) != GRS_OK)
     return r;
   uint32_t* recv = static_cast<uint32_t*>(s->xrbuf);
   // 6. exchange of encoded words; the self part is a device copy
@@ -2943,7 +3073,7 @@ grs_status grs_shard_encode(grs_sorter* s, const uint32_t* d_sorted, size_t n,
   auto go = [&](auto nconst) -> grs_status {
     constexpr int N = decltype(nconst)::value;
     using Dig = grs::SplitterIdxDigit<uint32_t, N>;
-    grs_status r = grow_buf(&s->shard_buf, &s->shard_bytes, sizeof(Dig), "grs_shard_encode: scratch");
+    grs_status r = grow_buf(s, &s->shard_buf, &s->shard_bytes, sizeof(Dig), "grs_shard_encode: scratch");
     if (r != GRS_OK) return r;
     Dig* dig = static_cast<Dig*>(s->shard_buf);
     CodecScratch cs;
@@ -3110,11 +3240,8 @@ static grs_status records_key_scratch(grs_sorter* s, void** keys, uint32_t** idx
   const size_t cap = std::max<size_t>(s->capacity, 1);
   const size_t koff = (cap * kb + 255) & ~static_cast<size_t>(255);
   if (!s->rec_kbuf) {
-    if (hipMalloc(&s->rec_kbuf, koff + cap * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      s->rec_kbuf = nullptr;
-      return set_err(GRS_ENOMEM, "grs_records_key_buffers: scratch allocation failed");
-    }
+    const grs_status r = sbuf_alloc(s, &s->rec_kbuf, koff + cap * 4, "grs_records_key_buffers: scratch");
+    if (r != GRS_OK) return r;
   }
   *keys = s->rec_kbuf;
   *idx = reinterpret_cast<uint32_t*>(static_cast<char*>(s->rec_kbuf) + koff);
@@ -3123,16 +3250,7 @@ static grs_status records_key_scratch(grs_sorter* s, void** keys, uint32_t** idx
 
 // rec_buf of at least `need` bytes (grown on demand; its contents are per call).
 static grs_status records_call_scratch(grs_sorter* s, size_t need) {
-  if (s->rec_bytes >= need) return GRS_OK;
-  if (s->rec_buf) (void)hipFree(s->rec_buf);
-  s->rec_buf = nullptr;
-  s->rec_bytes = 0;
-  if (hipMalloc(&s->rec_buf, need) != hipSuccess) {
-    (void)hipGetLastError();
-    return set_err(GRS_ENOMEM, "grs_sort_records: scratch allocation failed");
-  }
-  s->rec_bytes = need;
-  return GRS_OK;
+  return grow_buf(s, &s->rec_buf, &s->rec_bytes, need, "grs_sort_records: scratch");
 }
 
 grs_status grs_records_key_buffers(grs_sorter* s, size_t n, size_t record_bytes, void** d_keys,
@@ -3253,6 +3371,9 @@ grs_status grs_lds_order_check(int device, int blocks, int items, unsigned long 
 
 const char* grs_pass_kernel(const grs_sorter* s, size_t n) {
   if (!s || n == 0) return "";
+  // the MSD-first schedule (grs_msd.hpp): its P1 scatter kernel (bench.py attributes the
+  // roofline to the slowest of P1 / P2 / P3 from their phase times)
+  if (use_msd(s, n, 0, s->key_type == GRS_KEY_U64 ? 64 : 32)) return "grs_onesweep_region";
   auto pick = [&](size_t big_tile, bool two_rounds = false) -> const char* {
     if (s->rank_mode != 0 || !use_big_tiles(s, n, big_tile) || two_rounds) return "grs_onesweep_v4";
     if (!use_persistent(s, (n + big_tile - 1) / big_tile, s->radix_bits)) return "grs_onesweep_v4";

@@ -472,6 +472,33 @@ __global__ void grs_fill_splitmix(K* __restrict__ out, uint64_t n, uint64_t seed
     out[i] = static_cast<K>(splitmix64(seed ^ (first + i)));
 }
 
+// The reference's own input: 0..N-1 shuffled (main.cpp:119-125).  pi = a seeded bijection of
+// [0, total): four rounds of x -> ((x * a_r + c_r) mod 2^b) ^ (that >> (b/2 + 1)) on b-bit
+// values (a_r odd: each step is invertible mod 2^b), walked along its cycle until the value is
+// below total (cycle walking keeps it a bijection of [0, total)).
+struct PermParams {
+  uint64_t a[4], c[4], mask;
+  int half;
+};
+__host__ __device__ __forceinline__ uint64_t perm_b(uint64_t x, const PermParams& p) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    x = (x * p.a[r] + p.c[r]) & p.mask;
+    x ^= x >> p.half;
+  }
+  return x;
+}
+template <typename K>
+__global__ void grs_fill_permutation(K* __restrict__ out, uint64_t n, uint64_t total, uint64_t first,
+                                     PermParams p) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    uint64_t x = perm_b(first + i, p);
+    while (x >= total) x = perm_b(x, p);
+    out[i] = static_cast<K>(x);
+  }
+}
+
 __global__ void grs_iota_u32(uint32_t* __restrict__ out, uint64_t n, uint32_t start) {
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x)

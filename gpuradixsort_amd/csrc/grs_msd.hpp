@@ -178,15 +178,18 @@ __global__ __launch_bounds__(1024) void grs_seg_plan(const uint32_t* __restrict_
 // caller).  Solo segments (one tile) are skipped: their pass counts them itself.  Persistent
 // grid over the plan's tiles; also zeroes the status words of the first segmented pass
 // (`zero`, rows of `radix` words; the layout is known only from the plan).
+// shift_dev (nullable): digit p is bits [*shift_dev + shift0 + 8p, +8) (a shift found on the device).
 template <typename K, int ND>
 __global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
                                                     const SegTile* __restrict__ rec,
                                                     const uint32_t* __restrict__ hdr, int shift0,
                                                     uint32_t* __restrict__ rows,
-                                                    uint32_t* __restrict__ zero, uint32_t radix) {
+                                                    uint32_t* __restrict__ zero, uint32_t radix,
+                                                    const uint32_t* __restrict__ shift_dev = nullptr) {
   __shared__ uint32_t h[ND * 256];
   const uint32_t t = threadIdx.x;
   const uint32_t tiles = hdr[0];
+  if (shift_dev != nullptr) shift0 += static_cast<int>(__builtin_amdgcn_readfirstlane(*shift_dev));
   const size_t zw = static_cast<size_t>(hdr[2] + 2 * hdr[1]) * radix;
   for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + t; i < zw; i += static_cast<size_t>(gridDim.x) * 256)
     zero[i] = 0;
@@ -226,31 +229,101 @@ __global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
 #define GRS_H2_CHUNK 262144
 #define GRS_H2_COPIES 32
 #define GRS_MSD_SAMPLE_CHUNKS 16384   // 64-key chunks the sample reads (2^20 keys)
+#define GRS_MSD_GUESS_CHUNKS 64       // 64-key chunks every sample block reads for the span guess
 
-// S: the top byte's histogram from an evenly spaced sample of 64-key chunks (all keys when
+// The MSD sort's span words in the call's control block (zeroed by the previous call):
+// [0..1] OR of the keys (lo, hi), [2..3] OR of their complements, [4] the top digit's shift.
+#define GRS_MSD_SPAN 1024
+
+// The top digit of the MSD sort: the byte whose highest bit is the keys' highest VARYING bit
+// (varying = OR(keys) & OR(~keys): bits that are not the same in every key), between bits
+// [8, 16) and the key's top byte.  Bits above it are equal in every key, so sorting by bits
+// [0, shift + 8) sorts the keys: the two scatters take bits [shift - 8, shift + 8) and the LDS
+// sort the bits below (the reference's own input, a shuffled 0..n-1 (main.cpp:119-125), varies
+// in its low log2(n) bits only; the top byte would leave 16 buckets at n = 2^28).
+template <typename K>
+__host__ __device__ inline uint32_t msd_top_shift(K varying) {
+  constexpr int KB = 8 * static_cast<int>(sizeof(K));
+  int hb = -1;
+  for (int b = KB - 1; b >= 0; --b)
+    if ((varying >> b) & K(1)) {
+      hb = b;
+      break;
+    }
+  const int s = hb - 7;
+  return static_cast<uint32_t>(s < 8 ? 8 : s > KB - 8 ? KB - 8 : s);
+}
+template <typename K>
+__device__ __forceinline__ K span_join(uint32_t lo, uint32_t hi) {
+  if constexpr (sizeof(K) == 8) return (static_cast<K>(hi) << 32) | lo;
+  else return static_cast<K>(lo);
+}
+// LDS rounds of P3 for top shift s: the bits below the 16-bit segment prefix, [0, s - 8)
+template <int RMAX>
+__device__ __forceinline__ int msd_p3_rounds(uint32_t s) {
+  const int r = (static_cast<int>(s) - 8 + 7) / 8;
+  return r < 1 ? 1 : r > RMAX ? RMAX : r;
+}
+
+// S: the top digit's histogram from an evenly spaced sample of 64-key chunks (all keys when
 // n <= 64 * chunks), added into samp[256] (zero); also does the clearing the LSD sort's
 // histogram kernel does (P1's status, the next call's control block) plus clear2 (h2 and the
-// big-segment counters).
+// big-segment counters).  The digit's shift is a guess from GRS_MSD_GUESS_CHUNKS evenly spaced
+// chunks that every block reads (so all blocks agree without communicating); block 0 writes it
+// to span[4] for P1, whose tiles then find the exact span (grs_msd_span checks the guess).
 template <typename K>
 __global__ __launch_bounds__(256) void grs_msd_sample(const K* __restrict__ keys, uint32_t n,
                                                       uint32_t* __restrict__ samp,
                                                       uint32_t* __restrict__ clear, uint32_t clear_words,
                                                       uint32_t* __restrict__ clear_ctrl,
-                                                      uint32_t* __restrict__ clear2, uint32_t clear2_words) {
+                                                      uint32_t* __restrict__ clear2, uint32_t clear2_words,
+                                                      uint32_t* __restrict__ span) {
   __shared__ uint32_t h[256];
+  __shared__ uint32_t sv[4];
   const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1);
   h[t] = 0;
+  if (t < 4) sv[t] = 0;
+  // the guess's keys first (16 per thread, in flight together)
+  constexpr uint32_t GC = GRS_MSD_GUESS_CHUNKS, GK = GC * GRS_WAVE / 256;
+  K g[GK];
+#pragma unroll
+  for (uint32_t u = 0; u < GK; ++u) {
+    const uint32_t i = u * 256 + t;
+    const uint32_t pos = n <= GC * GRS_WAVE
+                             ? i
+                             : static_cast<uint32_t>(static_cast<uint64_t>(i >> 6) * (n - GRS_WAVE) / (GC - 1)) + (i & 63u);
+    g[u] = i < n ? keys[pos] : K(0);
+  }
   const uint32_t gs = gridDim.x * 256;
   for (uint32_t i = blockIdx.x * 256 + t; i < clear_words; i += gs) clear[i] = 0;
   for (uint32_t i = blockIdx.x * 256 + t; i < clear2_words; i += gs) clear2[i] = 0;
   constexpr uint32_t H = GRS_CTRL_HIST_WORDS, TK = GRS_MAX_PASSES * GRS_XCDS;
   for (uint32_t i = blockIdx.x * 256 + t; i < H + TK; i += gs) clear_ctrl[i] = 0;
+  K o = 0, no = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < GK; ++u)
+    if (u * 256 + t < n) {
+      o |= g[u];
+      no |= static_cast<K>(~g[u]);
+    }
+  uint32_t v[4] = {static_cast<uint32_t>(o), static_cast<uint32_t>(static_cast<uint64_t>(o) >> 32),
+                   static_cast<uint32_t>(no), static_cast<uint32_t>(static_cast<uint64_t>(no) >> 32)};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v[q] |= __shfl_xor(v[q], s);
+  }
+  __syncthreads();   // h and sv zeroed
+  if (lane == 0)
+    for (int q = 0; q < 4; ++q) atomicOr(&sv[q], v[q]);
   __syncthreads();
+  const uint32_t top = msd_top_shift<K>(span_join<K>(sv[0], sv[1]) & span_join<K>(sv[2], sv[3]));
+  if (blockIdx.x == 0 && t == 0) span[4] = top;
+  auto bin = [&](K k) { return static_cast<uint32_t>(k >> top) & 255u; };
   constexpr uint32_t C = GRS_MSD_SAMPLE_CHUNKS;
-  constexpr int TOP = 8 * static_cast<int>(sizeof(K)) - 8;
   if (n <= C * GRS_WAVE) {
     for (uint32_t i = blockIdx.x * 256 + t; i < n; i += gs)
-      atomicAdd(&h[static_cast<uint32_t>(keys[i] >> TOP)], 1u);
+      atomicAdd(&h[bin(keys[i])], 1u);
   } else {
     // every wave's chunks loaded before any is counted (the loads overlap)
     constexpr uint32_t U = 4;
@@ -265,11 +338,49 @@ __global__ __launch_bounds__(256) void grs_msd_sample(const K* __restrict__ keys
       }
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u)
-        if (c0 + u * waves < C) atomicAdd(&h[static_cast<uint32_t>(k[u] >> TOP)], 1u);
+        if (c0 + u * waves < C) atomicAdd(&h[bin(k[u])], 1u);
     }
   }
   __syncthreads();
   if (h[t] != 0u) atomicAdd(&samp[t], h[t]);
+}
+
+// After P1 (one block): the exact span (P1's tiles ORed every key into span[0..3]) fixes the top
+// digit's shift.  A shift above the sample's guess (a varying bit the guess missed) or a run
+// that outgrew its region (totals[256], set by P1) plans the redo: P1 again with exact counts at
+// the exact shift, the whole input as one segment of TILEF-key tiles (grs_seg_hist and a
+// persistent grs_onesweep_seg), and sets totals[256] so that the plans downstream take the
+// exact layout; an empty plan otherwise (the redo's launches leave at once).
+template <typename K, uint32_t TILEF>
+__global__ __launch_bounds__(256) void grs_msd_span(uint32_t n, uint32_t* __restrict__ span,
+                                                    uint32_t* __restrict__ totals,
+                                                    SegTile* __restrict__ rec, uint32_t* __restrict__ hdr) {
+  __shared__ uint32_t tiles;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) {
+    const uint32_t sx = msd_top_shift<K>(span_join<K>(span[0], span[1]) & span_join<K>(span[2], span[3]));
+    bool redo = totals[256] != 0u;
+    if (sx != span[4]) {
+      span[4] = sx;
+      totals[256] = 1u;
+      redo = true;
+    }
+    tiles = redo ? n / TILEF + (n % TILEF != 0u ? 1u : 0u) : 0u;
+  }
+  __syncthreads();
+  constexpr uint32_t G = GRS_LB_GROUP;
+  const uint32_t T = tiles;
+  for (uint32_t k = t; k < T; k += 256) {
+    const uint32_t q = k / G;
+    const uint32_t flags = (k % G) | (min(G, T - q * G) << 4) | ((T == 1 ? 1u : 0u) << 8) | (q << 9) |
+                           (k + 1 == T ? 0x80000000u : 0u);
+    rec[k] = SegTile{k, q, flags, k * TILEF, min(TILEF, n - k * TILEF), 0u, n, 0u};
+  }
+  if (t == 0) {
+    hdr[0] = T;
+    hdr[1] = T > 1 ? (T + G - 1) / G : 0u;
+    hdr[2] = T > 1 ? T : 0u;
+  }
 }
 
 // The top-byte bucket table after P1: in[s] = where bucket s's keys lie in alt, len[s] = its
@@ -333,7 +444,8 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
                                                          uint32_t zero_words,
                                                          const uint32_t* __restrict__ tab, uint32_t chunk,
                                                          uint32_t sample_shift = 0,
-                                                         const uint32_t* __restrict__ gate = nullptr) {
+                                                         const uint32_t* __restrict__ gate = nullptr,
+                                                         const uint32_t* __restrict__ top_shift = nullptr) {
   constexpr uint32_t B = 1024;
   constexpr uint32_t LW = 256 * GRS_H2_COPIES;
   __shared__ __attribute__((aligned(16))) uint32_t h[LW];
@@ -355,7 +467,9 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   const uint32_t c0 = tab[s] + j * chunk;
   const uint32_t cl = min(chunk, tab[257 + s] - j * chunk);
   uint32_t* const base = h + (t & (GRS_H2_COPIES - 1));
-  constexpr int SH = 8 * static_cast<int>(sizeof(K)) - 16;   // the second byte from the top
+  // the byte below the top digit (top_shift: the MSD sort's shift found on the device)
+  const int SH = top_shift != nullptr ? static_cast<int>(__builtin_amdgcn_readfirstlane(*top_shift)) - 8
+                                      : 8 * static_cast<int>(sizeof(K)) - 16;
   auto count = [&](K k) {
     atomicAdd(base + (static_cast<uint32_t>(k >> SH) & 255u) * GRS_H2_COPIES, 1u);
   };
@@ -566,9 +680,12 @@ struct LocalSort {
   static constexpr int ROUNDS = RMAX;
   static_assert(W <= 16 && BLOCK >= 256, "digit threads: waves 0..3");
   static_assert(!C16 || SMAX < 65536, "16-bit positions");
+  // 16-B vectors of keys / values; the arrays hold SMAX + one vector, so that element p can sit
+  // at p + a (a < vector) with a the misalignment of the HBM run it comes from or goes to
+  static constexpr uint32_t KV = 16 / sizeof(K), VV = 4;
   struct Smem {
-    K sk[SMAX];
-    uint32_t sv[PAIRS ? SMAX : 1];
+    alignas(16) K sk[SMAX + KV];
+    alignas(16) uint32_t sv[PAIRS ? SMAX + VV : 4];
     uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
     uint32_t wtot[4];
     uint32_t slot;
@@ -598,8 +715,10 @@ struct LocalSort {
       if constexpr (PAIRS) v[j] = i < len ? vin[lo + i] : 0u;
     }
   }
-  // `rounds` stable 8-bit rounds from the registers; the sorted segment is left in sm.sk / sm.sv
-  __device__ __forceinline__ static void sort_rounds(Smem& sm, K (&k)[I], Vals& v, uint32_t len, int rounds) {
+  // `rounds` stable 8-bit rounds from the registers; the sorted segment is left in sm.sk / sm.sv,
+  // element p at sm.sk[p + ak] / sm.sv[p + av] (ak, av: store_vec's alignment shifts)
+  __device__ __forceinline__ static void sort_rounds(Smem& sm, K (&k)[I], Vals& v, uint32_t len, int rounds,
+                                                     uint32_t ak = 0, uint32_t av = 0, int shift0 = 0) {
     uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
     auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return sm.cnt[a]; };
     auto cst = [&](uint32_t a, uint32_t x) {
@@ -609,7 +728,7 @@ struct LocalSort {
 #pragma unroll
     for (int pass = 0; pass < ROUNDS; ++pass) {
       if (pass >= rounds) break;   // uniform
-      const int shift = 8 * pass;
+      const int shift = shift0 + 8 * pass;
       auto digit = [&](K x) { return static_cast<uint32_t>(x >> shift) & 255u; };
       for (uint32_t c = t; c < W * 256 / (C16 ? 2 : 1); c += BLOCK) sm.cnt[c] = 0;
       __syncthreads();
@@ -648,13 +767,15 @@ struct LocalSort {
         }
       }
       __syncthreads();
+      const bool last = pass + 1 >= rounds;
+      const uint32_t sk_off = last ? ak : 0u, sv_off = last ? av : 0u;
 #pragma unroll
       for (uint32_t j = 0; j < I; ++j) {
         const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
         if (i < len) {
           const uint32_t dst = cld(w * 256 + digit(k[j])) + r[j];
-          sm.sk[dst] = k[j];
-          if constexpr (PAIRS) sm.sv[dst] = v[j];
+          sm.sk[dst + sk_off] = k[j];
+          if constexpr (PAIRS) sm.sv[dst + sv_off] = v[j];
         }
       }
       __syncthreads();
@@ -676,6 +797,134 @@ struct LocalSort {
       kout[lo + i] = sm.sk[i];
       if constexpr (PAIRS) vout[lo + i] = sm.sv[i];
     }
+  }
+
+  // ---- 16-B accesses (one dwordx4 per lane) for runs at any element alignment ----
+  // Where element p of a run starting at `at` sits relative to a 16-B boundary: (address / E) % V.
+  template <typename T, uint32_t V>
+  __device__ __forceinline__ static uint32_t mis(const T* at) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(at) / sizeof(T)) % V;
+  }
+  // run[0, len) -> lds[a, a + len) with a = mis(run) by LDS-DMA (global_load_lds_dwordx4, no
+  // registers): wave w moves the 1-KB chunks w, w + W, ... (a wave-instruction writes 64 x 16 B
+  // from its wave-uniform LDS base, lds + a + head being 16-B aligned like run + head); the
+  // scalar head and tail by ordinary loads.  The caller waits (vmcnt(0)) and synchronises.
+  template <typename T, uint32_t V>
+  __device__ __forceinline__ static void copy_in_glds(T* lds, const T* run, uint32_t len) {
+    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+    const uint32_t a = mis<T, V>(run);
+    const uint32_t head = min(len, (V - a) % V);
+    const uint32_t nv = (len - head) / V;
+    if (t < head) lds[a + t] = run[t];
+    const T* src = run + head;
+    T* dst = lds + a + head;
+    for (uint32_t c = w; c * GRS_WAVE < nv; c += W) {
+      const uint32_t vi = c * GRS_WAVE + lane;
+      if (vi < nv)
+        __builtin_amdgcn_global_load_lds(src + vi * V, dst + c * GRS_WAVE * V, 16, 0, 0);
+    }
+    const uint32_t r = head + nv * V + t;
+    if (r < len) lds[a + r] = run[r];   // (the tail is < V < BLOCK elements)
+  }
+  // lds[a, a + len) -> run[0, len) with a = mis(run) (sort_rounds' shift)
+  template <typename T, uint32_t V>
+  __device__ __forceinline__ static void copy_out(T* run, const T* lds, uint32_t len) {
+    const uint32_t t = threadIdx.x, a = mis<T, V>(run);
+    const uint32_t head = min(len, (V - a) % V);
+    const uint32_t nv = (len - head) / V;
+    if (t < head) run[t] = lds[a + t];
+    uint4* dst = reinterpret_cast<uint4*>(run + head);
+    const uint4* src = reinterpret_cast<const uint4*>(lds + a + head);
+    for (uint32_t c = t; c < nv; c += BLOCK) dst[c] = src[c];
+    const uint32_t r = head + nv * V + t;
+    if (r < len) run[r] = lds[a + r];
+  }
+  // the segment's keys (and payload) into registers, wave-striped as load() leaves them: 16-B
+  // LDS-DMA loads into sm.sk / sm.sv, then conflict-free 4-B LDS reads
+  __device__ __forceinline__ static void load_lds(Smem& sm, K (&k)[I], Vals& v, const K* kin, const uint32_t* vin,
+                                                  uint32_t len) {
+    copy_in_glds<K, KV>(sm.sk, kin, len);
+    if constexpr (PAIRS) copy_in_glds<uint32_t, VV>(sm.sv, vin, len);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t ak = mis<K, KV>(kin), av = PAIRS ? mis<uint32_t, VV>(vin) : 0u;
+    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+#pragma unroll
+    for (uint32_t j = 0; j < I; ++j) {
+      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
+      k[j] = i < len ? sm.sk[ak + i] : K(0);
+      if constexpr (PAIRS) v[j] = i < len ? sm.sv[av + i] : 0u;
+    }
+    __syncthreads();   // every read before the first round's counters and scatter
+  }
+  // run() with 16-B HBM stores (and, GLDS, 16-B LDS-DMA loads): kin / vin and kout / vout are
+  // the segment's runs, at any alignment
+  template <bool GLDS>
+  __device__ __forceinline__ static void run_vec(Smem& sm, const K* kin, const uint32_t* vin, K* kout,
+                                                 uint32_t* vout, uint32_t len, int rounds) {
+    K k[I];
+    Vals v;
+    auto ld = [&]() {
+      if constexpr (GLDS) load_lds(sm, k, v, kin, vin, len);
+      else load(k, v, kin, vin, 0u, len);
+    };
+    ld();
+    const uint32_t ak = mis<K, KV>(kout), av = PAIRS ? mis<uint32_t, VV>(vout) : 0u;
+    if (ROUNDS > 2 && rounds > 2) {
+      // more than two rounds (u64 keys): two on the top 16 of the bits to sort, then the runs
+      // of keys equal in them -- short in a uniform segment (4096 keys in 65536 bins: ~6 % of
+      // the keys, runs of 2-4) -- finished by an insertion sort on the bits below, stable; a
+      // run past kRunMax sends the segment through every round instead (its keys read again)
+      if constexpr (ROUNDS > 2) {   // (u32 keys never take this branch: no code for it)
+        sort_rounds(sm, k, v, len, 2, ak, av, 8 * rounds - 16);
+        if (finish_runs(sm, len, 8 * rounds - 16, ak, av)) {
+          ld();
+          sort_rounds(sm, k, v, len, rounds, ak, av);
+        }
+      }
+    } else {
+      sort_rounds(sm, k, v, len, rounds, ak, av);   // (ends with a barrier after its scatter)
+    }
+    copy_out<K, KV>(kout, sm.sk, len);
+    if constexpr (PAIRS) copy_out<uint32_t, VV>(vout, sm.sv, len);
+  }
+  static constexpr uint32_t kRunMax = 48;
+  // The sorted segment in LDS (sm.sk[ak + p]) is ordered by key >> hb and, inside each run of equal
+  // key >> hb, by input order; sort every run by the whole key with a stable insertion sort (one
+  // thread per run; the runs are disjoint and their key >> hb never changes, so the run bounds
+  // other threads read stay valid).  Returns true (uniform) if a run was longer than kRunMax
+  // (left unsorted: the caller sorts the segment by every round instead).
+  __device__ __forceinline__ static bool finish_runs(Smem& sm, uint32_t len, int hb, uint32_t ak, uint32_t av) {
+    __syncthreads();   // the last round's scatter
+    if (threadIdx.x == 0) sm.slot = 0;
+    __syncthreads();
+    K* const a = sm.sk + ak;
+    uint32_t* const b = sm.sv + av;
+    for (uint32_t p = threadIdx.x; p < len; p += BLOCK) {
+      const K hi = a[p] >> hb;
+      if (p != 0 && (a[p - 1] >> hb) == hi) continue;   // not a run start
+      uint32_t e = p + 1;
+      while (e < len && (a[e] >> hb) == hi && e - p <= kRunMax) ++e;
+      if (e - p > kRunMax) {
+        sm.slot = 1;
+        continue;
+      }
+      for (uint32_t q = p + 1; q < e; ++q) {   // insertion sort of a[p, e): stable
+        const K x = a[q];
+        uint32_t y = 0;
+        if constexpr (PAIRS) y = b[q];
+        uint32_t r = q;
+        while (r > p && a[r - 1] > x) {
+          a[r] = a[r - 1];
+          if constexpr (PAIRS) b[r] = b[r - 1];
+          --r;
+        }
+        a[r] = x;
+        if constexpr (PAIRS) b[r] = y;
+      }
+    }
+    __syncthreads();
+    return sm.slot != 0u;
   }
 };
 
@@ -701,7 +950,8 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
                                                        uint32_t* __restrict__ big_start,
                                                        uint32_t* __restrict__ big_len,
                                                        uint32_t* __restrict__ big_row,
-                                                       uint32_t* __restrict__ rows) {
+                                                       uint32_t* __restrict__ rows,
+                                                       const uint32_t* __restrict__ top_shift) {
   using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
   constexpr uint32_t ND = LS::ROUNDS;   // fallback digits (histogram row of ND x 256 words)
   __shared__ typename LS::Smem sm;
@@ -743,7 +993,11 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
       for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(sm.slot) * ND * 256 + i] = 0;
     return;
   }
-  LS::run(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, 0u, len, LS::ROUNDS);
+  // the bits below the segment's 16-bit prefix (bits above the top digit are equal in every key);
+  // 16-B HBM loads and stores through LDS at the runs' own alignments
+  const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
+  LS::template run_vec<false>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, len,
+                              rounds);
 }
 
 // P3's second shape: the mid list's segments (persistent grid, a segment per workgroup in
@@ -755,7 +1009,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict_
                                                             const K* __restrict__ rk,
                                                             const uint32_t* __restrict__ rv,
                                                             const uint32_t* __restrict__ spill,
-                                                            const uint32_t* __restrict__ mid) {
+                                                            const uint32_t* __restrict__ mid,
+                                                            const uint32_t* __restrict__ top_shift) {
   using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
   __shared__ typename LS::Smem sm;
   const uint32_t count = mid[0];
@@ -763,9 +1018,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict_
   const bool inplace = *spill != 0u;
   const K* const kin = inplace ? keys : rk;
   const uint32_t* const vin = inplace ? vals : rv;
+  const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
   for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
     const uint32_t lo = mid[2 + 3 * e], o = mid[3 + 3 * e], len = mid[4 + 3 * e];
-    LS::run(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, 0u, len, LS::ROUNDS);
+    LS::template run_vec<false>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr,
+                                len, rounds);
     __syncthreads();   // every LDS read of this segment before the next one's
   }
 }

@@ -223,6 +223,7 @@ struct V4Smem {
   uint32_t wsum[2 * WAVES];     // wave totals of the digit scans
   uint32_t ticket;
   uint32_t next;                // persistent kernel: the next tile's ticket
+  uint32_t span[4];             // OPT 262144: OR of the tile's keys (lo, hi), OR of their complements
   alignas(16) K keys[LTILE];
   uint32_t vals[PAIRS ? LTILE : 1];
   // indexed digits (partition): tile-local start of every digit, from which the store phase
@@ -250,6 +251,8 @@ using V4SmemFor = V4Smem<K, PAIRS, RB, BLOCK, ITEMS, (OPT & 256) != 0, DigitF::k
 //   16384 / 32768: the records read / written are SPLIT over two buffers: records [0, n/2)
 //        in keys_in / keys_out and [n/2, n) in vals_in / vals_out (n even; the caller's two
 //        4n-byte arrays hold n records that way)
+//   262144 span: the ranking also ORs the tile's valid keys and their complements into sm.span
+//        (zeroed by the kernel; the MSD sort's first scatter learns the keys' exact bit span)
 
 // Load tile `tile` wave-striped: item j of lane l of wave w is tile key w*64*ITEMS + j*64 + l.
 // Keys past n (last tile) are all-ones padding, which sorts after every valid key of its digit.
@@ -578,7 +581,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(
       // bounds-checked build, tools/diag).
       const uint64_t last = sp.seg_len >= publish ? static_cast<uint64_t>(sp.seg_len - publish) : 0u;
       const uint64_t want = static_cast<uint64_t>(gstart) + static_cast<uint64_t>(prefix);
+#ifndef GRS_TEST_NO_CLAMP
       start = sp.seg_start + static_cast<uint32_t>(want < last ? want : last);
+#else
+      // scratch builds only (tools/diag/canary_no_clamp.py): the clamp removed, so that a region
+      // run past its room writes past the region buffer and the guard bands must show it
+      (void)last;
+      start = sp.seg_start + static_cast<uint32_t>(want);
+#endif
     }
 #ifdef GRS_DIAG
     if (diag_lim[0] != 0u && publish != 0u && start + publish > diag_lim[0] &&
@@ -605,6 +615,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   lds_barrier();  // B4
 
   // ---- store: consecutive threads write consecutive slots of each digit run ----
+  // (SPAN: the stored keys, which are the tile's valid keys, ORed on the way)
+  constexpr bool SPAN = (OPT & 262144) != 0;
+  K s_or = 0, s_nor = 0;
   // digit of reordered position i.  Indexed digits: a thread visits increasing positions, so
   // its digit only moves forward through the tile-local digit starts (at most RADIX - 1 steps
   // per tile, over empty digits too).
@@ -676,6 +689,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(
         const K kk = sm.keys[i];
         const uint32_t d = dig_at(roff + i, kk);
         put(sm.base[d] + roff + i, kk, i);
+        if constexpr (SPAN) {
+          s_or |= kk;
+          s_nor |= static_cast<K>(~kk);
+        }
       }
     } else {
 #pragma unroll
@@ -685,8 +702,23 @@ __device__ __forceinline__ uint32_t onesweep_tile(
           const K kk = sm.keys[i];
           const uint32_t d = dig_at(roff + i, kk);
           put(sm.base[d] + roff + i, kk, i);
+          if constexpr (SPAN) {
+            s_or |= kk;
+            s_nor |= static_cast<K>(~kk);
+          }
         }
       }
+    }
+  }
+  if constexpr (SPAN) {   // wave OR, then one LDS OR per wave (read by the kernel after a barrier)
+    uint32_t v[4] = {static_cast<uint32_t>(s_or), static_cast<uint32_t>(static_cast<uint64_t>(s_or) >> 32),
+                     static_cast<uint32_t>(s_nor), static_cast<uint32_t>(static_cast<uint64_t>(s_nor) >> 32)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (sizeof(K) == 4 && (q & 1)) continue;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v[q] |= __shfl_xor(v[q], o);
+      if (lane == 0 && v[q] != 0u) atomicOr(&sm.span[q], v[q]);
     }
   }
   return next;
@@ -727,18 +759,20 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
 // to a REGION of R_d = (sample[d] * mult >> 20) + pad keys -- the sampled share of the top byte,
 // with slack -- instead of its exact place, so the keys need no counting read before the pass.
 // region_len = sum of the regions (the clamp bound).  The last ticket writes the digit totals
-// to totals[0..RADIX) and sets totals[RADIX] when a run outgrew its region; it then also plans
-// the redo (the whole input as one segment of TILEF-key tiles, for grs_seg_hist and a persistent
-// grs_onesweep_seg) into redo_rec / redo_hdr, or writes an empty plan.
-template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT, uint32_t TILEF>
+// to totals[0..RADIX) and sets totals[RADIX] when a run outgrew its region.
+// span (the MSD sort's span words, grs_msd.hpp GRS_MSD_SPAN): the digit's shift is span[4] (the
+// sample's guess of the keys' top varying byte), and every tile ORs its keys into span[0..1] and
+// their complements into span[2..3], so that grs_msd_span learns the exact span and plans the
+// redo (a run past its region, or a varying bit above the guessed digit).
+template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT>
 __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
     const K* __restrict__ keys_in, K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, uint32_t n, const RadixDigit<K> dig,
     const uint32_t* __restrict__ sample, unsigned long long mult, uint32_t pad,
     uint32_t region_len, uint32_t* __restrict__ ticket, uint32_t* __restrict__ status,
     uint32_t* __restrict__ status_next, uint32_t* __restrict__ error_word,
-    uint32_t* __restrict__ totals, SegTile* __restrict__ redo_rec, uint32_t* __restrict__ redo_hdr) {
-  constexpr int ROPT = OPT | 131072;
+    uint32_t* __restrict__ totals, uint32_t* __restrict__ span) {
+  constexpr int ROPT = OPT | 131072 | 262144;
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, ROPT, RadixDigit<K>>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
@@ -747,7 +781,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
   K key[ITEMS];
   uint32_t val[ITEMS];
   if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+  if (t < 4) sm.span[t] = 0;
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
+  RadixDigit<K> dg = dig;
+  dg.shift = static_cast<int>(__builtin_amdgcn_readfirstlane(span[4]));
   __syncthreads();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
   tile_load<K, PAIRS, BLOCK, ITEMS, ROPT>(key, val, keys_in, vals_in, n, tile, tt);
@@ -758,25 +795,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_region(
   TileSpan sp = TileSpan::whole(tile, n, SM::TILE);
   sp.seg_len = region_len;
   onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, ROPT>(sm, sp, key, val, keys_in, keys_out, vals_in,
-                                                  vals_out, n, dig, gh, ticket, status, status_next,
+                                                  vals_out, n, dg, gh, ticket, status, status_next,
                                                   error_word, PassDebug::read(error_word), nullptr,
                                                   totals);
-  if (tile + 1u == sp.tiles) {   // the redo's plan (its digit threads wrote the spill flag)
-    __syncthreads();
-    constexpr uint32_t G = GRS_LB_GROUP;
-    const bool spill = __hip_atomic_load(&totals[SM::RADIX], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-    const uint32_t T = spill ? n / TILEF + (n % TILEF != 0u ? 1u : 0u) : 0u;
-    for (uint32_t k = t; k < T; k += BLOCK) {
-      const uint32_t q = k / G;
-      const uint32_t flags = (k % G) | (min(G, T - q * G) << 4) | ((T == 1 ? 1u : 0u) << 8) | (q << 9) |
-                             (k + 1 == T ? 0x80000000u : 0u);
-      redo_rec[k] = SegTile{k, q, flags, k * TILEF, min(TILEF, n - k * TILEF), 0u, n, 0u};
-    }
-    if (t == 0) {
-      redo_hdr[0] = T;
-      redo_hdr[1] = T > 1 ? (T + G - 1) / G : 0u;
-      redo_hdr[2] = T > 1 ? T : 0u;
-    }
+  lds_barrier();   // every wave's OR in sm.span
+  if (t < 4 && (sizeof(K) == 8 || (t & 1u) == 0u)) {
+    // one global OR per word, and only when it adds bits (all but the first tiles skip it)
+    const uint32_t mine = sm.span[t];
+    const uint32_t cur = __hip_atomic_load(&span[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur | mine) != cur) atomicOr(&span[t], mine);
   }
 }
 
@@ -920,7 +947,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
     uint32_t* __restrict__ ticket, uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
     uint32_t* __restrict__ error_word, uint32_t* __restrict__ digit_starts,
     uint32_t* __restrict__ totals = nullptr, uint32_t* __restrict__ spill = nullptr,
-    const uint32_t* __restrict__ gate = nullptr) {
+    const uint32_t* __restrict__ gate = nullptr, const uint32_t* __restrict__ shift_dev = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, RadixDigit<K>>;
   static_assert((OPT & (16384 | 32768)) == 0, "segmented passes: records in one buffer (n unknown)");
   __shared__ SM sm;
@@ -928,6 +955,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
   // gate (nullable): run only when *gate != 0 (a redo that is usually not needed)
   if (gate != nullptr && __builtin_amdgcn_readfirstlane(*gate) == 0u) return;
   const PassDebug dbg = PassDebug::read(error_word);
+  // shift_dev (nullable, the MSD sort's digit shift found on the device): the digit's shift is
+  // *shift_dev + dig.shift
+  RadixDigit<K> dg = dig;
+  if (shift_dev != nullptr) dg.shift += static_cast<int>(__builtin_amdgcn_readfirstlane(*shift_dev));
   for (;;) {
     if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
     for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
@@ -955,7 +986,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_seg(
     // tile writes the digit totals to totals[seg * RADIX + d] and sets *spill if one outgrew
     uint32_t* const tot = (OPT & 131072) != 0 ? totals + static_cast<size_t>(r.seg) * SM::RADIX : nullptr;
     onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT, false, true>(sm, sp, key, val, keys_in, keys_out, vals_in,
-                                                   vals_out, 0u, dig, gh, ticket, status,
+                                                   vals_out, 0u, dg, gh, ticket, status,
                                                    status_next, error_word, dbg, ds, tot, spill);
     if constexpr (!PERSIST) return;
     lds_barrier();   // every LDS read of the finished tile before the next ticket's reset

@@ -82,6 +82,13 @@ class RadixSorter:
     def scratch_bytes(self) -> int:
         return int(lib().grs_scratch_bytes(self._h))
 
+    def check_guards(self) -> int:
+        """Guard words of the sorter's scratch that a kernel overwrote since the last check
+        (grs_debug_check_guards; synchronises the device, restores them): 0 expected."""
+        bad = ctypes.c_uint64()
+        check(lib().grs_debug_check_guards(self._h, ctypes.byref(bad)), "grs_debug_check_guards")
+        return int(bad.value)
+
     @property
     def rank_mode(self) -> str:
         """'atomic' (lane-ordered LDS atomics, the default) or 'match' (ballot fallback)."""
@@ -261,6 +268,17 @@ def fill_splitmix(out: torch.Tensor, seed: int, first_index: int = 0,
     check(lib().grs_fill_splitmix(_ptr(out), out.numel(), out.element_size(),
                                   seed & (2**64 - 1), first_index, _stream_ptr(stream)),
           "grs_fill_splitmix")
+    return out
+
+
+def fill_permutation(out: torch.Tensor, seed: int, total: Optional[int] = None, first_index: int = 0,
+                     stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """The reference's own input (main.cpp:119-125: 0..N-1 shuffled): out[i] = pi(first_index + i)
+    for a seeded bijection pi of [0, total) (total defaults to out.numel()), on the device."""
+    total = out.numel() if total is None else int(total)
+    check(lib().grs_fill_permutation(_ptr(out), out.numel(), out.element_size(), total,
+                                     seed & (2**64 - 1), first_index, _stream_ptr(stream)),
+          "grs_fill_permutation")
     return out
 
 

@@ -40,7 +40,9 @@
 extern "C" {
 #endif
 
-#define GRS_VERSION 300 /* 3.0.0: options API (no environment knobs) */
+#define GRS_VERSION 400 /* 4.0.0: grs_timing gained `kind` (3.x callers' structs are 4 bytes
+                           shorter); guard bands + grs_debug_check_guards; grs_fill_permutation;
+                           the MSD sort's scratch allocated by capacity / option */
 
 typedef enum grs_status {
   GRS_OK = 0,
@@ -92,8 +94,26 @@ grs_status grs_create(grs_sorter** out, size_t capacity, grs_key_type key_type,
                       int with_u32_payload, int radix_bits, int device);
 void grs_destroy(grs_sorter* s);
 
-/* Bytes of device scratch the sorter holds (ping-pong + look-back status + control). */
+/* Bytes of device scratch the sorter holds now (second buffer, look-back status, control blocks,
+ * the MSD sort's scratch, and buffers other entry points grew on demand), guard bands included.
+ * Per element of capacity n (E = key + payload bytes):
+ *   LSD passes (radix_bits 4, u64 pairs, capacity < 48M items):  n E + ~n/1000 E
+ *   + the MSD sort's scratch (8-bit digits, u32 keys / u32 pairs / u64 keys, allocated at
+ *     grs_create from 48M items of capacity, or by grs_set_option(GRS_OPT_MSD, 1)):
+ *     the second buffer grows to 1.125 n + 1M elements and a region buffer of 1.25 n + 4M
+ *     elements joins it, ~2.4 n E in all (C4's 2^30 u32 keys: ~10 GB beside its 4.3 GB of
+ *     keys); grs_set_option(GRS_OPT_MSD, 0) releases it (the sorter then runs the LSD passes).
+ * If the MSD scratch does not fit at grs_create, the sorter is created without it. */
 size_t grs_scratch_bytes(const grs_sorter* s);
+
+/* Debug canaries: every scratch allocation of the sorter ends in a 16-KB guard band (and the
+ * arrays inside one allocation -- the two status buffers, keys and payload of the second and
+ * region buffers, the MSD tables -- are separated by one), filled with a pattern when allocated.
+ * Synchronises the sorter's device, counts the guard words that no longer hold the pattern (a
+ * kernel wrote past one of its scratch arrays), restores them, and returns the count in
+ * *bad_words (0 expected).  New with respect to the reference, whose scan silently overflows
+ * past 2^20 items (PrefixScanBuffer.comp:36). */
+grs_status grs_debug_check_guards(grs_sorter* s, uint64_t* bad_words);
 
 /* Ranking used by this sorter's passes: 0 = lane-ordered LDS atomics (the default; probed on
  * the device at grs_create), 1 = wave64 ballot-match fallback (probe failed, or
@@ -155,13 +175,17 @@ typedef enum grs_option {
                                 grs_sort_segmented's long segments: 0 keeps them on the segmented
                                 LSD instead of the top-byte scatter + LDS sorts.  2 (test hook):
                                 1, with the byte-2 scatter's sampled regions refused, so its exact
-                                redo runs */
+                                redo runs.  Memory: 0 releases the MSD sort's scratch (~1.4 n
+                                elements, grs_scratch_bytes), 1 / 2 allocate it (GRS_ENOMEM if it
+                                does not fit), -1 keeps it from 48M items of capacity; a change
+                                synchronises the device */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);
 
 /* Name of the pass kernel a sort of n items launches ("grs_onesweep_v4" or, on small grids,
- * "grs_onesweep_v6"): what profiling and roofline reports attribute the pass time to. */
+ * "grs_onesweep_v6"; "grs_onesweep_region" when the MSD-first schedule runs, whose phases
+ * grs_timing kind 1 reports): what profiling and roofline reports attribute the pass time to. */
 const char* grs_pass_kernel(const grs_sorter* s, size_t n);
 
 /* Stable ascending sort of d_keys[0..n) in place; when the sorter was created with a
@@ -341,6 +365,13 @@ grs_status grs_copy_u32(const uint32_t* d_src, uint32_t* d_dst, size_t n, void* 
  * to key_bytes (4 or 8). */
 grs_status grs_fill_splitmix(void* d_keys, size_t n, int key_bytes, uint64_t seed,
                              uint64_t first_index, void* stream);
+
+/* The reference's own input, 0..total-1 shuffled (main.cpp:119-125): key[i] = pi(first_index + i)
+ * for a seeded bijection pi of [0, total) (four multiply-xorshift rounds on the next power of two,
+ * cycle-walked below total); first_index + n <= total, total <= 2^32 for 4-byte keys.  Sharded
+ * callers fill rank r's slice with first_index = r * n_local. */
+grs_status grs_fill_permutation(void* d_keys, size_t n, int key_bytes, uint64_t total, uint64_t seed,
+                                uint64_t first_index, void* stream);
 
 /* Number of i in [1, n) with key[i] < key[i-1] (the reference's monotonic check,
  * ParallelSort.cpp:336-352).  Synchronises. */

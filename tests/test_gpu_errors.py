@@ -30,7 +30,13 @@ SHAPES = [
     (32, False, 4, {"tile": "big"}),                  # 4-bit digits (C2's kernel)
     (32, False, 4, {"tile": "big", "pass": "fused"}),  # 4-bit digits, every pass in one launch
     (32, False, 8, {"rank": "match", "tile": "big"}),  # ballot-match fallback
+    # the MSD-first schedule (the default from 48M keys) at a size where H2 samples and P2
+    # scatters into sampled regions: P1 (grs_onesweep_region) and P2 (grs_onesweep_seg) time out
+    (32, False, 8, {"msd": "always"}),
+    (32, True, 8, {"msd": "always"}),
+    (64, False, 8, {"msd": "always"}),
 ]
+MSD_N = (1 << 27) + 3
 
 
 def _input(gpu, n, key_bits, pairs, seed):
@@ -59,7 +65,7 @@ def test_timeout_surfaces_then_sorter_recovers(gpu, shape):
     from gpuradixsort_amd._lib import GrsError
 
     key_bits, pairs, rb, opts = shape
-    n = 1 << 22
+    n = MSD_N if opts.get("msd") == "always" else 1 << 22
     s = grs.RadixSorter(n, key_bits=key_bits, pairs=pairs, radix_bits=rb, options=opts)
     assert s.get_option("fault_tile") == -1
     # all-ones keys first: the sorter's scratch then holds the largest digit everywhere, so
@@ -69,6 +75,7 @@ def test_timeout_surfaces_then_sorter_recovers(gpu, shape):
     k.view(torch.int32 if key_bits == 32 else torch.int64).fill_(-1)
     s.sort(k, v)
     s.check_error()
+    assert s.check_guards() == 0
     s.set_option("fault_tile", 0)
     assert s.get_option("fault_tile") == 0
     # the keys (and values) sit at the front of larger buffers whose tails must stay untouched
@@ -93,6 +100,8 @@ def test_timeout_surfaces_then_sorter_recovers(gpu, shape):
             "a timed-out sort wrote values past n"
     # the error word is sticky until read: the check above cleared it
     s.check_error()
+    # and a timed-out sort stays inside the sorter's own scratch arrays too
+    assert s.check_guards() == 0, "a timed-out sort wrote past a scratch array (guard band)"
 
     # the same sorter, hook off: the next sort is bit-exact (status buffers, tickets and the
     # alternating control blocks are consistent after a timed-out sort)
@@ -101,9 +110,13 @@ def test_timeout_surfaces_then_sorter_recovers(gpu, shape):
     ek, ev = _expected(k, v)
     s.sort(k, v)
     s.check_error()
+    assert s.check_guards() == 0
     assert (k.cpu().numpy() == ek).all()
     if pairs:
         assert (v.cpu().numpy() == ev).all()
+    s.close()
+    del k, v, kbuf, vbuf
+    torch.cuda.empty_cache()
 
 
 def test_device_wide_check_reports_timeout(gpu):

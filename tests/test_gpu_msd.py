@@ -7,6 +7,11 @@ ParallelSort.cpp:236-298 restated by oracle.ref_parallel_sort) bit for bit.  Key
 path is the u32 keys-without-payload sort, so the check is the sorted multiset -- the same
 output order as the reference's path, which test_u32_matches_reference_path pins for the LSD
 schedule.
+
+Every sort here is followed by the sorter's guard-band check (grs_debug_check_guards): the
+scratch arrays the MSD kernels write (second buffer, region buffer, tables, status buffers)
+end in guard bands, and a kernel that writes past one fails the test even when its output
+happens to come out right (round 5's P2 region spill did exactly that).
 """
 import numpy as np
 import pytest
@@ -43,6 +48,7 @@ def run(keys: np.ndarray, dev, mode="always"):
     s.sort(k)
     torch.cuda.synchronize()
     s.check_error()
+    assert s.check_guards() == 0, "a kernel wrote past a scratch array (guard band)"
     return k.cpu().numpy()
 
 
@@ -89,7 +95,9 @@ def _segment_keys(rng, sizes):
         parts.append(prefix | rng.integers(0, 1 << 16, c, dtype=np.uint32))
     keys = np.concatenate(parts)
     rng.shuffle(keys)
-    return keys
+    # one key of prefix 0xFFFF at the end: the keys vary in their top bit, so the MSD digits
+    # stay the top two bytes (the span-adaptive digit would otherwise move below a constant top)
+    return np.append(keys, np.uint32(0xFFFFFFFF))
 
 
 @pytest.mark.parametrize("sizes", [
@@ -152,6 +160,37 @@ def test_msd_region_spill_redo(gpu):
     assert np.array_equal(run(keys2, gpu), np.sort(keys2))
 
 
+def test_msd_p1_region_spill_stays_in_bounds(gpu):
+    """7120 keys of top byte 0xFF where the sample never looks: digit 255's P1 region (4096 keys,
+    the last region, ending 1024 elements before the second buffer does) is outgrown by ~3000
+    keys.  The run clamp must hold the run inside the buffer (guard bands intact: a build
+    without the clamp overwrites them, tools/diag/canary_no_clamp.py) and the exact redo must
+    sort it -- keys only and u32 pairs."""
+    import gpuradixsort_amd as grs
+
+    n, chunks = 1 << 22, 16384
+    rng = np.random.default_rng(4243)
+    keys = rng.integers(0, 0xFF000000, n, dtype=np.uint64).astype(np.uint32)
+    starts = (np.arange(chunks, dtype=np.uint64) * np.uint64(n - 64) // np.uint64(chunks - 1)).astype(np.int64)
+    seen = np.zeros(n, bool)
+    seen[(starts[:, None] + np.arange(64)[None, :]).ravel()] = True
+    hot = rng.choice(np.flatnonzero(~seen), 4096 + 3024, replace=False)
+    keys[hot] = np.uint32(0xFF000000) | rng.integers(0, 1 << 24, hot.size, dtype=np.uint32)
+    perm = np.argsort(keys, kind="stable")
+    for pairs in (False, True):
+        s = grs.RadixSorter(n, key_bits=32, pairs=pairs, radix_bits=8)   # capacity n: regions fill alt
+        s.set_option("msd", "always")
+        k = torch.from_numpy(keys).to(gpu)
+        v = torch.arange(n, dtype=torch.int32, device=gpu).view(torch.uint32) if pairs else None
+        s.sort(k, v)
+        s.check_error()
+        assert s.check_guards() == 0, pairs
+        assert np.array_equal(k.cpu().numpy(), keys[perm]), pairs
+        if pairs:
+            assert np.array_equal(v.cpu().numpy(), perm.astype(np.uint32))
+        s.close()
+
+
 def run_typed(keys: np.ndarray, dev, pairs: bool, mode="always"):
     kb = keys.dtype.itemsize * 8
     s = msd_sorter(keys.size, mode, kb, pairs)
@@ -160,6 +199,7 @@ def run_typed(keys: np.ndarray, dev, pairs: bool, mode="always"):
     s.sort(k, v)
     torch.cuda.synchronize()
     s.check_error()
+    assert s.check_guards() == 0, "a kernel wrote past a scratch array (guard band)"
     return k.cpu().numpy(), (v.cpu().numpy() if pairs else None)
 
 
@@ -251,6 +291,7 @@ def test_msd_p2_region_spill(gpu):
     piece = (np.arange(n, dtype=np.int64) // PIECE) % 2
     keys = np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)
     keys |= rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    keys[-1] |= np.uint32(1 << 31)   # the top byte varies: P1 / P2 stay on bytes 3 / 2
     got = run(keys, gpu, "always")
     assert np.array_equal(got, np.sort(keys))
     keys2 = rng.integers(0, 1 << 32, n, dtype=np.uint32)
@@ -289,6 +330,7 @@ def test_msd_pairs_sampled_p2(gpu):
         piece = (np.arange(n, dtype=np.int64) // PIECE) % 2
         spill = (np.where(piece == 0, 0, 255).astype(np.uint32) << np.uint32(16)) | \
             rng.integers(0, 1 << 16, n, dtype=np.uint32)
+        spill[-1] |= np.uint32(1 << 31)   # the top byte varies: P1 / P2 stay on bytes 3 / 2
         dup = rng.integers(0, 1 << 32, n, dtype=np.uint32)
         dup[::3] = dup[1]
         for name, keys in (("dup", dup), ("p2_spill", spill)):
@@ -297,6 +339,7 @@ def test_msd_pairs_sampled_p2(gpu):
             s.sort(k, v)
             torch.cuda.synchronize()
             s.check_error()
+            assert s.check_guards() == 0, name
             perm = np.argsort(keys, kind="stable")
             assert np.array_equal(k.cpu().numpy(), keys[perm]), name
             assert np.array_equal(v.cpu().numpy(), perm.astype(np.uint32)), name

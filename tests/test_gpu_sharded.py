@@ -189,3 +189,31 @@ def test_region_spill_redo(gpu, world1, key_bits, pairs):
     assert s.redo_count() == before + 2
     assert np.array_equal(ko.cpu().numpy(), keys[perm])
     s.sorter.close()
+
+
+@pytest.mark.parametrize("n", [300_007, 1 << 20])
+@pytest.mark.parametrize("dist_name", ["uniform", "ties", "span_redo"])
+def test_presorted_out_of_place_msd(gpu, world1, n, dist_name):
+    """The presorted exchange sorts its shard OUT OF PLACE (input -> the output tensor): with
+    option msd=always that is the MSD schedule's src_in path (the sample, P1 and P1's redo read
+    the caller's input; the result lands in the output).  span_redo: keys below 2^20 with a few
+    top-bit keys where the span guess does not look, so P1's exact span redoes it.  Output ==
+    the stable sort; the input tensor is left as it was."""
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    rng = np.random.default_rng(n + len(dist_name))
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    if dist_name == "ties":
+        keys[::3] = keys[1]
+    elif dist_name == "span_redo":
+        keys = rng.integers(0, 1 << 20, n, dtype=np.uint64).astype(np.uint32)
+        keys[[100, 101, n // 2 + 100, n - 100]] |= np.uint32(1 << 31)   # off the 64 guess chunks
+    s = ShardedSorter(n, key_bits=32, device=gpu, comm=world1,
+                      options={"sharded_path": "general", "msd": "always"})
+    k = torch.from_numpy(keys).to(gpu)
+    ko, _ = s.sort(k)
+    assert s.last_n_out == n
+    assert np.array_equal(ko.cpu().numpy(), np.sort(keys, kind="stable"))
+    assert np.array_equal(k.cpu().numpy(), keys)
+    assert s.sorter.check_guards() == 0
+    s.sorter.close()

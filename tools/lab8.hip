@@ -1,0 +1,77 @@
+// lab8.hip — round-6 laboratory (not part of libgrs): P3 (grs::LocalSort, grs_msd.hpp) with
+// one-dword-per-lane HBM accesses (the shipped round-5 form) against 16-B accesses through LDS,
+// on segments of P3's real geometry: variable lengths, read from regions at any alignment,
+// written packed at any alignment (tools/lab8.py).
+//   MODE 0  dword striped loads, dword stores (LocalSort::run, round 5)
+//   MODE 1  dword striped loads, 16-B stores (LocalSort::run_vec<false>)
+//   MODE 2  16-B LDS-DMA loads (global_load_lds_dwordx4), 16-B stores (LocalSort::run_vec<true>)
+#include <hip/hip_runtime.h>
+
+#include "../gpuradixsort_amd/csrc/grs_msd.hpp"
+
+namespace {
+
+template <int BLOCK, int I, bool C16, int MODE>
+__global__ __launch_bounds__(BLOCK) void lab_p3v(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                 const uint32_t* __restrict__ inoff,
+                                                 const uint32_t* __restrict__ outoff,
+                                                 const uint32_t* __restrict__ lens, int rounds) {
+  using LS = grs::LocalSort<uint32_t, false, BLOCK, I, C16, 2>;
+  __shared__ typename LS::Smem sm;
+  const uint32_t len = lens[blockIdx.x];
+  if (len == 0) return;
+  const uint32_t* kin = in + inoff[blockIdx.x];
+  uint32_t* kout = out + outoff[blockIdx.x];
+  if constexpr (MODE == 0) LS::run(sm, kin, nullptr, kout, nullptr, 0u, len, rounds);
+  else LS::template run_vec<MODE == 2>(sm, kin, nullptr, kout, nullptr, len, rounds);
+}
+
+// u64 keys (C5's P3): MODE 0 = LocalSort::run (6 rounds), 1 / 2 = run_vec<false / true> (2 rounds +
+// the runs finished by insertion)
+template <int BLOCK, int I, int MODE>
+__global__ __launch_bounds__(BLOCK) void lab_p3w(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+                                                 const uint32_t* __restrict__ inoff,
+                                                 const uint32_t* __restrict__ outoff,
+                                                 const uint32_t* __restrict__ lens, int rounds) {
+  using LS = grs::LocalSort<uint64_t, false, BLOCK, I, false>;
+  __shared__ typename LS::Smem sm;
+  const uint32_t len = lens[blockIdx.x];
+  if (len == 0) return;
+  const uint64_t* kin = in + inoff[blockIdx.x];
+  uint64_t* kout = out + outoff[blockIdx.x];
+  if constexpr (MODE == 0) LS::run(sm, kin, nullptr, kout, nullptr, 0u, len, rounds);
+  else LS::template run_vec<MODE == 2>(sm, kin, nullptr, kout, nullptr, len, rounds);
+}
+
+}  // namespace
+
+extern "C" int lab8_p3w(int block, int items, int mode, int rounds, const uint64_t* in, uint64_t* out,
+                        const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens, uint32_t nseg,
+                        void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (block == 256 && items == 20 && mode == 0)
+    hipLaunchKernelGGL((lab_p3w<256, 20, 0>), dim3(nseg), dim3(256), 0, s, in, out, inoff, outoff, lens, rounds);
+  else if (block == 256 && items == 20 && mode == 1)
+    hipLaunchKernelGGL((lab_p3w<256, 20, 1>), dim3(nseg), dim3(256), 0, s, in, out, inoff, outoff, lens, rounds);
+  else if (block == 256 && items == 20 && mode == 2)
+    hipLaunchKernelGGL((lab_p3w<256, 20, 2>), dim3(nseg), dim3(256), 0, s, in, out, inoff, outoff, lens, rounds);
+  else
+    return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int lab8_p3(int block, int items, int c16, int mode, int rounds, const uint32_t* in, uint32_t* out,
+                       const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens, uint32_t nseg,
+                       void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define P3(B, I, C, M)                                                                                     \
+  if (block == B && items == I && c16 == C && mode == M) {                                                \
+    hipLaunchKernelGGL((lab_p3v<B, I, C != 0, M>), dim3(nseg), dim3(B), 0, s, in, out, inoff, outoff, lens, \
+                       rounds);                                                                           \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                      \
+  }
+  P3(768, 24, 1, 0) P3(768, 24, 1, 1) P3(768, 24, 1, 2)
+  P3(256, 20, 0, 0) P3(256, 20, 0, 1) P3(256, 20, 0, 2)
+#undef P3
+  return -1;
+}
