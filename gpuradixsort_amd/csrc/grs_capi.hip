@@ -308,6 +308,8 @@ struct grs_sorter {
   int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
+  int seg_route = 0;               // GRS_OPT_SEG_ROUTE: 0 by shape, 1 segmented passes, 2 one
+                                   // composite-key sort (grs_sort_segmented's longer segments)
   int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
                                    // 2 = 1 with P2's regions refused (test hook: the exact redo)
   // The MSD sort's scratch (msd_scratch): allocated at grs_create from kMsdMinN items of capacity,
@@ -723,6 +725,10 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value < -1 || value > 2) return bad();
       s->msd_mode = value;
       break;
+    case GRS_OPT_SEG_ROUTE:
+      if (value < 0 || value > 2) return bad();
+      s->seg_route = value;
+      break;
 
     default:
       return set_err(GRS_EINVAL, "grs_set_option: unknown option");
@@ -763,6 +769,7 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_MERGE: *value = s->merge_mode; break;
     case GRS_OPT_FAULT_TILE: *value = s->fault_tile; break;
     case GRS_OPT_MSD: *value = s->msd_mode; break;
+    case GRS_OPT_SEG_ROUTE: *value = s->seg_route; break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -902,7 +909,7 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc, uint32_t* vdst,
                        uint32_t n, const DigitF& dig, const DigitF* dig_dev, const uint32_t* hist,
                        uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt, hipStream_t stream,
-                       uint32_t expect_tile = 0) {
+                       uint32_t expect_tile = 0, const uint32_t* plan = nullptr) {
   const uint32_t tiles = (n + Tile::TILE - 1) / Tile::TILE;
   if (status_words_for(tiles, 1u << RB) > s->status_words)
     return set_err(GRS_ECAPACITY, "status buffer too small (pass: " + std::to_string(tiles) + " tiles, have " +
@@ -914,12 +921,12 @@ grs_status launch_pass(grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc
     hipLaunchKernelGGL((grs::grs_onesweep_v6<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(grid), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev, plan);
   } else {
     hipLaunchKernelGGL((grs::grs_onesweep_v4<K, PAIRS, RB, Tile::BLOCK, Tile::ITEMS, Tile::MINW,
                                              OPT, DigitF>),
                        dim3(tiles), dim3(Tile::BLOCK), 0, stream, src, dst, vsrc, vdst, n, dig, hist,
-                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev);
+                       ticket, st_cur, st_nxt, s->ctrl + GRS_CTRL_ERROR, dig_dev, plan);
   }
   GRS_HIP(hipGetLastError());
   return GRS_OK;
@@ -931,7 +938,7 @@ template <typename K, bool PAIRS, int RB, typename Tile, uint32_t OPT, bool PERS
 grs_status launch_rec(int kind, grs_sorter* s, const K* src, K* dst, const uint32_t* vsrc,
                       uint32_t* vdst, uint32_t n, const grs::RadixDigit<K>& dig,
                       const uint32_t* hist, uint32_t* ticket, uint32_t* st_cur, uint32_t* st_nxt,
-                      hipStream_t stream, uint32_t expect_tile) {
+                      hipStream_t stream, uint32_t expect_tile, const uint32_t* plan = nullptr) {
   using Dig = grs::RadixDigit<K>;
   constexpr bool R = sizeof(K) == 4 && PAIRS && RB == 8;
   constexpr uint32_t W = R ? 8192u : 0u, Rd = R ? 4096u : 0u, RS = R ? 16384u : 0u, WS = R ? 32768u : 0u;
@@ -940,7 +947,7 @@ grs_status launch_rec(int kind, grs_sorter* s, const K* src, K* dst, const uint3
     case 2: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
     case 3: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | RS | W, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
     case 4: return launch_pass<K, PAIRS, RB, Tile, OPT | Rd | W | WS, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
-    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile);
+    default: return launch_pass<K, PAIRS, RB, Tile, OPT, PERSIST>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, hist, ticket, st_cur, st_nxt, stream, expect_tile, plan);
   }
 }
 
@@ -1078,28 +1085,38 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
       return GRS_OK;
     }
   }
+  // the pass plan (grs_pass_plan): passes whose digit is the same for every key are skipped or
+  // become one copy (record passes and out-of-place sorts keep every pass)
+  const uint32_t* plan = nullptr;
+  if (!rec && !src_in && passes >= 2) {
+    uint32_t* const pw = s->ctrl + GRS_CTRL_PLAN;
+    hipLaunchKernelGGL(grs::grs_pass_plan, dim3(1), dim3(64), 0, stream, hist, static_cast<uint32_t>(RADIX), passes, n, pw);
+    GRS_HIP(hipGetLastError());
+    plan = pw;
+  }
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + p * RB;
     const int bits = std::min(RB, end_bit - shift);
     uint32_t* st_cur = (p & 1) ? st1 : st0;
+    const uint32_t* pp = plan ? plan + p : nullptr;
     uint32_t* st_nxt = (p & 1) ? st0 : st1;
     const Dig dig{shift, (1u << bits) - 1u};
     const uint32_t* ph = hist + p * GRS_HIST_PASS_STRIDE;
     uint32_t* tk = tickets + p * GRS_XCDS;
     if (s->rank_mode != 0) {
-      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile)
-              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile);
+      r = big ? launch_pass<K, PAIRS, RB, MatchTile<K, PAIRS>, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, pp)
+              : launch_pass<K, PAIRS, RB, Small, kMatchOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, pp);
     } else if (xl) {
       if constexpr (kXlType)
-        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
+        r = launch_rec<K, PAIRS, RB, XL, XL::OPT, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, pp);
     } else if (persist && big) {
       if constexpr (!Big::TWO_ROUNDS)
-        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
+        r = launch_rec<K, PAIRS, RB, Big, kBig, true>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile, pp);
     } else if (big && rec) {
       r = launch_rec<K, PAIRS, RB, Big, kBig, false>(rec_kind(p), s, src, dst, vsrc, vdst, n, dig, ph, tk, st_cur, st_nxt, stream, tile);
     } else {
-      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile)
-              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile);
+      r = big ? launch_pass<K, PAIRS, RB, Big, kBig>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, pp)
+              : launch_pass<K, PAIRS, RB, Small, kSmallOpt>(s, src, dst, vsrc, vdst, n, dig, (const Dig*)nullptr, ph, tk, st_cur, st_nxt, stream, tile, pp);
     }
     if (r != GRS_OK) return r;
     if ((r = mark()) != GRS_OK) return r;
@@ -2241,6 +2258,10 @@ grs_status sort_segmented_msd_any(grs_sorter* s, K* keys, uint32_t* vals, uint32
 
 extern "C" {
 
+// grs_sort_segmented: below this average segment length (and past the LDS-sized segments) the
+// composite-key sort instead of the segmented passes
+static constexpr size_t kSegRouteMinAvg = 0;
+
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
                               const uint32_t* d_offsets, int num_segments, void* stream) {
   if (!s) return set_err(GRS_EINVAL, "grs_sort_segmented: NULL sorter");
@@ -2316,7 +2337,11 @@ grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, siz
   // by one (each a whole sort: MSD or LSD); segments of 4K keys and more on average whose top-byte
   // runs fit LDS take the top-byte scatter + LDS sorts; anything else the segmented LSD
   const size_t avg = n / static_cast<size_t>(num_segments);
-  if (s->rank_mode == 0 && s->radix_bits == 8 &&
+  // segmented passes launch a workgroup per segment at least (a segment shorter than a tile is a
+  // solo tile), so very many short segments beside a long one take the composite-key sort
+  // (kSegRouteMinAvg: tools/bench_seg_route.py)
+  const bool seg_passes = s->seg_route == 1 || (s->seg_route == 0 && avg >= kSegRouteMinAvg);
+  if (s->rank_mode == 0 && s->radix_bits == 8 && seg_passes && s->seg_route != 2 &&
       !(num_segments <= GRS_MAX_SPLITTERS + 1 && avg >= (size_t(1) << 22))) {
     int prev = 0;
     GRS_HIP(hipGetDevice(&prev));

@@ -53,9 +53,11 @@
 //   GRS_CTRL_TICKETS + pass * 8        per-pass tile ticket counter
 //   GRS_CTRL_ERROR                     nonzero = a bounded spin timed out; [1], [2] the pass's
 //                                      debug words (grs_pass.hpp PassDebug)
+//   GRS_CTRL_PLAN + pass               the LSD sort's pass plan (grs_pass_plan), written each call
 #define GRS_MAX_PASSES 16               // u64 keys at 4-bit digits
 #define GRS_HIST_PASS_STRIDE 256
 #define GRS_CTRL_HIST_WORDS (GRS_MAX_PASSES * GRS_HIST_PASS_STRIDE)
 #define GRS_CTRL_TICKETS GRS_CTRL_HIST_WORDS
 #define GRS_CTRL_ERROR (GRS_CTRL_TICKETS + GRS_MAX_PASSES * GRS_XCDS)
-#define GRS_CTRL_WORDS (GRS_CTRL_ERROR + 16)   // multiple of 4 words (16-B memset)
+#define GRS_CTRL_PLAN (GRS_CTRL_ERROR + 16)
+#define GRS_CTRL_WORDS (GRS_CTRL_PLAN + GRS_MAX_PASSES)   // multiple of 4 words (16-B memset)

@@ -378,6 +378,37 @@ __global__ __launch_bounds__(256) void grs_lb_totals(const uint32_t* __restrict_
   }
 }
 
+// The LSD sort's pass plan (one wave, after the upfront histogram): pass p is TRIVIAL when one
+// digit holds all n keys -- its stable scatter is the identity (the reference's own input,
+// 0..N-1 shuffled, has log2 N varying bits: at N = 2^24 the 4-bit passes 6 and 7 see one
+// digit).  plan[p] = 0 run the pass, 1 copy the keys through unchanged, 2 skip it: a maximal run
+// of trivial passes of even length is skipped (every pass flips the buffers, so the data ends
+// where it would have), one of odd length copies once and skips the rest.  The number of
+// buffer flips keeps its parity, so the host's copy-back decision stands.
+enum PassPlan : uint32_t { kPassRun = 0, kPassCopy = 1, kPassSkip = 2 };
+__global__ __launch_bounds__(64) void grs_pass_plan(const uint32_t* __restrict__ hist, uint32_t radix,
+                                                    int passes, uint32_t n, uint32_t* __restrict__ plan) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t trivial = 0;   // bit p: pass p sees one digit
+  for (int p = 0; p < passes; ++p) {
+    bool one = false;
+    for (uint32_t d = lane; d < radix; d += 64) one |= hist[p * GRS_HIST_PASS_STRIDE + d] == n;
+    if (__ballot(one) != 0ull) trivial |= 1u << p;
+  }
+  if (lane == 0) {
+    for (int p = 0; p < passes;) {
+      if (!((trivial >> p) & 1u)) {
+        plan[p++] = kPassRun;
+        continue;
+      }
+      int e = p;
+      while (e < passes && ((trivial >> e) & 1u)) ++e;
+      for (int q = p; q < e; ++q) plan[q] = ((e - p) & 1) && q == p ? kPassCopy : kPassSkip;
+      p = e;
+    }
+  }
+}
+
 // Control block and look-back status of a region-mode partition pass, in one launch instead of
 // three memsets: ctrl[0, ctrl_words) = 0 (digit counts, tickets), then the count + 1 digit
 // "counts" = region (the pass's digit-start scan yields b * region), status[0, words) = 0.

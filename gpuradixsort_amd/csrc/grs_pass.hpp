@@ -724,8 +724,33 @@ __device__ __forceinline__ uint32_t onesweep_tile(
   return next;
 }
 
+// A tile of a pass the LSD plan elides (grs_pass_plan: the pass's digit is the same for every
+// key, so its stable scatter is the identity): the tile's words of the next pass's status
+// zeroed as onesweep_tile would (the next pass's look-back reads them), and for kPassCopy its
+// keys (and payload) copied to the same indices.
+template <typename K, bool PAIRS, int RADIX, int BLOCK>
+__device__ __forceinline__ void elided_tile(uint32_t mode, const TileSpan& sp, const K* __restrict__ keys_in,
+                                            K* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+                                            uint32_t* __restrict__ vals_out, uint32_t* __restrict__ status_next) {
+  const uint32_t t = threadIdx.x;
+  if (t < static_cast<uint32_t>(RADIX)) {
+    status_next[static_cast<size_t>(sp.tile) * RADIX + t] = 0;
+    if (sp.jg == 0) {
+      status_next[static_cast<size_t>(sp.tiles + sp.group) * RADIX + t] = 0;
+      status_next[static_cast<size_t>(sp.tiles + sp.groups + sp.group) * RADIX + t] = 0;
+    }
+  }
+  if (mode == kPassCopy) {
+    for (uint32_t i = t; i < sp.valid; i += BLOCK) {
+      keys_out[sp.base + i] = keys_in[sp.base + i];
+      if constexpr (PAIRS) vals_out[sp.base + i] = vals_in[sp.base + i];
+    }
+  }
+}
+
 // One tile per workgroup (grid = tiles), tile ids from a ticket counter.  dig_dev: when not
-// null, the digit functor is read from device memory instead of the `dig` argument.
+// null, the digit functor is read from device memory instead of the `dig` argument.  plan
+// (nullable): this pass's word of grs_pass_plan -- an elided pass only zeroes (and copies).
 template <typename K, bool PAIRS, int RB, int BLOCK, int ITEMS, int MINW, int OPT = 0,
           typename DigitF = RadixDigit<K>>
 __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
@@ -733,7 +758,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev,
+    const uint32_t* __restrict__ plan = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
@@ -741,12 +767,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v4(
   asm volatile("" : "+v"(tt));
   K key[ITEMS];
   uint32_t val[ITEMS];
+  const uint32_t mode = plan != nullptr ? __builtin_amdgcn_readfirstlane(*plan) : 0u;
   if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   // digit functor computed on the device (multi-GPU splitters): uniform scalar loads
   const DigitF dg = dig_dev != nullptr ? *dig_dev : dig;
   __syncthreads();
   const uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+  if (mode != 0u) {
+    elided_tile<K, PAIRS, SM::RADIX, BLOCK>(mode, TileSpan::whole(tile, n, SM::TILE), keys_in, keys_out, vals_in,
+                                            vals_out, status_next);
+    return;
+  }
   tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, tt);
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
   onesweep_tile<K, PAIRS, RB, BLOCK, ITEMS, OPT>(sm, TileSpan::whole(tile, n, SM::TILE), key, val,
@@ -825,10 +857,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
     uint32_t* __restrict__ vals_out, uint32_t n, const DigitF dig,
     const uint32_t* __restrict__ pass_hist, uint32_t* __restrict__ ticket,
     uint32_t* __restrict__ status, uint32_t* __restrict__ status_next,
-    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev) {
+    uint32_t* __restrict__ error_word, const DigitF* __restrict__ dig_dev,
+    const uint32_t* __restrict__ plan = nullptr) {
   using SM = V4SmemFor<K, PAIRS, RB, BLOCK, ITEMS, OPT, DigitF>;
   __shared__ SM sm;
   const uint32_t t = threadIdx.x;
+  const uint32_t mode = plan != nullptr ? __builtin_amdgcn_readfirstlane(*plan) : 0u;
   if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
   for (uint32_t i = t; i < sizeof(sm.cnt) / 4; i += BLOCK) sm.cnt[i] = 0;
   const uint32_t gh = t < static_cast<uint32_t>(SM::RADIX) ? pass_hist[t] : 0u;
@@ -837,6 +871,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_onesweep_v6(
   __syncthreads();
   const uint32_t tiles = (n + SM::TILE - 1) / SM::TILE;
   uint32_t tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+  if (mode != 0u) {   // an elided pass (grs_pass_plan): the same ticket loop, zeroing / copying
+    while (tile < tiles) {
+      elided_tile<K, PAIRS, SM::RADIX, BLOCK>(mode, TileSpan::whole(tile, n, SM::TILE), keys_in, keys_out,
+                                              vals_in, vals_out, status_next);
+      __syncthreads();   // every thread has read sm.ticket
+      if (t == 0) sm.ticket = atomicAdd(ticket, 1u);
+      __syncthreads();
+      tile = __builtin_amdgcn_readfirstlane(sm.ticket);
+    }
+    return;
+  }
   K key[ITEMS];
   uint32_t val[ITEMS];
   if (tile < tiles) tile_load<K, PAIRS, BLOCK, ITEMS, OPT>(key, val, keys_in, vals_in, n, tile, t);

@@ -166,7 +166,7 @@ typedef enum grs_option {
                                 polls, so the later tiles of its look-back group time out: the
                                 sort's output is wrong and GRS_ETIMEOUT surfaces through
                                 grs_check_error / grs_stream_check_error (the error path's test) */
-  GRS_OPT_MSD = 11           /* u32 keys, u32 keys + u32 payload, u64 keys; 8-bit digits, the
+  GRS_OPT_MSD = 11,          /* u32 keys, u32 keys + u32 payload, u64 keys; 8-bit digits, the
                                 whole key: -1 by size (default: from 48M keys), 0 never, 1 always
                                 -- the MSD-first sort (two stable scatters by the top two bytes
                                 into 65536 segments, each finished in LDS by one workgroup;
@@ -179,6 +179,9 @@ typedef enum grs_option {
                                 elements, grs_scratch_bytes), 1 / 2 allocate it (GRS_ENOMEM if it
                                 does not fit), -1 keeps it from 48M items of capacity; a change
                                 synchronises the device */
+  GRS_OPT_SEG_ROUTE = 12     /* grs_sort_segmented past the LDS-sized segments: 0 (default) by
+                                shape, 1 the segmented passes (top-byte scatter + LDS runs, or the
+                                segmented LSD), 2 one sort of composite (segment, key) keys */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);

@@ -171,3 +171,70 @@ def test_fill_permutation_is_a_permutation(gpu, total):
     part = torch.empty(total // 3, dtype=torch.uint32, device=gpu)
     grs.fill_permutation(part, 99, total=total, first_index=total // 3)
     assert np.array_equal(part.cpu().numpy(), h[total // 3: total // 3 + total // 3])
+
+
+def _lsd_cases(n, kb, rng):
+    """Inputs whose LSD digits are partly constant: the passes grs_pass_plan elides."""
+    dt = np.uint32 if kb == 32 else np.uint64
+    top = np.iinfo(dt).max
+    yield "perm", rng.permutation(n).astype(dt)                       # main.cpp:119-125
+    yield "all_equal", np.full(n, 0x5A, dt)                          # every pass constant
+    yield "low_byte", rng.integers(0, 256, n).astype(dt)             # 3 (7) trivial top passes
+    yield "hole", ((rng.integers(0, top, n, dtype=dt, endpoint=True) & dt(~(0xFF << 16) & top))
+                   | dt(0xAB << 16))                                 # a constant middle byte
+    yield "top_only", rng.integers(0, 256, n).astype(dt) << dt(kb - 8)   # low passes constant
+
+
+@pytest.mark.parametrize("radix_bits", [4, 8])
+@pytest.mark.parametrize("kb,pairs", [(32, False), (32, True), (64, False), (64, True)])
+def test_lsd_elides_constant_digits(gpu, radix_bits, kb, pairs):
+    """The LSD schedule (below 48M keys, and every 4-bit sort) skips the passes whose digit is
+    the same for every key, or turns an odd run of them into one copy (grs_pass_plan): keys and
+    the stable permutation must come out as the stable sort, at a small-tile and a big-tile size,
+    with the sorter's guard bands intact."""
+    import gpuradixsort_amd as grs
+
+    for n in (300_007, (1 << 22) + 1):
+        rng = np.random.default_rng(n + kb + radix_bits + pairs)
+        s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=radix_bits)
+        for name, keys in _lsd_cases(n, kb, rng):
+            k = torch.from_numpy(keys).to(gpu)
+            v = torch.arange(n, dtype=torch.int32, device=gpu).view(torch.uint32) if pairs else None
+            s.sort(k, v)
+            s.check_error()
+            perm = np.argsort(keys, kind="stable")
+            assert np.array_equal(k.cpu().numpy(), keys[perm]), (name, n)
+            if pairs:
+                assert np.array_equal(v.cpu().numpy(), perm.astype(np.uint32)), (name, n)
+        assert s.check_guards() == 0
+        s.close()
+
+
+def test_lsd_plan_c2_reference_input(gpu):
+    """BASELINE C2's size and digit width (2^24 u32 keys, 4-bit LSD) on the reference's input:
+    sorted to 0..n-1 exactly, and faster than the same sort of uniform keys (passes 6 and 7 see
+    one digit and are skipped)."""
+    import gpuradixsort_amd as grs
+
+    n = 1 << 24
+    s = grs.RadixSorter(n, key_bits=32, radix_bits=4)
+    k = torch.empty(n, dtype=torch.uint32, device=gpu)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = {}
+    for dist in ("uniform", "perm"):
+        ts = []
+        for i in range(6):
+            if dist == "perm":
+                grs.fill_permutation(k, 7 + i)
+            else:
+                grs.fill_splitmix(k, 7 + i)
+            e0.record()
+            s.sort(k)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ms[dist] = sorted(ts[1:])[2]
+    s.check_error()
+    assert torch.equal(k.view(torch.int32).to(torch.int64), torch.arange(n, device=gpu))
+    assert ms["perm"] < ms["uniform"], ms
+    s.close()
