@@ -66,6 +66,7 @@ OPTIONS = {
     "fault_tile": (10, {"off": -1}),   # test hook: tile v of every pass never publishes
     "msd": (11, {"size": -1, "never": 0, "always": 1, "exact_p2": 2}),
     "seg_route": (12, {"shape": 0, "passes": 1, "composite": 2}),
+    "h2_chunk": (13, {"size": 0}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares

@@ -308,6 +308,7 @@ struct grs_sorter {
   int xl_mode = 0;                 // GRS_OPT_XL: 0 by size, 1 wherever big tiles run, 2 never
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
+  uint32_t h2_chunk = 0;           // GRS_OPT_H2_CHUNK: 0 by size, else H2's chunk (keys per block)
   int seg_route = 0;               // GRS_OPT_SEG_ROUTE: 0 by shape, 1 segmented passes, 2 one
                                    // composite-key sort (grs_sort_segmented's longer segments)
   int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
@@ -573,8 +574,11 @@ size_t max_status_words(const grs_sorter* s, size_t cap, size_t radix) {
   const size_t big = std::min(BigTile<K, PAIRS>::TILE, BigTile4<K, PAIRS>::TILE);
   const size_t small = SmallTile<K, PAIRS>::TILE;
   size_t w0 = 0;
-  // small tiles are used below one big tile per CU (or everywhere when forced)
-  const size_t small_cap = s->tile_mode == 0 ? cap : std::min(cap, big * std::max(1, s->cus));
+  // small tiles are used below one big tile per CU (or everywhere when forced): below the
+  // LARGER of the two big tiles per CU (use_big_tiles asks with the sort's own big tile; sized
+  // with the smaller one, u32 pairs and u64 sorts of 4.19M-4.46M items were refused)
+  const size_t big_max = std::max(BigTile<K, PAIRS>::TILE, BigTile4<K, PAIRS>::TILE);
+  const size_t small_cap = s->tile_mode == 0 ? cap : std::min(cap, big_max * std::max(1, s->cus));
   const size_t match = MatchTile<K, PAIRS>::TILE;
   w0 = status_words_for((cap + match - 1) / match, radix);
   size_t w = std::max(std::max(w0, status_words_for((cap + big - 1) / big, radix)),
@@ -729,6 +733,10 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value < 0 || value > 2) return bad();
       s->seg_route = value;
       break;
+    case GRS_OPT_H2_CHUNK:
+      if (value != 0 && (value < 4096 || value > (1 << 20) || (value & (value - 1)) != 0)) return bad();
+      s->h2_chunk = static_cast<uint32_t>(value);
+      break;
 
     default:
       return set_err(GRS_EINVAL, "grs_set_option: unknown option");
@@ -770,6 +778,7 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_FAULT_TILE: *value = s->fault_tile; break;
     case GRS_OPT_MSD: *value = s->msd_mode; break;
     case GRS_OPT_SEG_ROUTE: *value = s->seg_route; break;
+    case GRS_OPT_H2_CHUNK: *value = static_cast<int>(s->h2_chunk); break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -1288,7 +1297,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   }
   // sample: the top byte's histogram; zeroes P1's status, the next call's control block, h2
   // and the big-segment counters
-  hipLaunchKernelGGL((grs::grs_msd_sample<K>), dim3(1024), dim3(256), 0, stream, src, n, samp, st[0],
+  hipLaunchKernelGGL((grs::grs_msd_sample<K>), dim3(std::max(1, s->cus)), dim3(256), 0, stream, src, n, samp, st[0],
                      static_cast<uint32_t>(words1), hist_next, h2, static_cast<uint32_t>(L.clear), span);
   GRS_HIP(hipGetLastError());
   s->cb_i ^= 1;
@@ -1346,6 +1355,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   uint32_t shift = 0;
   while (shift < 3 && (static_cast<uint64_t>(n) >> (shift + 1)) >= 65536ull * 1024) ++shift;
   chunk = std::min<uint32_t>(chunk << shift, 1u << 20);   // sampled: about as many keys a block
+  if (s->h2_chunk != 0) chunk = s->h2_chunk;             // (GRS_OPT_H2_CHUNK: A/B runs)
   // the region buffer's room (option msd = 2, a test hook: none, so the exact redo runs)
   const uint64_t cap2 = s->msd_mode == 2 ? 0 : static_cast<uint64_t>(msd_alt2_words(s->capacity));
   {
@@ -2259,8 +2269,10 @@ grs_status sort_segmented_msd_any(grs_sorter* s, K* keys, uint32_t* vals, uint32
 extern "C" {
 
 // grs_sort_segmented: below this average segment length (and past the LDS-sized segments) the
-// composite-key sort instead of the segmented passes
-static constexpr size_t kSegRouteMinAvg = 0;
+// composite-key sort instead of the segmented passes, which launch a workgroup per segment at
+// least (tools/bench_seg_route.py, one 16M-key segment beside short ones, 2^24-2^25 keys in all:
+// 1M x 4 keys 318 vs 1.4 ms, 16K x 1024 5.1 vs 1.6, 8K x 2048 2.7 vs 1.6, 4K x 4096 0.85 vs 1.6)
+static constexpr size_t kSegRouteMinAvg = 4096;
 
 grs_status grs_sort_segmented(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n,
                               const uint32_t* d_offsets, int num_segments, void* stream) {

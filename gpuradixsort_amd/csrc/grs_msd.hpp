@@ -322,11 +322,19 @@ __global__ __launch_bounds__(256) void grs_msd_sample(const K* __restrict__ keys
   auto bin = [&](K k) { return static_cast<uint32_t>(k >> top) & 255u; };
   constexpr uint32_t C = GRS_MSD_SAMPLE_CHUNKS;
   if (n <= C * GRS_WAVE) {
-    for (uint32_t i = blockIdx.x * 256 + t; i < n; i += gs)
-      atomicAdd(&h[bin(keys[i])], 1u);
+    for (uint32_t i0 = blockIdx.x * 256 + t; i0 < n; i0 += 4 * gs) {   // four loads in flight
+      K x[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) x[u] = i0 + u * gs < n ? keys[i0 + u * gs] : K(0);
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (i0 + u * gs < n) atomicAdd(&h[bin(x[u])], 1u);
+    }
   } else {
-    // every wave's chunks loaded before any is counted (the loads overlap)
-    constexpr uint32_t U = 4;
+    // every wave's chunks loaded before any is counted (the loads overlap): one block per CU, 16
+    // chunks per wave in flight (1024 blocks adding 256 counts each into the same 256 words cost
+    // 24 us at 2^28 under the profiler, round 5)
+    constexpr uint32_t U = 16;
     const uint32_t waves = gridDim.x * 4;
     for (uint32_t c0 = blockIdx.x * 4 + (t >> 6); c0 < C; c0 += U * waves) {
       K k[U];
@@ -683,9 +691,22 @@ struct LocalSort {
   // 16-B vectors of keys / values; the arrays hold SMAX + one vector, so that element p can sit
   // at p + a (a < vector) with a the misalignment of the HBM run it comes from or goes to
   static constexpr uint32_t KV = 16 / sizeof(K), VV = 4;
+  // LDS positions are swizzled: element x sits at swz(x), which XORs the 16-B group index inside
+  // each 64-group with bits 8.. of x.  A rounds' scatter whose digit runs are all 256 long (the
+  // reference's 0..N-1 shuffled: every 16-bit segment of 2^30 keys holds each value of its low 14
+  // bits once) sends a wave-instruction's 64 keys to 64 run starts 256 apart -- one LDS bank,
+  // a 64-way conflict that made P3 1.8x slower; swizzled, at most 4 lanes share a bank.  The
+  // 16-B groups stay whole, so copy_out's vector reads stand.
+  template <uint32_t V>   // V elements per 16-B group
+  __device__ __forceinline__ static uint32_t swz_t(uint32_t x) {
+    return x ^ (((x >> 8) & 15u) << (V == 4 ? 2 : V == 2 ? 1 : 0));
+  }
+  __device__ __forceinline__ static uint32_t swz(uint32_t x) { return swz_t<KV>(x); }
+  __device__ __forceinline__ static uint32_t swzv(uint32_t x) { return swz_t<VV>(x); }
+  static constexpr uint32_t SK = (SMAX + KV + 63) / 64 * 64;   // swz stays inside a 64-group
   struct Smem {
-    alignas(16) K sk[SMAX + KV];
-    alignas(16) uint32_t sv[PAIRS ? SMAX + VV : 4];
+    alignas(16) K sk[SK];
+    alignas(16) uint32_t sv[PAIRS ? (SMAX + VV + 63) / 64 * 64 : 4];
     uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
     uint32_t wtot[4];
     uint32_t slot;
@@ -774,8 +795,8 @@ struct LocalSort {
         const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
         if (i < len) {
           const uint32_t dst = cld(w * 256 + digit(k[j])) + r[j];
-          sm.sk[dst + sk_off] = k[j];
-          if constexpr (PAIRS) sm.sv[dst + sv_off] = v[j];
+          sm.sk[swz(dst + sk_off)] = k[j];
+          if constexpr (PAIRS) sm.sv[swzv(dst + sv_off)] = v[j];
         }
       }
       __syncthreads();
@@ -784,8 +805,8 @@ struct LocalSort {
         for (uint32_t j = 0; j < I; ++j) {
           const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
           if (i < len) {
-            k[j] = sm.sk[i];
-            if constexpr (PAIRS) v[j] = sm.sv[i];
+            k[j] = sm.sk[swz(i)];
+            if constexpr (PAIRS) v[j] = sm.sv[swzv(i)];
           }
         }
       }
@@ -794,8 +815,8 @@ struct LocalSort {
   // the sorted segment from LDS to HBM, consecutive threads on consecutive keys
   __device__ __forceinline__ static void store(Smem& sm, K* kout, uint32_t* vout, uint32_t lo, uint32_t len) {
     for (uint32_t i = threadIdx.x; i < len; i += BLOCK) {
-      kout[lo + i] = sm.sk[i];
-      if constexpr (PAIRS) vout[lo + i] = sm.sv[i];
+      kout[lo + i] = sm.sk[swz(i)];
+      if constexpr (PAIRS) vout[lo + i] = sm.sv[swzv(i)];
     }
   }
 
@@ -805,69 +826,37 @@ struct LocalSort {
   __device__ __forceinline__ static uint32_t mis(const T* at) {
     return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(at) / sizeof(T)) % V;
   }
-  // run[0, len) -> lds[a, a + len) with a = mis(run) by LDS-DMA (global_load_lds_dwordx4, no
-  // registers): wave w moves the 1-KB chunks w, w + W, ... (a wave-instruction writes 64 x 16 B
-  // from its wave-uniform LDS base, lds + a + head being 16-B aligned like run + head); the
-  // scalar head and tail by ordinary loads.  The caller waits (vmcnt(0)) and synchronises.
-  template <typename T, uint32_t V>
-  __device__ __forceinline__ static void copy_in_glds(T* lds, const T* run, uint32_t len) {
-    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-    const uint32_t a = mis<T, V>(run);
-    const uint32_t head = min(len, (V - a) % V);
-    const uint32_t nv = (len - head) / V;
-    if (t < head) lds[a + t] = run[t];
-    const T* src = run + head;
-    T* dst = lds + a + head;
-    for (uint32_t c = w; c * GRS_WAVE < nv; c += W) {
-      const uint32_t vi = c * GRS_WAVE + lane;
-      if (vi < nv)
-        __builtin_amdgcn_global_load_lds(src + vi * V, dst + c * GRS_WAVE * V, 16, 0, 0);
-    }
-    const uint32_t r = head + nv * V + t;
-    if (r < len) lds[a + r] = run[r];   // (the tail is < V < BLOCK elements)
-  }
-  // lds[a, a + len) -> run[0, len) with a = mis(run) (sort_rounds' shift)
-  template <typename T, uint32_t V>
+  // lds[a, a + len) -> run[0, len) with a = mis(run) (sort_rounds' shift).  ROT: the workgroup
+  // starts its vectors at a rotation of (blockIdx * 97 mod 256) x 256 B, so that the hundreds of
+  // workgroups storing at once are not all at the same offset of their runs: runs that start at
+  // multiples of 64 KB (the reference's 0..N-1 shuffled at 2^30: 16384-key segments) would
+  // otherwise send every workgroup's stores to the same HBM channels at the same time
+  template <typename T, uint32_t V, bool ROT = true>
   __device__ __forceinline__ static void copy_out(T* run, const T* lds, uint32_t len) {
     const uint32_t t = threadIdx.x, a = mis<T, V>(run);
     const uint32_t head = min(len, (V - a) % V);
     const uint32_t nv = (len - head) / V;
-    if (t < head) run[t] = lds[a + t];
+    if (t < head) run[t] = lds[swz_t<V>(a + t)];
     uint4* dst = reinterpret_cast<uint4*>(run + head);
-    const uint4* src = reinterpret_cast<const uint4*>(lds + a + head);
-    for (uint32_t c = t; c < nv; c += BLOCK) dst[c] = src[c];
-    const uint32_t r = head + nv * V + t;
-    if (r < len) run[r] = lds[a + r];
-  }
-  // the segment's keys (and payload) into registers, wave-striped as load() leaves them: 16-B
-  // LDS-DMA loads into sm.sk / sm.sv, then conflict-free 4-B LDS reads
-  __device__ __forceinline__ static void load_lds(Smem& sm, K (&k)[I], Vals& v, const K* kin, const uint32_t* vin,
-                                                  uint32_t len) {
-    copy_in_glds<K, KV>(sm.sk, kin, len);
-    if constexpr (PAIRS) copy_in_glds<uint32_t, VV>(sm.sv, vin, len);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const uint32_t ak = mis<K, KV>(kin), av = PAIRS ? mis<uint32_t, VV>(vin) : 0u;
-    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
-#pragma unroll
-    for (uint32_t j = 0; j < I; ++j) {
-      const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-      k[j] = i < len ? sm.sk[ak + i] : K(0);
-      if constexpr (PAIRS) v[j] = i < len ? sm.sv[av + i] : 0u;
+    const uint32_t rot = ROT && nv != 0u ? ((blockIdx.x * 97u & 255u) * 16u) % nv : 0u;
+    for (uint32_t c = t; c < nv; c += BLOCK) {
+      uint32_t r = c + rot;
+      if (r >= nv) r -= nv;
+      // the group's V elements: V-aligned in LDS, whole under the swizzle
+      dst[r] = *reinterpret_cast<const uint4*>(lds + swz_t<V>(a + head + r * V));
     }
-    __syncthreads();   // every read before the first round's counters and scatter
+    const uint32_t r = head + nv * V + t;
+    if (r < len) run[r] = lds[swz_t<V>(a + r)];
   }
-  // run() with 16-B HBM stores (and, GLDS, 16-B LDS-DMA loads): kin / vin and kout / vout are
-  // the segment's runs, at any alignment
-  template <bool GLDS>
+  // run() with 16-B HBM stores (the loads stay one element per lane, wave-striped: staging them
+  // through LDS with 16-B LDS-DMA loads measured slower, tools/lab8.py): kin / vin and kout /
+  // vout are the segment's runs, at any alignment
+  template <bool ROT = true>
   __device__ __forceinline__ static void run_vec(Smem& sm, const K* kin, const uint32_t* vin, K* kout,
                                                  uint32_t* vout, uint32_t len, int rounds) {
     K k[I];
     Vals v;
-    auto ld = [&]() {
-      if constexpr (GLDS) load_lds(sm, k, v, kin, vin, len);
-      else load(k, v, kin, vin, 0u, len);
-    };
+    auto ld = [&]() { load(k, v, kin, vin, 0u, len); };
     ld();
     const uint32_t ak = mis<K, KV>(kout), av = PAIRS ? mis<uint32_t, VV>(vout) : 0u;
     if (ROUNDS > 2 && rounds > 2) {
@@ -885,8 +874,8 @@ struct LocalSort {
     } else {
       sort_rounds(sm, k, v, len, rounds, ak, av);   // (ends with a barrier after its scatter)
     }
-    copy_out<K, KV>(kout, sm.sk, len);
-    if constexpr (PAIRS) copy_out<uint32_t, VV>(vout, sm.sv, len);
+    copy_out<K, KV, ROT>(kout, sm.sk, len);
+    if constexpr (PAIRS) copy_out<uint32_t, VV, ROT>(vout, sm.sv, len);
   }
   static constexpr uint32_t kRunMax = 48;
   // The sorted segment in LDS (sm.sk[ak + p]) is ordered by key >> hb and, inside each run of equal
@@ -898,29 +887,29 @@ struct LocalSort {
     __syncthreads();   // the last round's scatter
     if (threadIdx.x == 0) sm.slot = 0;
     __syncthreads();
-    K* const a = sm.sk + ak;
-    uint32_t* const b = sm.sv + av;
+    auto A = [&](uint32_t p) -> K& { return sm.sk[swz(ak + p)]; };
+    auto B = [&](uint32_t p) -> uint32_t& { return sm.sv[swzv(av + p)]; };
     for (uint32_t p = threadIdx.x; p < len; p += BLOCK) {
-      const K hi = a[p] >> hb;
-      if (p != 0 && (a[p - 1] >> hb) == hi) continue;   // not a run start
+      const K hi = A(p) >> hb;
+      if (p != 0 && (A(p - 1) >> hb) == hi) continue;   // not a run start
       uint32_t e = p + 1;
-      while (e < len && (a[e] >> hb) == hi && e - p <= kRunMax) ++e;
+      while (e < len && (A(e) >> hb) == hi && e - p <= kRunMax) ++e;
       if (e - p > kRunMax) {
         sm.slot = 1;
         continue;
       }
-      for (uint32_t q = p + 1; q < e; ++q) {   // insertion sort of a[p, e): stable
-        const K x = a[q];
+      for (uint32_t q = p + 1; q < e; ++q) {   // insertion sort of [p, e): stable
+        const K x = A(q);
         uint32_t y = 0;
-        if constexpr (PAIRS) y = b[q];
+        if constexpr (PAIRS) y = B(q);
         uint32_t r = q;
-        while (r > p && a[r - 1] > x) {
-          a[r] = a[r - 1];
-          if constexpr (PAIRS) b[r] = b[r - 1];
+        while (r > p && A(r - 1) > x) {
+          A(r) = A(r - 1);
+          if constexpr (PAIRS) B(r) = B(r - 1);
           --r;
         }
-        a[r] = x;
-        if constexpr (PAIRS) b[r] = y;
+        A(r) = x;
+        if constexpr (PAIRS) B(r) = y;
       }
     }
     __syncthreads();
@@ -996,8 +985,8 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
   // the bits below the segment's 16-bit prefix (bits above the top digit are equal in every key);
   // 16-B HBM loads and stores through LDS at the runs' own alignments
   const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
-  LS::template run_vec<false>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, len,
-                              rounds);
+  LS::template run_vec<>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, len,
+                         rounds);
 }
 
 // P3's second shape: the mid list's segments (persistent grid, a segment per workgroup in
@@ -1021,8 +1010,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict_
   const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
   for (uint32_t e = blockIdx.x; e < count; e += gridDim.x) {
     const uint32_t lo = mid[2 + 3 * e], o = mid[3 + 3 * e], len = mid[4 + 3 * e];
-    LS::template run_vec<false>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr,
-                                len, rounds);
+    LS::template run_vec<>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr,
+                           len, rounds);
     __syncthreads();   // every LDS read of this segment before the next one's
   }
 }

@@ -179,9 +179,12 @@ typedef enum grs_option {
                                 elements, grs_scratch_bytes), 1 / 2 allocate it (GRS_ENOMEM if it
                                 does not fit), -1 keeps it from 48M items of capacity; a change
                                 synchronises the device */
-  GRS_OPT_SEG_ROUTE = 12     /* grs_sort_segmented past the LDS-sized segments: 0 (default) by
+  GRS_OPT_SEG_ROUTE = 12,    /* grs_sort_segmented past the LDS-sized segments: 0 (default) by
                                 shape, 1 the segmented passes (top-byte scatter + LDS runs, or the
                                 segmented LSD), 2 one sort of composite (segment, key) keys */
+  GRS_OPT_H2_CHUNK = 13      /* the MSD sort's byte-2 histogram: 0 (default) by size, else the
+                                keys of P1's output per workgroup (a power of two, 4096..2^20;
+                                A/B runs) */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);

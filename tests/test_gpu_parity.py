@@ -444,6 +444,32 @@ def test_config_digests_full_size(gpu, name, radix_bits):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("kb,pairs,rb,n", [(32, True, 8, 16384 * 256 + 13), (64, False, 8, 16384 * 256 + 13),
+                                         (64, True, 8, 10240 * 256 + 13), (32, False, 8, 32768 * 256 + 13),
+                                         (64, True, 4, 10240 * 256 + 13), (32, True, 4, 16384 * 256 + 13)])
+def test_status_sizing_at_the_small_big_boundary(gpu, kb, pairs, rb, n):
+    """Sizes just past (smaller big tile) x CUs, where the sort still takes small tiles: the
+    look-back status was sized for fewer of them and the sort was refused (GRS_ECAPACITY) before
+    round 6.  Default options, a sorter of exactly n, the stable sort out."""
+    rng = np.random.default_rng(n + kb)
+    dt = np.uint32 if kb == 32 else np.uint64
+    keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+    keys[::7] = keys[3]
+    import gpuradixsort_amd as grs
+
+    s = grs.RadixSorter(n, key_bits=kb, pairs=pairs, radix_bits=rb)   # capacity exactly n
+    k = to_dev(keys, gpu)
+    v = to_dev(np.arange(n, dtype=np.uint32), gpu) if pairs else None
+    s.sort(k, v)
+    s.check_error()
+    perm = np.argsort(keys, kind="stable")
+    assert np.array_equal(k.cpu().numpy(), keys[perm])
+    if pairs:
+        assert np.array_equal(v.cpu().numpy(), perm.astype(np.uint32))
+    assert s.check_guards() == 0
+    s.close()
+
+
 def test_capacity_and_argument_errors(gpu):
     import gpuradixsort_amd as grs
 

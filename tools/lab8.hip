@@ -3,8 +3,10 @@
 // on segments of P3's real geometry: variable lengths, read from regions at any alignment,
 // written packed at any alignment (tools/lab8.py).
 //   MODE 0  dword striped loads, dword stores (LocalSort::run, round 5)
-//   MODE 1  dword striped loads, 16-B stores (LocalSort::run_vec<false>)
-//   MODE 2  16-B LDS-DMA loads (global_load_lds_dwordx4), 16-B stores (LocalSort::run_vec<true>)
+//   MODE 1  dword striped loads, 16-B stores rotated per workgroup (LocalSort::run_vec, shipped)
+//   MODE 3  as 1 without the rotation (run_vec<false>)
+// (MODE 2, 16-B LDS-DMA loads through LDS, measured in session r6s3 and removed: 2^30 2025 us
+// against 1829 for MODE 3; skeleton 1634 vs 1670)
 #include <hip/hip_runtime.h>
 
 #include "../gpuradixsort_amd/csrc/grs_msd.hpp"
@@ -23,11 +25,12 @@ __global__ __launch_bounds__(BLOCK) void lab_p3v(const uint32_t* __restrict__ in
   const uint32_t* kin = in + inoff[blockIdx.x];
   uint32_t* kout = out + outoff[blockIdx.x];
   if constexpr (MODE == 0) LS::run(sm, kin, nullptr, kout, nullptr, 0u, len, rounds);
-  else LS::template run_vec<MODE == 2>(sm, kin, nullptr, kout, nullptr, len, rounds);
+  else if constexpr (MODE == 3) LS::template run_vec<false>(sm, kin, nullptr, kout, nullptr, len, rounds);
+  else LS::template run_vec<>(sm, kin, nullptr, kout, nullptr, len, rounds);
 }
 
-// u64 keys (C5's P3): MODE 0 = LocalSort::run (6 rounds), 1 / 2 = run_vec<false / true> (2 rounds +
-// the runs finished by insertion)
+// u64 keys (C5's P3): MODE 0 = LocalSort::run (6 rounds), 1 = run_vec (2 rounds + the runs
+// finished by insertion, 16-B stores)
 template <int BLOCK, int I, int MODE>
 __global__ __launch_bounds__(BLOCK) void lab_p3w(const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
                                                  const uint32_t* __restrict__ inoff,
@@ -40,7 +43,7 @@ __global__ __launch_bounds__(BLOCK) void lab_p3w(const uint64_t* __restrict__ in
   const uint64_t* kin = in + inoff[blockIdx.x];
   uint64_t* kout = out + outoff[blockIdx.x];
   if constexpr (MODE == 0) LS::run(sm, kin, nullptr, kout, nullptr, 0u, len, rounds);
-  else LS::template run_vec<MODE == 2>(sm, kin, nullptr, kout, nullptr, len, rounds);
+  else LS::template run_vec<>(sm, kin, nullptr, kout, nullptr, len, rounds);
 }
 
 }  // namespace
@@ -49,14 +52,13 @@ extern "C" int lab8_p3w(int block, int items, int mode, int rounds, const uint64
                         const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens, uint32_t nseg,
                         void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (block == 256 && items == 20 && mode == 0)
-    hipLaunchKernelGGL((lab_p3w<256, 20, 0>), dim3(nseg), dim3(256), 0, s, in, out, inoff, outoff, lens, rounds);
-  else if (block == 256 && items == 20 && mode == 1)
-    hipLaunchKernelGGL((lab_p3w<256, 20, 1>), dim3(nseg), dim3(256), 0, s, in, out, inoff, outoff, lens, rounds);
-  else if (block == 256 && items == 20 && mode == 2)
-    hipLaunchKernelGGL((lab_p3w<256, 20, 2>), dim3(nseg), dim3(256), 0, s, in, out, inoff, outoff, lens, rounds);
+#define P3W(B, I, M)                                                                                          \
+  if (block == B && items == I && mode == M)                                                                  \
+    hipLaunchKernelGGL((lab_p3w<B, I, M>), dim3(nseg), dim3(B), 0, s, in, out, inoff, outoff, lens, rounds);   \
   else
+  P3W(256, 20, 0) P3W(256, 20, 1) P3W(512, 10, 0) P3W(512, 10, 1) P3W(1024, 5, 0) P3W(1024, 5, 1)
     return -1;
+#undef P3W
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -70,8 +72,8 @@ extern "C" int lab8_p3(int block, int items, int c16, int mode, int rounds, cons
                        rounds);                                                                           \
     return hipGetLastError() == hipSuccess ? 0 : -2;                                                      \
   }
-  P3(768, 24, 1, 0) P3(768, 24, 1, 1) P3(768, 24, 1, 2)
-  P3(256, 20, 0, 0) P3(256, 20, 0, 1) P3(256, 20, 0, 2)
+  P3(768, 24, 1, 0) P3(768, 24, 1, 1) P3(768, 24, 1, 3)
+  P3(256, 20, 0, 0) P3(256, 20, 0, 1) P3(256, 20, 0, 3)
 #undef P3
   return -1;
 }

@@ -17,14 +17,15 @@ import gpuradixsort_amd as grs  # noqa: E402
 
 L = ctypes.CDLL(os.path.join(HERE, "liblab8.so"))
 vp = ctypes.c_void_p
-NAMES = {0: "dword ld / dword st", 1: "dword ld / 16B st", 2: "16B glds ld / 16B st"}
+NAMES = {0: "dword ld / dword st", 1: "dword ld / 16B st rot", 3: "dword ld / 16B st"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 30)
     ap.add_argument("--shapes", default="768:24:1")
-    ap.add_argument("--modes", default="0,1,2")
+    ap.add_argument("--modes", default="0,1,3")
+    ap.add_argument("--u64-shapes", default="256:20,512:10,1024:5")
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--exact", action="store_true",
                     help="segments of exactly n / 65536 keys, no gaps (every run 16-B... 64-KB aligned, as the "
@@ -44,7 +45,7 @@ def main():
     diff = a.n - int(lens.sum())
     lens += diff // nseg
     lens[: abs(diff % nseg)] += 1 if diff % nseg > 0 else 0
-    assert int(lens.sum()) == a.n and int(lens.max()) <= m + sd + 1, (int(lens.sum()), int(lens.max()))
+    assert int(lens.sum()) == a.n and int(lens.max()) <= m + sd + 2, (int(lens.sum()), int(lens.max()))
     gaps = torch.randint(0, 257, (nseg,), generator=g)
     if a.exact:
         lens = torch.full((nseg,), m, dtype=torch.int64)
@@ -115,22 +116,27 @@ def run_u64(a, dev, nseg, m, sd, lens, inoff, outoff, total_in, n):
     stream = vp(torch.cuda.current_stream().cuda_stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     print(f"u64: n {n}, segments {nseg} of {m} +- {sd}", flush=True)
-    for mode in (0, 1, 2):
-        ts = []
-        for _ in range(a.reps):
-            e0.record()
-            rc = L.lab8_p3w(256, 20, mode, 6, vp(keys.data_ptr()), vp(out.data_ptr()), vp(d_in.data_ptr()),
-                            vp(d_out.data_ptr()), vp(d_len.data_ptr()), nseg, stream)
-            e1.record()
-            torch.cuda.synchronize()
-            assert rc == 0, rc
-            ts.append(e0.elapsed_time(e1))
-        ms = statistics.median(ts)
-        ok = bool(torch.equal(out[:n], want))
-        name = {0: "6 rounds, 8-B", 1: "8-B ld, 16-B st, 2 rounds + runs", 2: "16-B glds, 2 rounds + runs"}[mode]
-        print(f"p3 u64 256:20 mode {mode} ({name}): "
-              f"{ms * 1e3:8.1f} us {n * 16 / ms / 1e6:7.1f} GB/s ({n * 16 / ms / 1e6 / 8000:.3f} of 8 TB/s) "
-              f"sorted={ok}", flush=True)
+    for spec in a.u64_shapes.split(","):
+        b, it = (int(x) for x in spec.split(":"))
+        if b * it < m + sd:
+            continue
+        for mode in (0, 1):
+            for rounds in (0, 6):
+                ts = []
+                for _ in range(a.reps):
+                    e0.record()
+                    rc = L.lab8_p3w(b, it, mode, rounds, vp(keys.data_ptr()), vp(out.data_ptr()),
+                                    vp(d_in.data_ptr()), vp(d_out.data_ptr()), vp(d_len.data_ptr()), nseg, stream)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    assert rc == 0, rc
+                    ts.append(e0.elapsed_time(e1))
+                ms = statistics.median(ts)
+                ok = f" sorted={bool(torch.equal(out[:n], want))}" if rounds else ""
+                name = {0: "6 rounds, 8-B", 1: "8-B ld, 16-B st, 2 rounds + runs"}[mode]
+                print(f"p3 u64 {spec} mode {mode} ({name}) rounds={rounds}: "
+                      f"{ms * 1e3:8.1f} us {n * 16 / ms / 1e6:7.1f} GB/s ({n * 16 / ms / 1e6 / 8000:.3f} of 8 TB/s)"
+                      f"{ok}", flush=True)
 
 
 if __name__ == "__main__":
