@@ -67,6 +67,7 @@ OPTIONS = {
     "msd": (11, {"size": -1, "never": 0, "always": 1, "exact_p2": 2}),
     "seg_route": (12, {"shape": 0, "passes": 1, "composite": 2}),
     "h2_chunk": (13, {"size": 0}),
+    "h2_piece": (14, {"default": 0}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares
@@ -78,6 +79,7 @@ SIGNATURES = [
     ("grs_destroy", None, [c_void_p]),
     ("grs_scratch_bytes", c_size_t, [c_void_p]),
     ("grs_debug_check_guards", c_int, [c_void_p, POINTER(c_uint64)]),
+    ("grs_debug_msd_flags", c_int, [c_void_p, POINTER(c_uint32)]),
     ("grs_rank_mode", c_int, [c_void_p]),
     ("grs_lds_order_check", c_int, [c_int, c_int, c_int, POINTER(c_ulonglong)]),
     ("grs_set_option", c_int, [c_void_p, c_int, c_int]),

@@ -309,6 +309,7 @@ struct grs_sorter {
   int probe_rank_mode = 0;         // the device probe's ranking (GRS_OPT_RANK 0 restores it)
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
   uint32_t h2_chunk = 0;           // GRS_OPT_H2_CHUNK: 0 by size, else H2's chunk (keys per block)
+  uint32_t h2_piece = 0;           // GRS_OPT_H2_PIECE: 0 default, else H2's sample piece (keys)
   int seg_route = 0;               // GRS_OPT_SEG_ROUTE: 0 by shape, 1 segmented passes, 2 one
                                    // composite-key sort (grs_sort_segmented's longer segments)
   int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
@@ -329,6 +330,9 @@ struct grs_sorter {
     std::vector<size_t> bands;     // byte offsets of its guard bands
   };
   std::vector<ScratchBuf> bufs;
+  int last_msd_cb = -1;            // the control block of the last sort when it ran the MSD
+                                   // schedule, else -1 (grs_debug_msd_flags)
+  uint32_t* last_msd_spill2 = nullptr;
   size_t alt_inner_band = 0;       // u32 pairs: the band between alt's keys and payload, which
   bool alt_band_dirty = false;     // the LSD record passes write records across (restored by
                                    // the next MSD sort or guard check)
@@ -479,7 +483,12 @@ using MsdLocalS = MsdLocal<256, 8, false>;    // small sorts: the unrolled item 
 using MsdLocalM = MsdLocal<256, 12, false>;   // the shape holds, not what the segment holds
 using MsdLocalA = MsdLocal<256, 20, false>;   // any element (40 KB of LDS at 8 B)
 using MsdLocalB = MsdLocal<512, 20, false>;
+using MsdLocalW = MsdLocal<1024, 5, false>;   // u64 keys in A's place: 5120 keys, sixteen waves (the
+                                              // two rounds + run finish, 1.40 ms at 2^28 against 1.74
+                                              // for 256 x 20, tools/lab8.py round 6)
 using MsdLocalC = MsdLocal<768, 24, true>;    // 4-byte elements: two 72-KB workgroups per CU
+using MsdLocalD = MsdLocal<1024, 36, true>;   // 4-byte elements past 1.13G keys: one 152-KB workgroup
+                                              // per CU (the MSD sort to ~2.3G keys)
 constexpr uint32_t kMsdSmaxMin = MsdLocalS::SMAX;
 // fallback and redo passes (persistent): the big tile of the key type; 17408 keys is the
 // smallest of them (u32 pairs, u64 keys), which sizes the tables
@@ -737,6 +746,10 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       if (value != 0 && (value < 4096 || value > (1 << 20) || (value & (value - 1)) != 0)) return bad();
       s->h2_chunk = static_cast<uint32_t>(value);
       break;
+    case GRS_OPT_H2_PIECE:
+      if (value != 0 && (value < 64 || value > 4096 || (value & (value - 1)) != 0)) return bad();
+      s->h2_piece = static_cast<uint32_t>(value);
+      break;
 
     default:
       return set_err(GRS_EINVAL, "grs_set_option: unknown option");
@@ -779,6 +792,7 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_MSD: *value = s->msd_mode; break;
     case GRS_OPT_SEG_ROUTE: *value = s->seg_route; break;
     case GRS_OPT_H2_CHUNK: *value = static_cast<int>(s->h2_chunk); break;
+    case GRS_OPT_H2_PIECE: *value = static_cast<int>(s->h2_piece); break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -870,6 +884,27 @@ grs_status grs_debug_check_guards(grs_sorter* s, uint64_t* bad_words) {
   }
   if (r == GRS_OK) s->alt_band_dirty = false;
   *bad_words = bad;
+  (void)hipSetDevice(prev);
+  return r;
+}
+
+grs_status grs_debug_msd_flags(grs_sorter* s, uint32_t* flags) {
+  if (!s || !flags) return set_err(GRS_EINVAL, "grs_debug_msd_flags: NULL argument");
+  if (s->last_msd_cb < 0) return set_err(GRS_EINVAL, "grs_debug_msd_flags: the last sort did not run the MSD schedule");
+  int prev = 0;
+  GRS_HIP(hipGetDevice(&prev));
+  GRS_HIP(hipSetDevice(s->device));
+  grs_status r = GRS_OK;
+  const uint32_t* hist = s->last_msd_cb == 0 ? s->ctrl : s->ctrl2;
+  uint32_t w[3] = {};
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&w[0], hist + 512 + 256, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&w[1], s->last_msd_spill2, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&w[2], hist + GRS_MSD_SPAN + 4, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    r = set_err(GRS_EHIP, "grs_debug_msd_flags: read-back");
+  flags[0] = w[0] != 0u;
+  flags[1] = w[1] != 0u;
+  flags[2] = w[2];
   (void)hipSetDevice(prev);
   return r;
 }
@@ -1167,6 +1202,7 @@ int msd_local_shape(size_t n, size_t elem) {
   if (need <= MsdLocalA::SMAX) return 1;
   if (need <= MsdLocalB::SMAX) return 2;
   if (elem == 4 && need <= MsdLocalC::SMAX) return 3;
+  if (elem == 4 && need <= MsdLocalD::SMAX) return 6;
   return 0;
 }
 
@@ -1288,6 +1324,8 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
 #define GRS_DIAG_CHECK(w)
 #endif
   if ((r = mark()) != GRS_OK) return r;
+  s->last_msd_cb = s->cb_i;
+  s->last_msd_spill2 = mb + L.spill2;
   if (s->cb_dirty && s->cb_i == 0) GRS_HIP(hipMemsetAsync(hist, 0, GRS_CTRL_ERROR * 4, stream));
   s->cb_dirty = false;
   if (s->alt_band_dirty) {   // an LSD record sort wrote across alt's inner guard band: restore it
@@ -1348,14 +1386,16 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   K* const rk = static_cast<K*>(s->alt2_keys);
   uint32_t* const rv = PAIRS ? s->alt2_vals : nullptr;
   // H2 chunks: ~8 rounds of the resident blocks (2 per CU), 32K to 256K keys; the sample: one
-  // GRS_H2_PIECE-key piece in 2^k, k so that a uniform 16-bit bin still gets ~1000 sampled keys
+  // 2^GRS_H2_PIECE_LOG-key piece in 2^k, k so that a uniform 16-bit bin still gets ~1000 sampled keys
+  // (1/16 at 2^30: the regions' 6-sigma slack is then 19 %, inside the region buffer's 25 %)
   uint32_t chunk = GRS_H2_CHUNK;
   while (chunk > 32768u && static_cast<uint64_t>(n) / chunk < 16u * static_cast<uint64_t>(std::max(1, s->cus)))
     chunk >>= 1;
   uint32_t shift = 0;
-  while (shift < 3 && (static_cast<uint64_t>(n) >> (shift + 1)) >= 65536ull * 1024) ++shift;
+  while (shift < 4 && (static_cast<uint64_t>(n) >> (shift + 1)) >= 65536ull * 1024) ++shift;
   chunk = std::min<uint32_t>(chunk << shift, 1u << 20);   // sampled: about as many keys a block
   if (s->h2_chunk != 0) chunk = s->h2_chunk;             // (GRS_OPT_H2_CHUNK: A/B runs)
+  const uint32_t piece_log = s->h2_piece != 0 ? static_cast<uint32_t>(__builtin_ctz(s->h2_piece)) : GRS_H2_PIECE_LOG;
   // the region buffer's room (option msd = 2, a test hook: none, so the exact redo runs)
   const uint64_t cap2 = s->msd_mode == 2 ? 0 : static_cast<uint64_t>(msd_alt2_words(s->capacity));
   {
@@ -1368,7 +1408,7 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
     GRS_HIP(hipGetLastError());
     hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
                        shift ? mb + L.h2s : h2x, st[1], static_cast<uint32_t>(words2), tab, chunk, shift,
-                       (const uint32_t*)nullptr, top);
+                       (const uint32_t*)nullptr, top, piece_log);
     GRS_HIP(hipGetLastError());
     if (shift) {
       uint32_t* const room = mb + L.room;
@@ -1491,10 +1531,15 @@ grs_status run_sort_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipS
   switch (msd_local_shape(n, sizeof(K) + (PAIRS ? 4 : 0))) {
     case 4: return run_msd<K, PAIRS, MsdLocalS>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 5: return run_msd<K, PAIRS, MsdLocalM>(s, keys, vals, n, stream, src_in, vsrc_in);
-    case 1: return run_msd<K, PAIRS, MsdLocalA>(s, keys, vals, n, stream, src_in, vsrc_in);
+    case 1:
+      if constexpr (sizeof(K) == 8) return run_msd<K, PAIRS, MsdLocalW>(s, keys, vals, n, stream, src_in, vsrc_in);
+      return run_msd<K, PAIRS, MsdLocalA>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 2: return run_msd<K, PAIRS, MsdLocalB>(s, keys, vals, n, stream, src_in, vsrc_in);
     case 3:
       if constexpr (sizeof(K) == 4 && !PAIRS) return run_msd<K, PAIRS, MsdLocalC>(s, keys, vals, n, stream, src_in, vsrc_in);
+      [[fallthrough]];
+    case 6:
+      if constexpr (sizeof(K) == 4 && !PAIRS) return run_msd<K, PAIRS, MsdLocalD>(s, keys, vals, n, stream, src_in, vsrc_in);
       [[fallthrough]];
     default: return set_err(GRS_EINVAL, "internal: no MSD shape for this n");
   }
@@ -1689,6 +1734,7 @@ grs_status grs_sort_bits(grs_sorter* s, void* d_keys, uint32_t* d_vals, size_t n
   const uint32_t n32 = static_cast<uint32_t>(n);
   grs_status r = GRS_EINVAL;
   const bool u64 = s->key_type == GRS_KEY_U64;
+  s->last_msd_cb = -1;
   if (use_msd(s, n, begin_bit, end_bit)) {
     if (!u64 && !s->pairs)
       r = run_sort_msd<uint32_t, false>(s, (uint32_t*)d_keys, nullptr, n32, st);

@@ -42,7 +42,10 @@ enum SegSource : int { kSegSizes = 0, kSegList = 1, kSegOffsets = 2, kSegMoved =
 // LDS of the planner: 6 words per segment (tile, row and group prefixes, start, length,
 // histogram row); larger tables keep them in global scratch (`spill`, 6 * (nseg + 1) words).
 #define GRS_PLAN_LDS_SEGS 2048
-#define GRS_H2_PIECE 256   // keys of one piece of H2's sample (grs_msd_hist2)
+#define GRS_H2_PIECE_LOG 8   // keys of one piece of H2's sample, log2 (grs_msd_hist2)
+#ifndef GRS_P3_LDS_LAYOUT   // P3's LDS positions (LocalSort::swz_t): 0 plain, 1 XOR swizzle, 2 padded
+#define GRS_P3_LDS_LAYOUT 1
+#endif
 #define GRS_PLAN_LDS_WORDS (6 * GRS_PLAN_LDS_SEGS + 5 * 16)
 
 // Block exclusive scan of NV values per thread over BLOCK threads (wsum: NV * waves words of
@@ -444,7 +447,9 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
 // H2: h2[(top byte) * 256 + byte 2] over P1's output, one chunk of one bucket per block (grid
 // >= n / chunk + 256; tab from grs_msd_plan2 with the same chunk: 256K keys at 2^30, fewer
 // below so the grid is several resident rounds, not 2.5 with a tail); zeroes `zero_words` of
-// `zero` (P2's status).  Two 1024-thread blocks per CU (8 waves per SIMD).
+// `zero` (P2's status).  Two 1024-thread blocks per CU (8 waves per SIMD).  (P1 writing the
+// sample itself, the byte below its digit at one output position in 16 or in whole 1024-position
+// windows, cost P1 230 us at 2^30 for the 110 us it saved here: round 6)
 template <typename K>
 __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ keys,
                                                          uint32_t* __restrict__ h2,
@@ -453,7 +458,8 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
                                                          const uint32_t* __restrict__ tab, uint32_t chunk,
                                                          uint32_t sample_shift = 0,
                                                          const uint32_t* __restrict__ gate = nullptr,
-                                                         const uint32_t* __restrict__ top_shift = nullptr) {
+                                                         const uint32_t* __restrict__ top_shift = nullptr,
+                                                         uint32_t piece_log = 8) {
   constexpr uint32_t B = 1024;
   constexpr uint32_t LW = 256 * GRS_H2_COPIES;
   __shared__ __attribute__((aligned(16))) uint32_t h[LW];
@@ -481,6 +487,16 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   auto count = [&](K k) {
     atomicAdd(base + (static_cast<uint32_t>(k >> SH) & 255u) * GRS_H2_COPIES, 1u);
   };
+  auto flush = [&]() {
+    __syncthreads();
+    if (t < 256) {
+      const uint32_t* row = h + t * GRS_H2_COPIES;
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
+      if (c != 0) atomicAdd(&h2[s * 256 + t], c);
+    }
+  };
   constexpr uint32_t VEC = 16 / sizeof(K);
   const K* kc = keys + c0;
   // 16-B loads from the first aligned key on
@@ -494,13 +510,14 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
     for (uint32_t q = 0; q < VEC; ++q) count(e[q]);
   };
   if (sample_shift != 0) {
-    // a sample: the first of every 2^sample_shift GRS_H2_PIECE-key pieces (whatever the input
-    // order, the pieces cover the chunk evenly); the bucket's scale is its length over its
+    // a sample: the first of every 2^sample_shift pieces of 2^piece_log keys (whatever the
+    // input order, the pieces cover the chunk evenly); the bucket's scale is its length over its
     // sampled keys
-    constexpr uint32_t PU = GRS_H2_PIECE / VEC;   // 16-B loads per piece
-    const uint32_t np = (nv + PU - 1) / PU;
-    const uint32_t ns = ((np + (1u << sample_shift) - 1) >> sample_shift) * PU;
-    auto at = [&](uint32_t m) { return ((m / PU) << sample_shift) * PU + m % PU; };
+    constexpr uint32_t VL = VEC == 4 ? 2 : 1;
+    const uint32_t pul = piece_log - VL, PU = 1u << pul;   // 16-B loads per piece
+    const uint32_t np = (nv + PU - 1) >> pul;
+    const uint32_t ns = ((np + (1u << sample_shift) - 1) >> sample_shift) << pul;
+    auto at = [&](uint32_t m) { return ((m >> pul) << (sample_shift + pul)) + (m & (PU - 1u)); };
     uint32_t m = t;
     for (; m + 3 * B < ns; m += 4 * B) {   // four loads in flight (one at a time: latency-bound)
       uint4 x[4];
@@ -519,14 +536,7 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
       const uint32_t v = at(m);
       if (v < nv) count4(kv[v]);
     }
-    __syncthreads();
-    if (t < 256) {
-      const uint32_t* row = h + t * GRS_H2_COPIES;
-      uint32_t c = 0;
-#pragma unroll
-      for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
-      if (c != 0) atomicAdd(&h2[s * 256 + t], c);
-    }
+    flush();
     return;
   }
   if (t < head) count(kc[t]);
@@ -540,14 +550,7 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   }
   for (; i < nv; i += B) count4(kv[i]);
   for (uint32_t r = head + nv * VEC + t; r < cl; r += B) count(kc[r]);
-  __syncthreads();
-  if (t < 256) {
-    const uint32_t* row = h + t * GRS_H2_COPIES;
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < GRS_H2_COPIES; ++k) c += row[(k + t) & (GRS_H2_COPIES - 1)];
-    if (c != 0) atomicAdd(&h2[s * 256 + t], c);
-  }
+  flush();
 }
 
 // The regions of P2 (one block of 256 per top-byte bucket s, a thread per byte-2 bin b), from
@@ -699,14 +702,36 @@ struct LocalSort {
   // 16-B groups stay whole, so copy_out's vector reads stand.
   template <uint32_t V>   // V elements per 16-B group
   __device__ __forceinline__ static uint32_t swz_t(uint32_t x) {
+#if GRS_P3_LDS_LAYOUT == 0
+    return x;
+#elif GRS_P3_LDS_LAYOUT == 2
+    return x + ((x >> 8) * V);   // one 16-B group of padding every 256 elements
+#else
     return x ^ (((x >> 8) & 15u) << (V == 4 ? 2 : V == 2 ? 1 : 0));
+#endif
   }
   __device__ __forceinline__ static uint32_t swz(uint32_t x) { return swz_t<KV>(x); }
   __device__ __forceinline__ static uint32_t swzv(uint32_t x) { return swz_t<VV>(x); }
-  static constexpr uint32_t SK = (SMAX + KV + 63) / 64 * 64;   // swz stays inside a 64-group
+  // swz_t(base + lane) for a wave-uniform base that is a multiple of 64 (lane < 64): the part
+  // that depends on the base is scalar, one VALU op per access is left
+  template <uint32_t V>
+  __device__ __forceinline__ static uint32_t swz_row(uint32_t base, uint32_t lane) {
+#if GRS_P3_LDS_LAYOUT == 0
+    return base + lane;
+#elif GRS_P3_LDS_LAYOUT == 2
+    return base + (base >> 8) * V + lane;
+#else
+    return base + (lane ^ (((base >> 8) & 15u) << (V == 4 ? 2 : V == 2 ? 1 : 0)));
+#endif
+  }
+  template <uint32_t V>
+  static constexpr uint32_t lds_len(uint32_t n) {   // (xor: stays inside a 64-group)
+    return GRS_P3_LDS_LAYOUT == 2 ? (n + (n >> 8) * V + 63) / 64 * 64 : (n + 63) / 64 * 64;
+  }
+  static constexpr uint32_t SK = lds_len<KV>(SMAX + KV);
   struct Smem {
     alignas(16) K sk[SK];
-    alignas(16) uint32_t sv[PAIRS ? (SMAX + VV + 63) / 64 * 64 : 4];
+    alignas(16) uint32_t sv[PAIRS ? lds_len<VV>(SMAX + VV) : 4];
     uint32_t cnt[W * 256 / (C16 ? 2 : 1)];
     uint32_t wtot[4];
     uint32_t slot;
@@ -801,12 +826,13 @@ struct LocalSort {
       }
       __syncthreads();
       if (pass + 1 < rounds) {
+        const uint32_t ws = __builtin_amdgcn_readfirstlane(w);
 #pragma unroll
         for (uint32_t j = 0; j < I; ++j) {
-          const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
-          if (i < len) {
-            k[j] = sm.sk[swz(i)];
-            if constexpr (PAIRS) v[j] = sm.sv[swzv(i)];
+          const uint32_t base = ws * GRS_WAVE * I + j * GRS_WAVE;
+          if (base + lane < len) {
+            k[j] = sm.sk[swz_row<KV>(base, lane)];
+            if constexpr (PAIRS) v[j] = sm.sv[swz_row<VV>(base, lane)];
           }
         }
       }

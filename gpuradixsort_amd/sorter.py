@@ -89,6 +89,14 @@ class RadixSorter:
         check(lib().grs_debug_check_guards(self._h, ctypes.byref(bad)), "grs_debug_check_guards")
         return int(bad.value)
 
+    def msd_flags(self) -> dict:
+        """What the last sort did in the MSD schedule (grs_debug_msd_flags; synchronises):
+        p1_redo (P1 ran twice), p2_exact (P2 took the exact path), top_shift (the top digit's
+        shift).  GrsError when the last sort took the LSD passes."""
+        f = (ctypes.c_uint32 * 3)()
+        check(lib().grs_debug_msd_flags(self._h, f), "grs_debug_msd_flags")
+        return {"p1_redo": bool(f[0]), "p2_exact": bool(f[1]), "top_shift": int(f[2])}
+
     @property
     def rank_mode(self) -> str:
         """'atomic' (lane-ordered LDS atomics, the default) or 'match' (ballot fallback)."""

@@ -115,6 +115,13 @@ size_t grs_scratch_bytes(const grs_sorter* s);
  * past 2^20 items (PrefixScanBuffer.comp:36). */
 grs_status grs_debug_check_guards(grs_sorter* s, uint64_t* bad_words);
 
+/* TEST HOOK: what the last grs_sort of this sorter did in the MSD schedule (GRS_EINVAL when it
+ * took the LSD passes): flags[0] = 1 when P1 ran twice (a run outgrew its sampled region, or the
+ * keys' span put the top digit above the sample's guess), flags[1] = 1 when P2 took the exact
+ * path (a sampled region overflowed, or a sort too small to sample), flags[2] = the top digit's
+ * shift.  Synchronises the device.  New with respect to the reference. */
+grs_status grs_debug_msd_flags(grs_sorter* s, uint32_t flags[3]);
+
 /* Ranking used by this sorter's passes: 0 = lane-ordered LDS atomics (the default; probed on
  * the device at grs_create), 1 = wave64 ballot-match fallback (probe failed, or
  * grs_set_option(GRS_OPT_RANK, 1)).  -1 for a NULL sorter. */
@@ -182,9 +189,11 @@ typedef enum grs_option {
   GRS_OPT_SEG_ROUTE = 12,    /* grs_sort_segmented past the LDS-sized segments: 0 (default) by
                                 shape, 1 the segmented passes (top-byte scatter + LDS runs, or the
                                 segmented LSD), 2 one sort of composite (segment, key) keys */
-  GRS_OPT_H2_CHUNK = 13      /* the MSD sort's byte-2 histogram: 0 (default) by size, else the
+  GRS_OPT_H2_CHUNK = 13,     /* the MSD sort's byte-2 histogram: 0 (default) by size, else the
                                 keys of P1's output per workgroup (a power of two, 4096..2^20;
                                 A/B runs) */
+  GRS_OPT_H2_PIECE = 14      /* the same histogram's sample: 0 (default) pieces of 256 keys, else
+                                the keys of a piece (a power of two, 64..4096; A/B runs) */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);

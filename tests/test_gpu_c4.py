@@ -158,6 +158,34 @@ def test_max_n_one_call(gpu):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("n,dist", [(1_500_000_000, "perm"), ((1 << 31) + 12345, "uniform")])
+def test_msd_past_c4(gpu, n, dist):
+    """u32 keys past 1.13G (16-bit segments of 23K-33K keys: P3's 36K-key shape): still the MSD
+    schedule (grs_debug_msd_flags answers, no redo, no exact P2), sorted and the same multiset;
+    the reference's shuffled 0..n-1 (1.5G: 32768-key segments) sorts to exactly 0..n-1."""
+    import gpuradixsort_amd as grs
+
+    k = torch.empty(n, dtype=torch.uint32, device=gpu)
+    if dist == "perm":
+        grs.fill_permutation(k, 0x5EED)
+    else:
+        grs.fill_splitmix(k, 0x6A09E667F3BCC908 + 5)
+    before = _checksums(k)
+    s = grs.RadixSorter(n, key_bits=32)
+    s.sort(k)
+    s.check_error()
+    f = s.msd_flags()
+    assert not f["p1_redo"] and not f["p2_exact"], f
+    assert s.check_guards() == 0
+    s.close()
+    assert grs.count_inversions(k) == 0
+    assert _checksums(k) == before
+    if dist == "perm":
+        assert int(k[:1].view(torch.int32).item()) == 0 and int(k[-1:].view(torch.int32).item()) == n - 1
+    del k
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("kb", [32, 64])
 def test_max_n_pairs_one_call(gpu, kb):
     """GRS_MAX_N (key, index) pairs in one call, u32 and u64 keys: keys sorted and

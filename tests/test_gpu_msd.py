@@ -69,7 +69,7 @@ def dists(n, rng):
     yield "narrow_29bit", rng.integers(0, 1 << 29, n, dtype=np.uint32)
 
 
-PIECE = 256   # keys of one piece of H2's sample (GRS_H2_PIECE, grs_msd.hpp)
+PIECE = 256   # keys of one piece of H2's sample (2^GRS_H2_PIECE_LOG, grs_msd.hpp)
 
 SIZES = [1, 2, 3, 64, 1000, 4097, 5121, 36865, 65537, 300007, 1 << 20]
 
@@ -282,7 +282,7 @@ def test_msd_sampled_p2(gpu, n):
 
 def test_msd_p2_region_spill(gpu):
     """A sample that misses a bin: every key in top-byte bucket 0 and, by 256-key piece of P1's
-    output (GRS_H2_PIECE), byte 2 = 0 in the sampled pieces (even ones: one in two is sampled at 2^27) and 255
+    output (2^GRS_H2_PIECE_LOG), byte 2 = 0 in the sampled pieces (even ones: one in two is sampled at 2^27) and 255
     in the others, so bin (0, 255) outgrows its region: P2's last tiles flag it, the exact
     histogram and pass run (gated on the flag) and P3 sorts in place -- bit-exact, and the
     sorter's next sort is too."""

@@ -146,6 +146,10 @@ def test_reference_distribution_full_size(gpu, n, pairs):
     s = grs.RadixSorter(n, key_bits=32, pairs=pairs)
     s.sort(k, v)
     s.check_error()
+    # no sampled region overflowed, and the guess found the span -- except when n is just above a
+    # power of two: the 77 keys with the top bit are not among the guess's 4096, so P1 runs twice
+    rare_top = n & (n - 1) != 0 and (n - (1 << (n.bit_length() - 1))) < n // 1000
+    assert s.msd_flags() == {"p1_redo": rare_top, "p2_exact": False, "top_shift": (n - 1).bit_length() - 8}
     assert s.check_guards() == 0
     s.close()
     ar = torch.arange(n, dtype=torch.int64, device=gpu)
@@ -238,3 +242,49 @@ def test_lsd_plan_c2_reference_input(gpu):
     assert torch.equal(k.view(torch.int32).to(torch.int64), torch.arange(n, device=gpu))
     assert ms["perm"] < ms["uniform"], ms
     s.close()
+
+
+@pytest.mark.parametrize("case", ["uniform", "span_redo", "spill_redo"])
+@pytest.mark.parametrize("pairs", [False, True])
+def test_h2_sample_paths(gpu, case, pairs):
+    """Sorts large enough to sample H2 (2^27 + 3 keys): uniform keys (no redo, no exact P2), and
+    H2's piece sample over a redone P1's exact layout -- a varying top bit the span guess
+    misses, or a run past its sampled region (every key of one top digit sits where the sample
+    does not look).  Keys and the stable permutation == torch's stable sort."""
+    import gpuradixsort_amd as grs
+
+    n = (1 << 27) + 3
+    g = torch.Generator(device=gpu).manual_seed(27 + pairs)
+    if case == "uniform":
+        k64 = torch.randint(0, 1 << 32, (n,), generator=g, device=gpu, dtype=torch.int64)
+    elif case == "span_redo":
+        k64 = torch.randint(0, 1 << 20, (n,), generator=g, device=gpu, dtype=torch.int64)
+        seen = np.zeros(n, bool)
+        seen[_guess_positions(n)] = True
+        hot = np.random.default_rng(5).choice(np.flatnonzero(~seen), 9, replace=False)
+        k64[torch.from_numpy(hot).to(gpu)] |= 1 << 31
+    else:
+        # top byte 0x00 everywhere except one contiguous block of top byte 0xFF between the
+        # sample's evenly spaced chunks (sampled share ~0, so its region is the pad alone)
+        k64 = torch.randint(0, 1 << 24, (n,), generator=g, device=gpu, dtype=torch.int64)
+        k64[100:100 + 8000] |= 0xFF << 24   # (between the sample's chunks at 0 and 8192)
+        k64[n - 1] |= 1 << 31
+    k = k64.to(torch.int32).view(torch.uint32)
+    v = None
+    if pairs:
+        v = torch.empty(n, dtype=torch.uint32, device=gpu)
+        grs.iota_u32(v)
+    s = grs.RadixSorter(n, key_bits=32, pairs=pairs)
+    s.sort(k, v)
+    s.check_error()
+    f = s.msd_flags()
+    assert f["p1_redo"] == (case != "uniform"), f
+    assert not f["p2_exact"], f
+    assert s.check_guards() == 0
+    s.close()
+    want, perm = torch.sort(k64, stable=True)
+    assert torch.equal(k.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, want)
+    if pairs:
+        assert torch.equal(v.view(torch.int32).to(torch.int64) & 0xFFFFFFFF, perm)
+    del k, v, k64, want, perm
+    torch.cuda.empty_cache()

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 import gpuradixsort_amd as grs  # noqa: E402
 
-L = ctypes.CDLL(os.path.join(HERE, "liblab8.so"))
+L = None   # the lab library (--lib)
 vp = ctypes.c_void_p
 NAMES = {0: "dword ld / dword st", 1: "dword ld / 16B st rot", 3: "dword ld / 16B st"}
 
@@ -34,7 +34,10 @@ def main():
                     help="the low bits of every segment a permutation of 0..m-1 (the reference's input)")
     ap.add_argument("--u64", action="store_true", help="u64 keys (C5), shape 256:20, modes 0 (6 rounds) / "
                                                        "1 (16-B, 2 rounds + run finish)")
+    ap.add_argument("--lib", default="liblab8.so", help="liblab8_lds0/2.so: P3's LDS layout 0 / 2 (Makefile)")
     a = ap.parse_args()
+    global L
+    L = ctypes.CDLL(os.path.join(HERE, a.lib))
     dev = torch.device("cuda", 0)
     nseg = 65536
     g = torch.Generator(device="cpu").manual_seed(8)
