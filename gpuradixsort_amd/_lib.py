@@ -61,13 +61,15 @@ OPTIONS = {
     "rank": (5, {"probe": 0, "match": 1}),
     "sharded_path": (6, {"auto": 0, "general": 1}),
     "sharded_send": (7, {"regions": 0, "contig": 1, "shrunk": 2}),
-    "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2}),
+    "exchange": (8, {"auto": 0, "partition": 1, "presorted": 2, "chunked": 3}),
     "merge": (9, {"rounds": 0, "kway": 1}),
     "fault_tile": (10, {"off": -1}),   # test hook: tile v of every pass never publishes
     "msd": (11, {"size": -1, "never": 0, "always": 1, "exact_p2": 2}),
     "seg_route": (12, {"shape": 0, "passes": 1, "composite": 2}),
     "h2_chunk": (13, {"size": 0}),
     "h2_piece": (14, {"default": 0}),
+    "p3": (15, {"per_segment": 0, "persistent": 1}),
+    "x_chunks": (16, {"default": 0}),
 }
 
 # (name, restype, argtypes) of every symbol include/grs.h declares
@@ -111,6 +113,8 @@ SIGNATURES = [
                                     POINTER(c_uint64)]),
     ("grs_shard_bounds_host", c_int, [c_void_p, c_size_t, c_int, c_void_p, c_void_p, c_int,
                                       POINTER(c_uint64)]),
+    ("grs_shard_chunk_plan_host", c_int, [c_void_p, c_int, c_int, c_int, c_uint64, POINTER(c_uint64),
+                                          POINTER(c_uint64), POINTER(c_uint64)]),
     ("grs_shard_samples_per_rank", c_int, [c_int]),
     ("grs_shard_sample", c_int, [c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("grs_shard_encode_words_max", c_size_t, [c_size_t, c_int]),

@@ -290,7 +290,14 @@ struct grs_sorter {
   void* codec_buf = nullptr;       // presorted exchange: plan, block sizes / offsets, scan, co-ranks
   size_t codec_bytes = 0;
   // options (grs_set_option; defaults pick by size; nothing is read from the environment)
-  int sharded_exchange = 0;        // GRS_OPT_EXCHANGE: 0 auto, 1 partition-first, 2 presorted
+  int sharded_exchange = 0;        // GRS_OPT_EXCHANGE: 0 auto, 1 partition-first, 2 presorted,
+                                   // 3 chunked partition-first (keys only)
+  int x_chunks = 0;                // GRS_OPT_X_CHUNKS: chunks of the chunked exchange (0: 4)
+  // the chunked exchange's second stream (RCCL calls) and events, created on first use
+  hipStream_t xstream = nullptr;
+  hipEvent_t xcev[17] = {};        // [c]: chunk c partitioned; [16]: the exchange done
+  hipEvent_t xhev = nullptr;       // a chunk's count rows landed on the host
+  uint32_t* xchunk_host = nullptr; // pinned: one chunk's count rows (G rows of G + 3 words)
   int merge_mode = 0;              // GRS_OPT_MERGE: 0 ceil(log2 k) 2-way rounds, 1 one k-way pass
   // last grs_sort_sharded call, with profiling on: events at call start / exchange start /
   // exchange end / call end, and the bytes that crossed the links (self part excluded)
@@ -310,6 +317,8 @@ struct grs_sorter {
   int fault_tile = -1;             // GRS_OPT_FAULT_TILE (test hook; ctrl debug words)
   uint32_t h2_chunk = 0;           // GRS_OPT_H2_CHUNK: 0 by size, else H2's chunk (keys per block)
   uint32_t h2_piece = 0;           // GRS_OPT_H2_PIECE: 0 default, else H2's sample piece (keys)
+  int p3_mode = 0;                 // GRS_OPT_P3: 0 a workgroup per segment, 1 persistent with
+                                   // prefetch (u32 keys / pairs; measured slower, round 6)
   int seg_route = 0;               // GRS_OPT_SEG_ROUTE: 0 by shape, 1 segmented passes, 2 one
                                    // composite-key sort (grs_sort_segmented's longer segments)
   int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
@@ -436,6 +445,11 @@ void grs_destroy(grs_sorter* s) {
     if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
   for (hipEvent_t e : s->xev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : s->xcev)
+    if (e) (void)hipEventDestroy(e);
+  if (s->xhev) (void)hipEventDestroy(s->xhev);
+  if (s->xstream) (void)hipStreamDestroy(s->xstream);
+  if (s->xchunk_host) (void)hipHostFree(s->xchunk_host);
   delete[] s->ev;
   delete[] s->info;
   (void)hipSetDevice(prev);
@@ -713,8 +727,12 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       s->sharded_send = value;
       break;
     case GRS_OPT_EXCHANGE:
-      if (value < 0 || value > 2) return bad();
+      if (value < 0 || value > 3) return bad();
       s->sharded_exchange = value;
+      break;
+    case GRS_OPT_X_CHUNKS:
+      if (value < 0 || value > 16) return bad();
+      s->x_chunks = value;
       break;
     case GRS_OPT_FAULT_TILE: {
       if (value < -1) return bad();
@@ -749,6 +767,10 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
     case GRS_OPT_H2_PIECE:
       if (value != 0 && (value < 64 || value > 4096 || (value & (value - 1)) != 0)) return bad();
       s->h2_piece = static_cast<uint32_t>(value);
+      break;
+    case GRS_OPT_P3:
+      if (value < 0 || value > 1) return bad();
+      s->p3_mode = value;
       break;
 
     default:
@@ -787,12 +809,14 @@ grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value) {
     case GRS_OPT_SHARDED_PATH: *value = s->sharded_general ? 1 : 0; break;
     case GRS_OPT_SHARDED_SEND: *value = s->sharded_send; break;
     case GRS_OPT_EXCHANGE: *value = s->sharded_exchange; break;
+    case GRS_OPT_X_CHUNKS: *value = s->x_chunks; break;
     case GRS_OPT_MERGE: *value = s->merge_mode; break;
     case GRS_OPT_FAULT_TILE: *value = s->fault_tile; break;
     case GRS_OPT_MSD: *value = s->msd_mode; break;
     case GRS_OPT_SEG_ROUTE: *value = s->seg_route; break;
     case GRS_OPT_H2_CHUNK: *value = static_cast<int>(s->h2_chunk); break;
     case GRS_OPT_H2_PIECE: *value = static_cast<int>(s->h2_piece); break;
+    case GRS_OPT_P3: *value = s->p3_mode; break;
     default: return set_err(GRS_EINVAL, "grs_get_option: unknown option");
   }
   return GRS_OK;
@@ -1477,9 +1501,33 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   // first: grs_msd_copy_big)
   using P3L = std::conditional_t<sizeof(K) == 4 && !PAIRS, MsdLocalC, MsdLocalB>;
   const uint32_t mid_max = P3L::SMAX > P3C::SMAX ? P3L::SMAX : P3C::SMAX;
-  hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
-                     dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
-                     mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows, top);
+  if constexpr (sizeof(K) == 4) {
+    if (s->p3_mode == 1) {
+      // persistent, the next segment's loads behind this one's stores (grs_msd_local_pf; the
+      // ticket: big[16], zeroed by the sample kernel).  Measured slower than a workgroup per
+      // segment (C4 P3 2.12 vs 1.97 ms, ns 0.80 vs 0.45: the ticket and the segment's table
+      // reads are a serial latency per segment that the dispatcher's fresh workgroups do not
+      // pay): an A/B option
+      using LS = grs::LocalSort<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16>;
+      constexpr int lds_per_cu = 160 * 1024 / static_cast<int>(sizeof(typename LS::Smem) + 16);
+      // (u32 keys on 512 x 20: three workgroups' 80 registers spill the loop; two)
+      constexpr int per_cu = std::min(std::min(lds_per_cu, 2048 / P3C::BLOCK), P3C::BLOCK == 512 && !PAIRS ? 2 : 8);
+      constexpr int minw = std::max(1, per_cu * P3C::BLOCK / GRS_WAVE / 4);
+      hipLaunchKernelGGL((grs::grs_msd_local_pf<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE, minw>),
+                         dim3(per_cu * std::max(1, s->cus)), dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2,
+                         mb + L.len2, mb + L.in2, mb + L.out2, mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart,
+                         mb + L.blen, mb + L.brow, rows, top, bigc + 16);
+    } else {
+      hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
+                         dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2,
+                         mb + L.out2, mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow,
+                         rows, top);
+    }
+  } else {
+    hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
+                       dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
+                       mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows, top);
+  }
   GRS_HIP(hipGetLastError());
   if (P3L::SMAX > P3C::SMAX) {
     constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
@@ -3036,10 +3084,150 @@ grs_status run_sharded_presorted(grs_sorter* s, const uint32_t* keys, uint32_t n
   return GRS_OK;
 }
 
+// grs_sort_sharded, chunked partition-first exchange (GRS_OPT_EXCHANGE = 3; keys without
+// payload: the received runs are laid out chunk-major, so equal keys from different sources
+// interleave, which only a payload could tell).  The partition of chunk c + 1 runs on the
+// caller's stream while chunk c crosses the links from a second stream that carries every RCCL
+// call of the exchange:
+//   stream st:  samples, all-gather, splitters, chunk digits | partition chunk 0, 1, ..., C-1
+//   stream X:   per chunk c: wait for partition c; all-gather its count rows (+ verdict);
+//               copy them to the host; [host: the chunk's plan]; grouped send / recv of chunk c
+//   then st waits for X and sorts the received run.
+// A timeout or a receive side too small on any rank stops every rank at the same chunk (each
+// reads every rank's rows of every chunk), before that chunk moves.  C (GRS_OPT_X_CHUNKS) must
+// be the same on every rank.
+template <typename K, int N>
+grs_status run_sharded_chunked(grs_sorter* s, const K* keys, uint32_t n, K* out_k, size_t out_cap,
+                               size_t* n_out, ncclComm_t comm, int g, int me, hipStream_t st) {
+  using Dig = grs::SplitterIdxDigit<K, N>;
+  const int C = s->x_chunks > 0 ? s->x_chunks : 4;
+  const uint32_t S = static_cast<uint32_t>(grs_shard_samples_per_rank(g));
+  const uint32_t chunk = (n + static_cast<uint32_t>(C) - 1) / static_cast<uint32_t>(C);
+  const int W = g + 3;   // words per rank in a chunk's count all-gather: counts + verdict
+  auto al = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+  const size_t gs = static_cast<size_t>(g) * S;
+  // scratch: sk[S] | sp[S] | ak[G*S] | ap[G*S] | rows[C][W] | mats[C][G*W] | dig | digs[C]
+  const size_t need = al(S * sizeof(K)) + al(S * 4) + al(gs * sizeof(K)) + al(gs * 4) +
+                      al(static_cast<size_t>(C) * W * 4) + al(static_cast<size_t>(C) * g * W * 4) + al(sizeof(Dig)) +
+                      al(static_cast<size_t>(C) * sizeof(Dig));
+  grs_status r = grow_buf(s, &s->shard_buf, &s->shard_bytes, need, "grs_sort_sharded: scratch");
+  if (r != GRS_OK) return r;
+  if (!s->xstream) GRS_HIP(hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking));
+  for (int c = 0; c <= 16; ++c)
+    if (!s->xcev[c]) GRS_HIP(hipEventCreateWithFlags(&s->xcev[c], hipEventDisableTiming));
+  if (!s->xhev) GRS_HIP(hipEventCreateWithFlags(&s->xhev, hipEventDisableTiming));
+  if (!s->xchunk_host && hipHostMalloc(reinterpret_cast<void**>(&s->xchunk_host), 16 * 19 * 4,
+                                       hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(GRS_ENOMEM, "grs_sort_sharded: pinned allocation failed");
+  }
+  char* b = static_cast<char*>(s->shard_buf);
+  K* sk = reinterpret_cast<K*>(b);                  b += al(S * sizeof(K));
+  uint32_t* sp = reinterpret_cast<uint32_t*>(b);     b += al(S * 4);
+  K* ak = reinterpret_cast<K*>(b);                   b += al(gs * sizeof(K));
+  uint32_t* ap = reinterpret_cast<uint32_t*>(b);     b += al(gs * 4);
+  uint32_t* rows = reinterpret_cast<uint32_t*>(b);   b += al(static_cast<size_t>(C) * W * 4);
+  uint32_t* mats = reinterpret_cast<uint32_t*>(b);   b += al(static_cast<size_t>(C) * g * W * 4);
+  Dig* dig = reinterpret_cast<Dig*>(b);              b += al(sizeof(Dig));
+  Dig* digs = reinterpret_cast<Dig*>(b);
+  hipStream_t X = s->xstream;
+  K* send = static_cast<K*>(s->alt_keys);   // chunk c's buckets, contiguous from c * chunk
+  const size_t cap = std::min<size_t>(out_cap, s->capacity);
+
+  if (xmark(s, 0, st) != GRS_OK) return GRS_EHIP;
+  // 1-3. samples, all-gathered; splitters; the chunks' digits
+  hipLaunchKernelGGL((grs::grs_shard_samples<K>), dim3((S + 255) / 256), dim3(256), 0, st, keys, n, S, sk, sp);
+  GRS_HIP(hipGetLastError());
+  GRS_RCCL(ncclGroupStart());
+  GRS_RCCL(ncclAllGather(sk, ak, S, nccl_type<K>(), comm, st));
+  GRS_RCCL(ncclAllGather(sp, ap, S, ncclUint32, comm, st));
+  GRS_RCCL(ncclGroupEnd());
+  hipLaunchKernelGGL((grs::grs_shard_splitters<K, N>), dim3(1), dim3(1024), 0, st, ak, ap,
+                     static_cast<uint32_t>(g), S, static_cast<uint32_t>(me), dig);
+  GRS_HIP(hipGetLastError());
+  hipLaunchKernelGGL((grs::grs_shard_chunk_digits<K, N>), dim3((C * GRS_MAX_SPLITTERS + 255) / 256), dim3(256), 0,
+                     st, dig, static_cast<uint32_t>(C), chunk, digs);
+  GRS_HIP(hipGetLastError());
+  // 4. every chunk's partition on st, each followed by its verdict words and an event
+  for (int c = 0; c < C; ++c) {
+    const uint32_t c0 = std::min<uint32_t>(n, static_cast<uint32_t>(c) * chunk);
+    const uint32_t cn = std::min<uint32_t>(n - c0, chunk);
+    uint32_t* row = rows + static_cast<size_t>(c) * W;
+    if (cn > 0) {
+      r = run_partition_n<K, false, N>(s, keys + c0, nullptr, send + c0, nullptr, cn, Dig{}, digs + c, g - 1, row,
+                                       st, 0u);
+      if (r != GRS_OK) return r;
+    } else {
+      GRS_HIP(hipMemsetAsync(row, 0, static_cast<size_t>(g) * 4, st));
+    }
+    if (append_verdict(s, row + g, cap, st) != GRS_OK) return GRS_EHIP;
+    GRS_HIP(hipEventRecord(s->xcev[c], st));
+  }
+  // 5. per chunk on X: count rows, the one host read of the chunk, its send / recv group
+  GRS_HIP(hipStreamWaitEvent(X, s->xcev[0], 0));   // (the samples' all-gather precedes it on st)
+  uint64_t recv_base = 0, recv_so_far[16] = {}, sent = 0, recvd = 0;
+  uint64_t soff[16], roff[16];
+  for (int c = 0; c < C; ++c) {
+    GRS_HIP(hipStreamWaitEvent(X, s->xcev[c], 0));
+    uint32_t* mat = mats + static_cast<size_t>(c) * g * W;
+    GRS_RCCL(ncclAllGather(rows + static_cast<size_t>(c) * W, mat, W, ncclUint32, comm, X));
+    GRS_HIP(hipMemcpyAsync(s->xchunk_host, mat, static_cast<size_t>(g) * W * 4, hipMemcpyDeviceToHost, X));
+    GRS_HIP(hipEventRecord(s->xhev, X));
+    GRS_HIP(hipEventSynchronize(s->xhev));
+    uint32_t* h = s->xchunk_host;
+    // every rank's cumulative receive after this chunk, for the verdict
+    uint64_t recv_tot[16] = {};
+    for (int q = 0; q < g; ++q) {
+      for (int p = 0; p < g; ++p) recv_so_far[p] += h[static_cast<size_t>(q) * W + p];
+    }
+    for (int p = 0; p < g; ++p) recv_tot[p] = recv_so_far[p];
+    if ((r = read_verdict(s, h, g, W, recv_tot, me, st)) != GRS_OK) return r;
+    for (int q = 0; q < g; ++q)
+      for (int p = 0; p < g; ++p) h[q * g + p] = h[static_cast<size_t>(q) * W + p];
+    const uint32_t c0 = std::min<uint32_t>(n, static_cast<uint32_t>(c) * chunk);
+    const uint64_t got = grs::shard_chunk_plan(h, g, me, c0, recv_base, soff, roff);
+    if (c == 0 && xmark(s, 1, X) != GRS_OK) return GRS_EHIP;
+    GRS_RCCL(ncclGroupStart());
+    for (int p = 0; p < g; ++p) {
+      if (p == me) continue;
+      const size_t sc = h[me * g + p], rc = h[p * g + me];
+      if (sc) GRS_RCCL(ncclSend(send + soff[p], sc, nccl_type<K>(), p, comm, X));
+      if (rc) GRS_RCCL(ncclRecv(out_k + roff[p], rc, nccl_type<K>(), p, comm, X));
+      sent += sc;
+      recvd += rc;
+    }
+    GRS_RCCL(ncclGroupEnd());
+    const size_t self = h[me * g + me];
+    if (self)
+      GRS_HIP(hipMemcpyAsync(out_k + roff[me], send + soff[me], self * sizeof(K), hipMemcpyDeviceToDevice, X));
+    recv_base += got;
+  }
+  GRS_HIP(hipEventRecord(s->xcev[16], X));
+  GRS_HIP(hipStreamWaitEvent(st, s->xcev[16], 0));
+  if (xmark(s, 2, st) != GRS_OK) return GRS_EHIP;
+  *n_out = static_cast<size_t>(recv_base);
+  // 6. local sort of the received run
+  const grs_status rs = grs_sort(s, out_k, nullptr, static_cast<size_t>(recv_base), st);
+  if (rs != GRS_OK || xmark(s, 3, st) != GRS_OK) return rs != GRS_OK ? rs : GRS_EHIP;
+  s->xev_recorded = s->ring > 0;
+  s->x_sent = sent * sizeof(K);
+  s->x_recv = recvd * sizeof(K);
+  s->x_presorted = 0;
+  return GRS_OK;
+}
+
 template <typename K, bool PAIRS>
 grs_status run_sharded(grs_sorter* s, const K* keys, const uint32_t* vals, uint32_t n, K* out_k,
                        uint32_t* out_v, size_t out_cap, size_t* n_out, ncclComm_t comm, int g,
                        int me, hipStream_t st) {
+  if constexpr (!PAIRS) {
+    if (s->sharded_exchange == 3) {   // chunked partition-first (keys only)
+      if (g <= 2) return run_sharded_chunked<K, 1>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+      if (g <= 4) return run_sharded_chunked<K, 3>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+      if (g <= 8) return run_sharded_chunked<K, 7>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+      return run_sharded_chunked<K, 15>(s, keys, n, out_k, out_cap, n_out, comm, g, me, st);
+    }
+  }
   if constexpr (sizeof(K) == 4 && !PAIRS) {
     // presorted exchange: u32 keys without payload, up to 4 ranks (GRS_OPT_EXCHANGE forces
     // either).  It moves ~1 byte a key instead of 4 but adds the
@@ -3308,6 +3496,20 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
       rank >= nranks)
     return set_err(GRS_EINVAL, "grs_shard_plan_host: bad argument");
   shard_plan(count_matrix, nranks, rank, send_off, recv_off, n_out);
+  return GRS_OK;
+}
+
+grs_status grs_shard_chunk_plan_host(const uint32_t* count_matrices, int nchunks, int nranks, int rank,
+                                     uint64_t chunk_len, uint64_t* send_off, uint64_t* recv_off, uint64_t* n_out) {
+  if (!count_matrices || !send_off || !recv_off || !n_out || nchunks < 1 || nranks < 1 || nranks > 16 ||
+      rank < 0 || rank >= nranks)
+    return set_err(GRS_EINVAL, "grs_shard_chunk_plan_host: bad argument");
+  const size_t gg = static_cast<size_t>(nranks) * nranks;
+  uint64_t base = 0;
+  for (int c = 0; c < nchunks; ++c)
+    base += grs::shard_chunk_plan(count_matrices + c * gg, nranks, rank, static_cast<uint64_t>(c) * chunk_len, base,
+                                  send_off + static_cast<size_t>(c) * nranks, recv_off + static_cast<size_t>(c) * nranks);
+  *n_out = base;
   return GRS_OK;
 }
 

@@ -751,9 +751,11 @@ struct LocalSort {
   }
   // the segment's keys (and payload) into registers, wave-striped (item j of lane l of wave w is
   // key w*64*I + j*64 + l)
+  // (t: threadIdx.x; a persistent caller passes an opaque copy per call, so that the compiler
+  // does not keep the I per-item offsets live across its loop)
   __device__ __forceinline__ static void load(K (&k)[I], Vals& v, const K* kin, const uint32_t* vin,
-                                              uint32_t lo, uint32_t len) {
-    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+                                              uint32_t lo, uint32_t len, uint32_t t = threadIdx.x) {
+    const uint32_t lane = t & (GRS_WAVE - 1), w = t >> 6;
 #pragma unroll
     for (uint32_t j = 0; j < I; ++j) {
       const uint32_t i = w * GRS_WAVE * I + j * GRS_WAVE + lane;
@@ -764,13 +766,14 @@ struct LocalSort {
   // `rounds` stable 8-bit rounds from the registers; the sorted segment is left in sm.sk / sm.sv,
   // element p at sm.sk[p + ak] / sm.sv[p + av] (ak, av: store_vec's alignment shifts)
   __device__ __forceinline__ static void sort_rounds(Smem& sm, K (&k)[I], Vals& v, uint32_t len, int rounds,
-                                                     uint32_t ak = 0, uint32_t av = 0, int shift0 = 0) {
+                                                     uint32_t ak = 0, uint32_t av = 0, int shift0 = 0,
+                                                     uint32_t t = threadIdx.x) {
     uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
     auto cld = [&](uint32_t a) -> uint32_t { if constexpr (C16) return c16[a]; else return sm.cnt[a]; };
     auto cst = [&](uint32_t a, uint32_t x) {
       if constexpr (C16) c16[a] = static_cast<uint16_t>(x); else sm.cnt[a] = x;
     };
-    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+    const uint32_t lane = t & (GRS_WAVE - 1), w = t >> 6;
 #pragma unroll
     for (int pass = 0; pass < ROUNDS; ++pass) {
       if (pass >= rounds) break;   // uniform
@@ -858,13 +861,13 @@ struct LocalSort {
   // multiples of 64 KB (the reference's 0..N-1 shuffled at 2^30: 16384-key segments) would
   // otherwise send every workgroup's stores to the same HBM channels at the same time
   template <typename T, uint32_t V, bool ROT = true>
-  __device__ __forceinline__ static void copy_out(T* run, const T* lds, uint32_t len) {
+  __device__ __forceinline__ static void copy_out(T* run, const T* lds, uint32_t len, uint32_t seed = blockIdx.x) {
     const uint32_t t = threadIdx.x, a = mis<T, V>(run);
     const uint32_t head = min(len, (V - a) % V);
     const uint32_t nv = (len - head) / V;
     if (t < head) run[t] = lds[swz_t<V>(a + t)];
     uint4* dst = reinterpret_cast<uint4*>(run + head);
-    const uint32_t rot = ROT && nv != 0u ? ((blockIdx.x * 97u & 255u) * 16u) % nv : 0u;
+    const uint32_t rot = ROT && nv != 0u ? ((seed * 97u & 255u) * 16u) % nv : 0u;
     for (uint32_t c = t; c < nv; c += BLOCK) {
       uint32_t r = c + rot;
       if (r >= nv) r -= nv;
@@ -952,6 +955,56 @@ struct LocalSort {
 // them, big[1] counts those longer than one fallback tile (TILEF keys), which get a histogram
 // row (ND digits) zeroed here; big_in / big_start / big_len / big_row hold (region start,
 // sorted start, length, row) per entry.
+// A P3 segment that is not sorted in this shape's LDS: one key (copied to its place, unless in
+// place), or longer than SMAX -- listed: up to mid_max keys in the mid list (mid[0] = count,
+// (in, out, len) from mid[2] on) for grs_msd_local_list's larger shape, longer ones in the big
+// list for the segmented LSD in place (grs_msd_copy_big moves them first): big[0] counts them,
+// big[1] counts those longer than one fallback tile (TILEF keys), which get a histogram row (ND
+// digits) zeroed here; big_in / big_start / big_len / big_row hold (region start, sorted start,
+// length, row) per entry.  Uniform in the workgroup; slot: an LDS word.
+template <typename K, bool PAIRS, int BLOCK, uint32_t SMAX, uint32_t ND, uint32_t TILEF>
+__device__ __forceinline__ void msd_local_other(uint32_t len, uint32_t lo, uint32_t o, bool inplace, const K* kin,
+                                                const uint32_t* vin, K* keys, uint32_t* vals, uint32_t mid_max,
+                                                uint32_t* mid, uint32_t* big, uint32_t* big_in,
+                                                uint32_t* big_start, uint32_t* big_len, uint32_t* big_row,
+                                                uint32_t* rows, uint32_t& slot) {
+  const uint32_t t = threadIdx.x;
+  if (len == 1u) {
+    if (!inplace && t == 0) {
+      keys[o] = kin[lo];
+      if constexpr (PAIRS) vals[o] = vin[lo];
+    }
+    return;
+  }
+  if (len <= SMAX) return;   // (0)
+  if (len <= mid_max) {   // the mid list (a larger LDS shape)
+    if (t == 0) {
+      const uint32_t e = atomicAdd(&mid[0], 1u);
+      mid[2 + 3 * e] = lo;
+      mid[3 + 3 * e] = o;
+      mid[4 + 3 * e] = len;
+    }
+    return;
+  }
+  if (t == 0) {
+    const uint32_t e = atomicAdd(&big[0], 1u);
+    const uint32_t row = len > TILEF ? atomicAdd(&big[1], 1u) : 0xFFFFFFFFu;
+    big_in[e] = lo;
+    big_start[e] = o;
+    big_len[e] = len;
+    big_row[e] = row;
+    slot = row;
+  }
+  __syncthreads();
+  const uint32_t row = slot;
+  if (row != 0xFFFFFFFFu)
+    for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(row) * ND * 256 + i] = 0;
+}
+
+// P3: one workgroup per 16-bit prefix b (grid 65536): its len2[b] keys (and payload), read at
+// in2[b] of the region buffer (rk / rv) -- or, after a P2 spill, of the caller's arrays, in
+// place -- sorted in LDS (LocalSort) and written to out2[b] of the caller's arrays
+// (grs_msd_starts); the others as msd_local_other says.
 template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF>
 __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uint32_t* __restrict__ vals,
                                                        const K* __restrict__ rk, const uint32_t* __restrict__ rv,
@@ -970,42 +1023,15 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
   using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
   constexpr uint32_t ND = LS::ROUNDS;   // fallback digits (histogram row of ND x 256 words)
   __shared__ typename LS::Smem sm;
-  const uint32_t t = threadIdx.x;
   const uint32_t len = len2[blockIdx.x];
   if (len == 0u) return;   // (the start of an empty segment was never written)
   const bool inplace = __builtin_amdgcn_readfirstlane(*spill) != 0u;
   const uint32_t lo = in2[blockIdx.x], o = out2[blockIdx.x];
   const K* const kin = inplace ? keys : rk;
   const uint32_t* const vin = inplace ? vals : rv;
-  if (len == 1u) {
-    if (!inplace && t == 0) {
-      keys[o] = kin[lo];
-      if constexpr (PAIRS) vals[o] = vin[lo];
-    }
-    return;
-  }
-  if (len > LS::SMAX) {
-    if (len <= mid_max) {   // the mid list (a larger LDS shape)
-      if (t == 0) {
-        const uint32_t e = atomicAdd(&mid[0], 1u);
-        mid[2 + 3 * e] = lo;
-        mid[3 + 3 * e] = o;
-        mid[4 + 3 * e] = len;
-      }
-      return;
-    }
-    if (t == 0) {
-      const uint32_t e = atomicAdd(&big[0], 1u);
-      const uint32_t row = len > TILEF ? atomicAdd(&big[1], 1u) : 0xFFFFFFFFu;
-      big_in[e] = lo;
-      big_start[e] = o;
-      big_len[e] = len;
-      big_row[e] = row;
-      sm.slot = row;
-    }
-    __syncthreads();
-    if (sm.slot != 0xFFFFFFFFu)
-      for (uint32_t i = t; i < ND * 256; i += BLOCK) rows[static_cast<size_t>(sm.slot) * ND * 256 + i] = 0;
+  if (len == 1u || len > LS::SMAX) {
+    msd_local_other<K, PAIRS, BLOCK, LS::SMAX, ND, TILEF>(len, lo, o, inplace, kin, vin, keys, vals, mid_max, mid,
+                                                          big, big_in, big_start, big_len, big_row, rows, sm.slot);
     return;
   }
   // the bits below the segment's 16-bit prefix (bits above the top digit are equal in every key);
@@ -1013,6 +1039,73 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
   const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
   LS::template run_vec<>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, len,
                          rounds);
+}
+
+// P3 persistent (keys sorted in at most two LDS rounds: u32 keys, u32 pairs): grid = resident
+// workgroups, each drawing segments from a ticket (*ticket zero at launch) until past 65536.
+// The next segment's keys are loaded into the registers as soon as this one's last round has
+// scattered them into LDS, so the loads fly while this segment is stored (one workgroup per
+// segment paid the full HBM latency of its loads after its predecessor's stores).  The same
+// results as grs_msd_local.
+template <typename K, bool PAIRS, int BLOCK, int I, bool C16, uint32_t TILEF, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_pf(
+    K* __restrict__ keys, uint32_t* __restrict__ vals, const K* __restrict__ rk, const uint32_t* __restrict__ rv,
+    const uint32_t* __restrict__ spill, const uint32_t* __restrict__ len2, const uint32_t* __restrict__ in2,
+    const uint32_t* __restrict__ out2, uint32_t mid_max, uint32_t* __restrict__ mid, uint32_t* __restrict__ big,
+    uint32_t* __restrict__ big_in, uint32_t* __restrict__ big_start, uint32_t* __restrict__ big_len,
+    uint32_t* __restrict__ big_row, uint32_t* __restrict__ rows, const uint32_t* __restrict__ top_shift,
+    uint32_t* __restrict__ ticket) {
+  using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
+  static_assert(LS::ROUNDS <= 2, "u64 keys: grs_msd_local (its run finish may reload the keys)");
+  constexpr uint32_t ND = LS::ROUNDS, NSEG = 65536;
+  __shared__ typename LS::Smem sm;
+  __shared__ uint32_t nxt;
+  const uint32_t t = threadIdx.x;
+  const bool inplace = __builtin_amdgcn_readfirstlane(*spill) != 0u;
+  const K* const kin = inplace ? keys : rk;
+  const uint32_t* const vin = inplace ? vals : rv;
+  const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
+  auto sorted_here = [](uint32_t l) { return l >= 2u && l <= LS::SMAX; };
+  if (t == 0) nxt = atomicAdd(ticket, 1u);
+  __syncthreads();
+  uint32_t b = __builtin_amdgcn_readfirstlane(nxt);
+  K k[I];
+  typename LS::Vals v;
+  uint32_t len = b < NSEG ? len2[b] : 0u;
+  if (b < NSEG && sorted_here(len)) LS::load(k, v, kin, vin, in2[b], len);
+  while (b < NSEG) {
+    __syncthreads();   // every thread has read nxt
+    if (t == 0) nxt = atomicAdd(ticket, 1u);
+    const uint32_t lo = in2[b], o = out2[b];
+    const bool here = sorted_here(len);
+    if (here) {
+      const uint32_t ak = LS::template mis<K, LS::KV>(keys + o);
+      const uint32_t av = PAIRS ? LS::template mis<uint32_t, LS::VV>(vals + o) : 0u;
+      uint32_t tt = t;
+      asm volatile("" : "+v"(tt));
+      LS::sort_rounds(sm, k, v, len, rounds, ak, av, 0, tt);   // (its barriers publish nxt)
+    } else {
+      if (len != 0u)
+        msd_local_other<K, PAIRS, BLOCK, LS::SMAX, ND, TILEF>(len, lo, o, inplace, kin, vin, keys, vals, mid_max,
+                                                              mid, big, big_in, big_start, big_len, big_row, rows,
+                                                              sm.slot);
+      __syncthreads();
+    }
+    const uint32_t nb = __builtin_amdgcn_readfirstlane(nxt);
+    const uint32_t nlen = nb < NSEG ? len2[nb] : 0u;
+    // the registers are free (the last round scattered them into LDS): the next segment's loads
+    if (nb < NSEG && sorted_here(nlen)) {
+      uint32_t tt = t;
+      asm volatile("" : "+v"(tt));
+      LS::load(k, v, kin, vin, in2[nb], nlen, tt);
+    }
+    if (here) {
+      LS::template copy_out<K, LS::KV>(keys + o, sm.sk, len, b);
+      if constexpr (PAIRS) LS::template copy_out<uint32_t, LS::VV>(vals + o, sm.sv, len, b);
+    }
+    b = nb;
+    len = nlen;
+  }
 }
 
 // P3's second shape: the mid list's segments (persistent grid, a segment per workgroup in

@@ -152,3 +152,41 @@ __global__ __launch_bounds__(1024) void grs_shard_splitters_sorted(const K* __re
 }
 
 }  // namespace grs
+
+namespace grs {
+
+// Chunked exchange (GRS_OPT_EXCHANGE = 3): the partition digit of chunk c of the shard (shard
+// positions [c * chunk, ...)) takes chunk-local indices, so its thresholds move down by
+// c * chunk (a threshold at or below the chunk's start becomes 0: every element of the chunk is
+// at or past it).  One thread per (chunk, splitter slot).
+template <typename K, int N>
+__global__ void grs_shard_chunk_digits(const SplitterIdxDigit<K, N>* __restrict__ dig, uint32_t chunks,
+                                       uint32_t chunk, SplitterIdxDigit<K, N>* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= chunks * GRS_MAX_SPLITTERS) return;
+  const uint32_t c = i / GRS_MAX_SPLITTERS, j = i % GRS_MAX_SPLITTERS;
+  const uint64_t base = static_cast<uint64_t>(c) * chunk;
+  if (j == 0) out[c].count = dig->count;
+  out[c].s[j] = dig->s[j];
+  const uint32_t th = dig->th[j];
+  out[c].th[j] = th == 0xFFFFFFFFu ? th : th <= base ? 0u : static_cast<uint32_t>(th - base);
+}
+
+// The chunked exchange's plan for chunk c: mat = the G x G count matrix of that chunk (row r:
+// what rank r's chunk c sends to each bucket), its buckets contiguous from c * chunk of the send
+// buffer; received chunk-major: chunk c's runs from every source follow everything received in
+// chunks < c (recv_base), in source-rank order.  send_off / recv_off: G entries; returns the
+// items received in this chunk.
+__host__ __forceinline__ uint64_t shard_chunk_plan(const uint32_t* mat, int g, int me, uint64_t chunk_start,
+                                                   uint64_t recv_base, uint64_t* send_off, uint64_t* recv_off) {
+  uint64_t so = chunk_start, ro = recv_base;
+  for (int p = 0; p < g; ++p) {
+    send_off[p] = so;
+    so += mat[me * g + p];
+    recv_off[p] = ro;
+    ro += mat[p * g + me];
+  }
+  return ro - recv_base;
+}
+
+}  // namespace grs

@@ -164,7 +164,10 @@ typedef enum grs_option {
                                 partition is redone into contiguous buckets), 1 bucket histogram
                                 + contiguous buckets always, 2 test hook: regions of n / (2G)
                                 items, so full buckets spill and the redo path runs */
-  GRS_OPT_EXCHANGE = 8,      /* 0 by rank count (default), 1 partition-first, 2 presorted */
+  GRS_OPT_EXCHANGE = 8,      /* 0 by rank count (default), 1 partition-first, 2 presorted, 3
+                                chunked partition-first (keys without payload: each chunk of the
+                                shard crosses the links while the next is partitioned; received
+                                chunk-major; not measured on more than one GPU) */
   GRS_OPT_MERGE = 9,         /* presorted exchange, receive side: 0 (default) ceil(log2 k)
                                 2-way merge rounds over the k received runs, 1 one k-way merge
                                 pass (sample-delimited tiles merged in LDS; slower at 8 ranks) */
@@ -192,8 +195,13 @@ typedef enum grs_option {
   GRS_OPT_H2_CHUNK = 13,     /* the MSD sort's byte-2 histogram: 0 (default) by size, else the
                                 keys of P1's output per workgroup (a power of two, 4096..2^20;
                                 A/B runs) */
-  GRS_OPT_H2_PIECE = 14      /* the same histogram's sample: 0 (default) pieces of 256 keys, else
+  GRS_OPT_H2_PIECE = 14,     /* the same histogram's sample: 0 (default) pieces of 256 keys, else
                                 the keys of a piece (a power of two, 64..4096; A/B runs) */
+  GRS_OPT_P3 = 15,           /* the MSD sort's LDS segment sort, u32 keys and u32 pairs: 0
+                                (default) one workgroup per segment, 1 persistent workgroups that
+                                load the next segment while storing this one (slower; A/B runs) */
+  GRS_OPT_X_CHUNKS = 16      /* chunks of the chunked exchange (GRS_OPT_EXCHANGE = 3): 0 (default)
+                                4, else 1..16; the same on every rank */
 } grs_option;
 grs_status grs_set_option(grs_sorter* s, grs_option opt, int value);
 grs_status grs_get_option(const grs_sorter* s, grs_option opt, int* value);
@@ -335,6 +343,13 @@ grs_status grs_shard_plan_host(const uint32_t* count_matrix, int nranks, int ran
 grs_status grs_shard_bounds_host(const void* sorted_keys, size_t n, int key_bytes,
                                  const void* splitters, const uint32_t* thresholds, int nranks,
                                  uint64_t* bounds_out);
+/* The chunked exchange's plan (GRS_OPT_EXCHANGE = 3): count_matrices = nchunks G x G matrices
+ * (chunk c's row r = what rank r's chunk c sends to each bucket; chunk c of a shard starts at
+ * c * chunk_len, its buckets contiguous from there in the send buffer).  Received chunk-major:
+ * send_off / recv_off get nchunks x G offsets, n_out the received total. */
+grs_status grs_shard_chunk_plan_host(const uint32_t* count_matrices, int nchunks, int nranks, int rank,
+                                     uint64_t chunk_len, uint64_t* send_off, uint64_t* recv_off,
+                                     uint64_t* n_out);
 /* Samples per rank of the sharded sort for nranks ranks (min(1024, 8192 / nranks)). */
 int grs_shard_samples_per_rank(int nranks);
 

@@ -151,3 +151,59 @@ def sim_presorted_sort(keys: np.ndarray, group=None):
     runs = np.split(rk.numpy().view(np.uint32), np.cumsum(rc)[:-1])
     assert all(np.all(r[1:] >= r[:-1]) for r in runs)   # every received run is sorted
     return np.sort(np.concatenate(runs), kind="stable"), mat
+
+
+def _chunk_thresholds(th: np.ndarray, base: int) -> np.ndarray:
+    """grs_shard_chunk_digits: the thresholds of the chunk that starts at shard position base."""
+    th = th.astype(np.uint64)
+    out = np.where(th == 0xFFFFFFFF, th, np.where(th <= base, 0, th - np.uint64(base)))
+    return out.astype(np.uint32)
+
+
+def sim_chunked_sort(keys: np.ndarray, chunks: int, group=None):
+    """The chunked partition-first exchange (run_sharded_chunked, keys only): the same splitters;
+    per chunk c of ceil(n / chunks) keys the partition digit with chunk-local thresholds, the
+    chunk's count matrix all-gathered, the plan from libgrs's host twin
+    grs_shard_chunk_plan_host (chunk-major receive), the chunk's exchange into its planned
+    place; then the local sort.  Returns (keys_out, [count matrix per chunk], receive buffer)."""
+    L, check = _lib()
+    G, me = dist.get_world_size(group), dist.get_rank(group)
+    S = int(L.grs_shard_samples_per_rank(G))
+    kb = keys.dtype.itemsize
+    n = keys.size
+    sk, sp = _samples(keys, S)
+    spl, th = _splitters(sk, sp, G, me, S, kb, keys.dtype, group)
+    every = _buckets(keys, spl, th)
+    chunk = (n + chunks - 1) // chunks
+    mats, sends = [], []
+    for c in range(chunks):
+        c0 = min(n, c * chunk)
+        part = keys[c0:min(n, c0 + chunk)]
+        b = _buckets(part, spl, _chunk_thresholds(th, c0))
+        assert np.array_equal(b, every[c0:c0 + part.size])   # same buckets as the whole shard's
+        sends.append(part[np.argsort(b, kind="stable")])
+        cnt = np.bincount(b, minlength=G).astype(np.uint32)
+        mats.append(np.ascontiguousarray(_all_gather_np(cnt, G, group)).reshape(G, G))
+    allm = np.ascontiguousarray(np.stack(mats))
+    soff = (ctypes.c_uint64 * (chunks * G))()
+    roff = (ctypes.c_uint64 * (chunks * G))()
+    n_out = ctypes.c_uint64()
+    check(L.grs_shard_chunk_plan_host(allm.ctypes.data, chunks, G, me, chunk, soff, roff, ctypes.byref(n_out)),
+          "grs_shard_chunk_plan_host")
+    wide = np.int64 if kb == 8 else np.int32
+    recv = np.zeros(int(n_out.value), keys.dtype)
+    base = 0
+    for c in range(chunks):
+        m = mats[c]
+        sc = [int(x) for x in m[me]]
+        rc = [int(x) for x in m[:, me]]
+        c0 = min(n, c * chunk)
+        assert [int(soff[c * G + p]) for p in range(G)] == list(c0 + np.concatenate([[0], np.cumsum(sc)[:-1]]))
+        assert [int(roff[c * G + p]) for p in range(G)] == list(base + np.concatenate([[0], np.cumsum(rc)[:-1]]))
+        rk = torch.empty(sum(rc), dtype=torch.int64 if kb == 8 else torch.int32)
+        dist.all_to_all_single(rk, torch.from_numpy(sends[c].view(wide).copy()), output_split_sizes=rc,
+                               input_split_sizes=sc, group=group)
+        recv[base:base + sum(rc)] = rk.numpy().view(keys.dtype)
+        base += sum(rc)
+    assert base == int(n_out.value)
+    return np.sort(recv), mats, recv

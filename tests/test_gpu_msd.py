@@ -114,6 +114,32 @@ def test_msd_segment_edges(gpu, sizes):
     assert np.array_equal(got, np.sort(keys))
 
 
+@pytest.mark.parametrize("pairs", [False, True])
+def test_msd_persistent_p3_option(gpu, pairs):
+    """Option p3=persistent (grs_msd_local_pf, an A/B variant): the same keys and permutation as
+    the stable sort, through the mid and big lists and at a size with many segments."""
+    import gpuradixsort_amd as grs
+
+    rng = np.random.default_rng(77 + pairs)
+    cases = [_segment_keys(rng, [5120, 5121, 1, 2, 4096]),
+             _segment_keys(rng, [6000, 10000, 18432, 18433, 100, 36865]),
+             rng.integers(0, 1 << 32, (1 << 22) + 3, dtype=np.uint64).astype(np.uint32)]
+    s = grs.RadixSorter(1 << 23, key_bits=32, pairs=pairs, radix_bits=8)
+    s.set_option("msd", "always")
+    s.set_option("p3", "persistent")
+    for keys in cases:
+        k = torch.from_numpy(keys).to(gpu)
+        v = torch.arange(keys.size, dtype=torch.int64, device=gpu).to(torch.uint32) if pairs else None
+        s.sort(k, v)
+        s.check_error()
+        perm = np.argsort(keys, kind="stable")
+        assert np.array_equal(k.cpu().numpy(), keys[perm])
+        if pairs:
+            assert np.array_equal(v.cpu().numpy(), perm.astype(np.uint32))
+    assert s.check_guards() == 0
+    s.close()
+
+
 @pytest.mark.parametrize("n", [1 << 24, (1 << 26) + 12345])
 def test_msd_larger(gpu, n):
     """Sizes where the MSD schedule is (or is about to be) the default: uniform and narrow

@@ -85,6 +85,38 @@ def test_sharded_sort_world1_rccl(gpu, world1, monkeypatch, path, key_bits, pair
     s.sorter.close()
 
 
+@pytest.mark.parametrize("key_bits,n,chunks,dist_name", [(32, 1_000_003, 4, "uniform"), (32, 300_001, 1, "ties"),
+                                                         (64, 777_777, 7, "uniform"), (32, 5, 4, "uniform"),
+                                                         (32, 60_000_013, 4, "uniform"), (64, 1_000_000, 16, "ties")])
+def test_sharded_chunked_world1_rccl(gpu, world1, key_bits, n, chunks, dist_name):
+    """The chunked partition-first exchange (exchange=chunked, keys only) on a one-rank RCCL
+    communicator: chunk digits, one partition per chunk on the caller's stream, per chunk the
+    count all-gather, host read, and send / recv (self copy) on the second stream, the local
+    sort after it -- sorted, with more chunks than keys, and past 48M keys (MSD local sort)."""
+    from gpuradixsort_amd.sharded import ShardedSorter
+
+    rng = np.random.default_rng(n + chunks)
+    dt = np.uint32 if key_bits == 32 else np.uint64
+    keys = rng.integers(0, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+    if dist_name == "ties":
+        keys[::7] = 3
+    s = ShardedSorter(n, key_bits=key_bits, device=gpu, comm=world1,
+                      options={"sharded_path": "general", "exchange": "chunked", "x_chunks": chunks})
+    k = torch.from_numpy(keys).to(gpu)
+    want = np.sort(keys)
+    for _ in range(2):
+        ko, _ = s.sort(k.clone())
+        assert s.last_n_out == n
+        assert np.array_equal(ko.cpu().numpy(), want)
+    s.set_profiling(2)
+    s.sort(k.clone())
+    xt = s.exchange_timing()
+    assert xt["bytes_sent"] == 0 and xt["total_ms"] >= xt["exchange_ms"] >= 0.0
+    s.sorter.check_error()
+    assert s.sorter.check_guards() == 0
+    s.sorter.close()
+
+
 @pytest.mark.parametrize("path", ["general", "one_rank"])
 def test_sharded_prefix_n(gpu, world1, monkeypatch, path):
     """n < keys.numel(): only the first n items take part (samples, partition, exchange,

@@ -125,6 +125,44 @@ def test_presorted_exchange_equals_sort(tmp_path, world, n_local, dist_name):
     assert np.load(tmp_path / "mat.npy").sum() == n_local * world
 
 
+def _worker_chunked(rank, world, port, n_local, key_bits, chunks, dist_name, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sharded_sim
+
+    allk = _input(dist_name, n_local * world, key_bits)
+    ko, mats, _ = sharded_sim.sim_chunked_sort(allk[rank * n_local:(rank + 1) * n_local].copy(), chunks)
+    np.save(os.path.join(out_dir, f"k{rank}.npy"), ko)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "all.npy"), allk)
+        np.save(os.path.join(out_dir, "mats.npy"), np.stack(mats))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_local,key_bits,chunks,dist_name", [
+    (2, 5000, 32, 4, "uniform"), (3, 3001, 64, 3, "skewed"), (4, 2500, 32, 1, "all_equal"),
+    (4, 20000, 32, 7, "few_unique"), (2, 3, 32, 4, "uniform"), (2, 0, 32, 4, "uniform"),
+    (8, 3000, 32, 4, "skewed"), (8, 2001, 64, 16, "few_unique"),
+])
+def test_chunked_exchange_equals_sort(tmp_path, world, n_local, key_bits, chunks, dist_name):
+    """The chunked partition-first exchange's orchestration (keys only; GRS_OPT_EXCHANGE = 3):
+    chunk-local thresholds give every key the bucket of the whole shard, the chunk-major plan of
+    libgrs's host twin places every chunk's runs, and the ranks' outputs concatenate to the
+    sorted input, balanced on duplicate-heavy inputs."""
+    port = _free_port()
+    mp.spawn(_worker_chunked, args=(world, port, n_local, key_bits, chunks, dist_name, str(tmp_path)),
+             nprocs=world, join=True)
+    allk = np.load(tmp_path / "all.npy")
+    outs = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
+    assert np.array_equal(np.concatenate(outs), np.sort(allk))
+    if n_local and dist_name in ("all_equal", "few_unique"):
+        sizes = np.array([o.size for o in outs], np.float64)
+        assert sizes.max() / sizes.mean() <= 1.1, sizes
+    assert np.load(tmp_path / "mats.npy").sum() == n_local * world
+
+
 def test_host_twins_validate_arguments():
     import ctypes
 
@@ -138,3 +176,9 @@ def test_host_twins_validate_arguments():
     so, ro, n = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)(), ctypes.c_uint64()
     assert L.grs_shard_plan_host(mat.ctypes.data, 2, 1, so, ro, ctypes.byref(n)) == 0
     assert list(so) == [0, 2] and list(ro) == [0, 1] and n.value == 6
+    # two chunks of 10: chunk 1's sends start at 10, its receives after chunk 0's 6
+    mats = np.array([[[3, 1], [2, 5]], [[4, 0], [1, 1]]], np.uint32)
+    so4, ro4 = (ctypes.c_uint64 * 4)(), (ctypes.c_uint64 * 4)()
+    assert L.grs_shard_chunk_plan_host(mats.ctypes.data, 2, 2, 1, 10, so4, ro4, ctypes.byref(n)) == 0
+    assert list(so4) == [0, 2, 10, 11] and list(ro4) == [0, 1, 6, 6] and n.value == 7
+    assert L.grs_shard_chunk_plan_host(None, 2, 2, 1, 10, so4, ro4, ctypes.byref(n)) == _lib.GRS_EINVAL

@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--total", type=int, default=1 << 30)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--chunks", type=int, default=4, help="chunks of the chunked exchange")
+    ap.add_argument("--link-gbs", type=float, default=64.0, help="xGMI GB/s per direction per link")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = lib()
@@ -98,6 +100,7 @@ def main():
                                       th.ctypes.data, G - 1, region, ctypes.c_void_p(cnt.data_ptr()), sp),
               "partition_regions")
     ms = timed(part_regions, a.reps)
+    ms_part_regions = ms
     s.check_error()
     print(json.dumps({"step": "partition_regions", "ranks": G, "n_local": n, "ms": round(ms, 4),
                       "GB/s": round(n * 8 / ms / 1e6, 1)}), flush=True)
@@ -108,6 +111,7 @@ def main():
         grs.fill_splitmix(b, seed)
     it = iter(bufs)
     ms = timed(lambda: s.sort(next(it)), a.reps)
+    ms_sort = ms
     s.check_error()
     print(json.dumps({"step": "local_sort", "n": n, "ms": round(ms, 4),
                       "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
@@ -120,6 +124,7 @@ def main():
             b.view(torch.int32).bitwise_and_((1 << (32 - lg)) - 1)
     it = iter(bufs)
     ms = timed(lambda: s.sort(next(it)), a.reps)
+    ms_sort_range = ms
     s.check_error()
     print(json.dumps({"step": "local_sort_one_range", "n": n, "key_range_bits": 32 - lg,
                       "ms": round(ms, 4), "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
@@ -133,18 +138,53 @@ def main():
     dist.init_process_group("gloo", rank=0, world_size=1)
     from gpuradixsort_amd.sharded import ShardedSorter
 
-    sh = ShardedSorter(n, key_bits=32, device=dev)
-    bufs = [torch.empty_like(shard) for _ in range(a.reps + 1)]
-    for b in bufs:
-        grs.fill_splitmix(b, seed)
-    it = iter(bufs)
-    ms = timed(lambda: sh.sort(next(it), check_error=False), a.reps)
-    sh.sorter.check_error()
-    assert sh.count_inversions() == 0
-    print(json.dumps({"step": "sharded_world1", "n": n, "ms": round(ms, 4),
-                      "Gkeys/s": round(n / ms / 1e6, 2)}), flush=True)
-    sh.close()
+    world1 = {}
+    for name, opts in [("sharded_world1", {}),
+                       ("sharded_world1_partition", {"sharded_path": "general", "exchange": "partition"}),
+                       ("sharded_world1_chunked", {"sharded_path": "general", "exchange": "chunked",
+                                                   "x_chunks": a.chunks})]:
+        sh = ShardedSorter(n, key_bits=32, device=dev, options=opts)
+        bufs = [torch.empty_like(shard) for _ in range(a.reps + 1)]
+        for b in bufs:
+            grs.fill_splitmix(b, seed)
+        it = iter(bufs)
+        ms = timed(lambda: sh.sort(next(it), check_error=False), a.reps)
+        sh.sorter.check_error()
+        assert sh.count_inversions() == 0
+        line = {"step": name, "n": n, "ms": round(ms, 4), "Gkeys/s": round(n / ms / 1e6, 2)}
+        if opts:
+            sh.set_profiling(2)
+            grs.fill_splitmix(bufs[0], seed)
+            sh.sort(bufs[0])
+            line["phases_ms"] = {k: round(v, 4) for k, v in sh.exchange_timing().items()
+                                 if k.endswith("_ms")}
+        world1[name] = ms
+        print(json.dumps(line), flush=True)
+        sh.close()
+        del bufs
     dist.destroy_process_group()
+
+    # one chunk's partition, and the step's critical path at G ranks from the measured parts:
+    # the exchange moves n / G keys over each of the G - 1 links (one link per peer)
+    cn = (n + a.chunks - 1) // a.chunks
+    ms_chunk = timed(lambda: check(L.grs_partition_ranges(
+        s._h, ctypes.c_void_p(shard.data_ptr()), None, ctypes.c_void_p(out.data_ptr()), None, cn,
+        spl.ctypes.data, th.ctypes.data, G - 1, ctypes.c_void_p(cnt.data_ptr()), sp), "partition"), a.reps)
+    link_ms = (n / G) * 4 / (a.link_gbs * 1e9) * 1e3
+    # fixed orchestration (samples, splitters, count all-gathers, host syncs) beyond partition
+    # and local sort, from the one-rank runs; the chunked run's extra per chunk on top of that
+    fixed = max(0.0, world1["sharded_world1_partition"] - ms_part_regions - ms_sort)
+    per_chunk = max(0.0, (world1["sharded_world1_chunked"] - world1["sharded_world1_partition"]) / a.chunks)
+    pf = ms_part_regions + link_ms + ms_sort_range + fixed
+    ch = ms_chunk + max((a.chunks - 1) * ms_chunk, link_ms + a.chunks * per_chunk) + ms_sort_range + fixed
+    print(json.dumps({"step": "projection", "ranks": G, "n_local": n, "chunks": a.chunks,
+                      "link_GBps": a.link_gbs, "link_ms": round(link_ms, 4),
+                      "partition_chunk_ms": round(ms_chunk, 4), "fixed_ms": round(fixed, 4),
+                      "chunk_overhead_ms": round(per_chunk, 4),
+                      "step_partition_first_ms": round(pf, 4), "step_chunked_ms": round(ch, 4),
+                      "speedup_vs_1gpu_partition_first": round(G * ms_sort / pf, 2),
+                      "speedup_vs_1gpu_chunked": round(G * ms_sort / ch, 2),
+                      "note": "unmeasured across GPUs: one-GPU parts plus link arithmetic"}), flush=True)
 
 
 if __name__ == "__main__":
