@@ -459,6 +459,9 @@ __global__ __launch_bounds__(GRS_HIST_BLOCK) void grs_digit_hist(
     uint4 x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) x[u] = kv[v + u * stride];
+    // all U issued before the first count (the scheduler otherwise pairs each load with its wait)
+#pragma unroll
+    for (int u = 0; u < U; ++u) asm volatile("" ::"v"(x[u].x), "v"(x[u].y), "v"(x[u].z), "v"(x[u].w));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const K* kk = reinterpret_cast<const K*>(&x[u]);

@@ -231,6 +231,9 @@ __global__ __launch_bounds__(256) void grs_seg_hist(const K* __restrict__ keys,
 // ---------------------------------------------------------------------------------------
 #define GRS_H2_CHUNK 262144
 #define GRS_H2_COPIES 32
+#ifndef GRS_H2_INFLIGHT
+#define GRS_H2_INFLIGHT 8   // 16-B loads in flight per thread in H2
+#endif
 #define GRS_MSD_SAMPLE_CHUNKS 16384   // 64-key chunks the sample reads (2^20 keys)
 #define GRS_MSD_GUESS_CHUNKS 64       // 64-key chunks every sample block reads for the span guess
 
@@ -519,18 +522,32 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
     const uint32_t ns = ((np + (1u << sample_shift) - 1) >> sample_shift) << pul;
     auto at = [&](uint32_t m) { return ((m >> pul) << (sample_shift + pul)) + (m & (PU - 1u)); };
     uint32_t m = t;
-    for (; m + 3 * B < ns; m += 4 * B) {   // four loads in flight (one at a time: latency-bound)
-      uint4 x[4];
-      bool ok[4];
+    // GRS_H2_INFLIGHT loads in flight per thread (a block's whole share in one or two rounds:
+    // the loop is latency-bound, one at a time ran at 0.7 TB/s)
+    constexpr int U = GRS_H2_INFLIGHT;
+    for (; m + (U - 1) * B < ns; m += U * B) {
+      uint4 x[U];
+      bool ok[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const uint32_t v = at(m + u * B);
         ok[u] = v < nv;
         x[u] = kv[ok[u] ? v : 0u];   // (nv >= 1 here: ns > 0)
       }
+      // every load issued before the first count (the scheduler otherwise pairs each load
+      // with its wait and counts: one in flight)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (ok[u]) count4(x[u]);
+      for (int u = 0; u < U; ++u) asm volatile("" ::"v"(x[u].x), "v"(x[u].y), "v"(x[u].z), "v"(x[u].w));
+      // (the counts add 0 for a load past the chunk instead of branching round it: a branch
+      // let the compiler sink each load into its branch and wait for it alone)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const K* e = reinterpret_cast<const K*>(&x[u]);
+        const uint32_t one = ok[u] ? 1u : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < VEC; ++q)
+          atomicAdd(base + (static_cast<uint32_t>(e[q] >> SH) & 255u) * GRS_H2_COPIES, one);
+      }
     }
     for (; m < ns; m += B) {
       const uint32_t v = at(m);
@@ -541,12 +558,15 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   }
   if (t < head) count(kc[t]);
   uint32_t i = t;
-  for (; i + 3 * B < nv; i += 4 * B) {
-    uint4 x[4];
+  constexpr int U = GRS_H2_INFLIGHT;
+  for (; i + (U - 1) * B < nv; i += U * B) {
+    uint4 x[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = kv[i + u * B];
+    for (int u = 0; u < U; ++u) x[u] = kv[i + u * B];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) count4(x[u]);
+    for (int u = 0; u < U; ++u) asm volatile("" ::"v"(x[u].x), "v"(x[u].y), "v"(x[u].z), "v"(x[u].w));
+#pragma unroll
+    for (int u = 0; u < U; ++u) count4(x[u]);
   }
   for (; i < nv; i += B) count4(kv[i]);
   for (uint32_t r = head + nv * VEC + t; r < cl; r += B) count(kc[r]);

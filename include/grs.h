@@ -40,9 +40,12 @@
 extern "C" {
 #endif
 
-#define GRS_VERSION 400 /* 4.0.0: grs_timing gained `kind` (3.x callers' structs are 4 bytes
-                           shorter); guard bands + grs_debug_check_guards; grs_fill_permutation;
-                           the MSD sort's scratch allocated by capacity / option */
+#define GRS_VERSION 410 /* 4.1.0: grs_debug_msd_flags, grs_shard_chunk_plan_host, options
+                           GRS_OPT_H2_PIECE, GRS_OPT_P3, GRS_OPT_X_CHUNKS and GRS_OPT_EXCHANGE = 3
+                           (additions only).  4.0.0: grs_timing gained `kind` (3.x callers'
+                           structs are 4 bytes shorter); guard bands + grs_debug_check_guards;
+                           grs_fill_permutation; the MSD sort's scratch allocated by capacity /
+                           option */
 
 typedef enum grs_status {
   GRS_OK = 0,

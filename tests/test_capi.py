@@ -36,7 +36,7 @@ def test_version_and_status_strings():
     from gpuradixsort_amd import _lib
 
     L = _lib.lib()
-    assert L.grs_version() == 400
+    assert L.grs_version() == 410
     assert L.grs_status_string(0) == b"GRS_OK"
     assert L.grs_status_string(4) == b"GRS_ECAPACITY"
 

@@ -159,6 +159,8 @@ def main():
             line["phases_ms"] = {k: round(v, 4) for k, v in sh.exchange_timing().items()
                                  if k.endswith("_ms")}
         world1[name] = ms
+        if opts:
+            world1[name + "_before"] = line["phases_ms"]["before_ms"]
         print(json.dumps(line), flush=True)
         sh.close()
         del bufs
@@ -171,9 +173,11 @@ def main():
         s._h, ctypes.c_void_p(shard.data_ptr()), None, ctypes.c_void_p(out.data_ptr()), None, cn,
         spl.ctypes.data, th.ctypes.data, G - 1, ctypes.c_void_p(cnt.data_ptr()), sp), "partition"), a.reps)
     link_ms = (n / G) * 4 / (a.link_gbs * 1e9) * 1e3
-    # fixed orchestration (samples, splitters, count all-gathers, host syncs) beyond partition
-    # and local sort, from the one-rank runs; the chunked run's extra per chunk on top of that
-    fixed = max(0.0, world1["sharded_world1_partition"] - ms_part_regions - ms_sort)
+    # fixed orchestration (samples, splitters, the count all-gather, the host sync): the one-rank
+    # partition-first run's phase before its exchange less its partition (its exchange phase is
+    # the self copy of the whole shard, 1/G of it at G ranks, overlapping the links); the
+    # chunked run's extra per chunk on top of that
+    fixed = max(0.0, world1["sharded_world1_partition_before"] - ms_part_regions)
     per_chunk = max(0.0, (world1["sharded_world1_chunked"] - world1["sharded_world1_partition"]) / a.chunks)
     pf = ms_part_regions + link_ms + ms_sort_range + fixed
     ch = ms_chunk + max((a.chunks - 1) * ms_chunk, link_ms + a.chunks * per_chunk) + ms_sort_range + fixed
