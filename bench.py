@@ -285,7 +285,7 @@ def moved_bytes(n, kb, pairs, rb, schedule):
     e = kb // 8 + (4 if pairs else 0)
     if schedule == "msd":
         k = 0
-        while k < 3 and (n >> (k + 1)) >= 65536 * 1024:
+        while k < 4 and (n >> (k + 1)) >= 65536 * 1024:
             k += 1
         return 3 * 2 * n * e + (n * (kb // 8)) // (1 << k) + (4 << 20)
     passes = -(-kb // rb)
@@ -441,8 +441,9 @@ def run_config(a, config, world, rank, local, dev, sharded, steps, warmup, dist=
         cpu_b = cpu_baseline(min(a.cpu_sample, n_local), kb, pairs, seed)
 
     # PMC bytes per launch: rocprofv3 child runs of this workload (after the timed region)
+    want_traffic = traffic
     traffic, traffic_info = None, None
-    if rank == 0 and world == 1 and not sharded and not a.no_traffic and traffic:
+    if rank == 0 and world == 1 and not sharded and not a.no_traffic and want_traffic:
         traffic_info, why = measure_traffic(a, config, options, n_local, kernel_name, dist)
         if traffic_info:
             traffic = traffic_info["bytes_per_launch"]
