@@ -1532,14 +1532,17 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   if (P3L::SMAX > P3C::SMAX) {
     constexpr int per_cu = P3L::SMAX * (sizeof(K) + (PAIRS ? 4 : 0)) <= 80 * 1024 ? 2 : 1;
     constexpr int minw = per_cu * P3L::BLOCK / GRS_WAVE / 4;
+    // (with grs_msd_copy_big's work: one launch fewer)
     hipLaunchKernelGGL((grs::grs_msd_local_list<K, PAIRS, P3L::BLOCK, P3L::I, P3L::C16, minw>),
                        dim3(per_cu * s->cus), dim3(P3L::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.mid,
-                       top);
+                       top, (const uint32_t*)bigc, (const uint32_t*)(mb + L.bin), (const uint32_t*)(mb + L.bstart),
+                       (const uint32_t*)(mb + L.blen));
+    GRS_HIP(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
+                       spill2, bigc, mb + L.bin, mb + L.bstart, mb + L.blen);
     GRS_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL((grs::grs_msd_copy_big<K, PAIRS>), dim3(4 * s->cus), dim3(256), 0, stream, rk, rv, keys, vals,
-                     spill2, bigc, mb + L.bin, mb + L.bstart, mb + L.blen);
-  GRS_HIP(hipGetLastError());
   GRS_DIAG_CHECK("P3");
   GRS_DIAG_SET(n, n);
   if ((r = mark()) != GRS_OK) return r;

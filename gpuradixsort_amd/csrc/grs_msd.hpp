@@ -1138,12 +1138,28 @@ __global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local_list(K* __restrict_
                                                             const uint32_t* __restrict__ rv,
                                                             const uint32_t* __restrict__ spill,
                                                             const uint32_t* __restrict__ mid,
-                                                            const uint32_t* __restrict__ top_shift) {
+                                                            const uint32_t* __restrict__ top_shift,
+                                                            const uint32_t* __restrict__ big = nullptr,
+                                                            const uint32_t* __restrict__ big_in = nullptr,
+                                                            const uint32_t* __restrict__ big_out = nullptr,
+                                                            const uint32_t* __restrict__ big_len = nullptr) {
   using LS = LocalSort<K, PAIRS, BLOCK, I, C16>;
   __shared__ typename LS::Smem sm;
+  const bool inplace = *spill != 0u;
+  // big (nullable): grs_msd_copy_big's work first, so that it needs no launch of its own (every
+  // workgroup takes a slice of every entry; disjoint from the mid list's segments)
+  if (big != nullptr && !inplace) {
+    const uint32_t nb = big[0];
+    for (uint32_t e = 0; e < nb; ++e) {
+      const uint32_t a = big_in[e], o = big_out[e], n = big_len[e];
+      for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        keys[o + i] = rk[a + i];
+        if constexpr (PAIRS) vals[o + i] = rv[a + i];
+      }
+    }
+  }
   const uint32_t count = mid[0];
   if (count == 0u) return;
-  const bool inplace = *spill != 0u;
   const K* const kin = inplace ? keys : rk;
   const uint32_t* const vin = inplace ? vals : rv;
   const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
