@@ -500,6 +500,9 @@ using MsdLocalB = MsdLocal<512, 20, false>;
 using MsdLocalW = MsdLocal<1024, 5, false>;   // u64 keys in A's place: 5120 keys, sixteen waves (the
                                               // two rounds + run finish, 1.40 ms at 2^28 against 1.74
                                               // for 256 x 20, tools/lab8.py round 6)
+using MsdLocalC2 = MsdLocal<768, 23, true>;   // 4-byte elements, C4's 2^30 keys: C less one item a
+                                              // thread (7 % empty slots instead of 11 %: P3 1.95 vs
+                                              // 2.04 ms at 2^30, tools/lab8.py round 6)
 using MsdLocalC = MsdLocal<768, 24, true>;    // 4-byte elements: two 72-KB workgroups per CU
 using MsdLocalD = MsdLocal<1024, 36, true>;   // 4-byte elements past 1.13G keys: one 152-KB workgroup
                                               // per CU (the MSD sort to ~2.3G keys)
@@ -1225,6 +1228,7 @@ int msd_local_shape(size_t n, size_t elem) {
   if (need <= MsdLocalM::SMAX) return 5;
   if (need <= MsdLocalA::SMAX) return 1;
   if (need <= MsdLocalB::SMAX) return 2;
+  if (elem == 4 && need <= MsdLocalC2::SMAX) return 7;
   if (elem == 4 && need <= MsdLocalC::SMAX) return 3;
   if (elem == 4 && need <= MsdLocalD::SMAX) return 6;
   return 0;
@@ -1591,6 +1595,9 @@ grs_status run_sort_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipS
       [[fallthrough]];
     case 6:
       if constexpr (sizeof(K) == 4 && !PAIRS) return run_msd<K, PAIRS, MsdLocalD>(s, keys, vals, n, stream, src_in, vsrc_in);
+      [[fallthrough]];
+    case 7:
+      if constexpr (sizeof(K) == 4 && !PAIRS) return run_msd<K, PAIRS, MsdLocalC2>(s, keys, vals, n, stream, src_in, vsrc_in);
       [[fallthrough]];
     default: return set_err(GRS_EINVAL, "internal: no MSD shape for this n");
   }

@@ -76,6 +76,7 @@ extern "C" int lab8_p3(int block, int items, int c16, int mode, int rounds, cons
   P3(256, 20, 0, 0) P3(256, 20, 0, 1) P3(256, 20, 0, 3)
   P3(512, 10, 0, 1) P3(1024, 5, 0, 1) P3(1024, 5, 1, 1)
   P3(1024, 18, 1, 1) P3(512, 36, 1, 1) P3(768, 23, 1, 1) P3(640, 28, 1, 1)
+  P3(256, 19, 0, 1) P3(768, 22, 1, 1)
 #undef P3
   return -1;
 }
