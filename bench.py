@@ -285,7 +285,7 @@ def moved_bytes(n, kb, pairs, rb, schedule):
     e = kb // 8 + (4 if pairs else 0)
     if schedule == "msd":
         k = 0
-        while k < 4 and (n >> (k + 1)) >= 65536 * 1024:
+        while k < 6 and (n >> (k + 1)) >= 65536 * 512:
             k += 1
         return 3 * 2 * n * e + (n * (kb // 8)) // (1 << k) + (4 << 20)
     passes = -(-kb // rb)

@@ -584,7 +584,7 @@ struct MsdLayout {   // word offsets into msd_buf
 size_t msd_alt_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 8 + 256 * 4096 + 1024; }
 // Elements of the third buffer (per array): P2 writes its runs into regions sized from a sample
 // of P1's output (grs_msd_plan3: at most this many, else the exact path runs).
-size_t msd_alt2_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 4 + 65536 * 64 + 1024; }
+size_t msd_alt2_words(size_t cap) { return std::max<size_t>(cap, 1) + cap / 10 * 3 + 65536 * 64 + 1024; }
 
 bool msd_type(const grs_sorter* s) {
   return s->radix_bits == 8 && !(s->key_type == GRS_KEY_U64 && s->pairs);
@@ -1414,13 +1414,14 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   K* const rk = static_cast<K*>(s->alt2_keys);
   uint32_t* const rv = PAIRS ? s->alt2_vals : nullptr;
   // H2 chunks: ~8 rounds of the resident blocks (2 per CU), 32K to 256K keys; the sample: one
-  // 2^GRS_H2_PIECE_LOG-key piece in 2^k, k so that a uniform 16-bit bin still gets ~1000 sampled keys
-  // (1/16 at 2^30: the regions' 6-sigma slack is then 19 %, inside the region buffer's 25 %)
+  // 2^GRS_H2_PIECE_LOG-key piece in 2^k, k so that a uniform 16-bit bin still gets 512-1023
+  // sampled keys (1/32 at 2^30: the regions' 6-sigma slack is then at most 26.5 %, inside the
+  // region buffer's 30 %)
   uint32_t chunk = GRS_H2_CHUNK;
   while (chunk > 32768u && static_cast<uint64_t>(n) / chunk < 16u * static_cast<uint64_t>(std::max(1, s->cus)))
     chunk >>= 1;
   uint32_t shift = 0;
-  while (shift < 4 && (static_cast<uint64_t>(n) >> (shift + 1)) >= 65536ull * 1024) ++shift;
+  while (shift < 6 && (static_cast<uint64_t>(n) >> (shift + 1)) >= 65536ull * 512) ++shift;
   chunk = std::min<uint32_t>(chunk << shift, 1u << 20);   // sampled: about as many keys a block
   if (s->h2_chunk != 0) chunk = s->h2_chunk;             // (GRS_OPT_H2_CHUNK: A/B runs)
   const uint32_t piece_log = s->h2_piece != 0 ? static_cast<uint32_t>(__builtin_ctz(s->h2_piece)) : GRS_H2_PIECE_LOG;

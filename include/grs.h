@@ -103,8 +103,8 @@ void grs_destroy(grs_sorter* s);
  *   LSD passes (radix_bits 4, u64 pairs, capacity < 48M items):  n E + ~n/1000 E
  *   + the MSD sort's scratch (8-bit digits, u32 keys / u32 pairs / u64 keys, allocated at
  *     grs_create from 48M items of capacity, or by grs_set_option(GRS_OPT_MSD, 1)):
- *     the second buffer grows to 1.125 n + 1M elements and a region buffer of 1.25 n + 4M
- *     elements joins it, ~2.4 n E in all (C4's 2^30 u32 keys: ~10 GB beside its 4.3 GB of
+ *     the second buffer grows to 1.125 n + 1M elements and a region buffer of 1.3 n + 4M
+ *     elements joins it, ~2.45 n E in all (C4's 2^30 u32 keys: ~10.5 GB beside its 4.3 GB of
  *     keys); grs_set_option(GRS_OPT_MSD, 0) releases it (the sorter then runs the LSD passes).
  * If the MSD scratch does not fit at grs_create, the sorter is created without it. */
 size_t grs_scratch_bytes(const grs_sorter* s);
