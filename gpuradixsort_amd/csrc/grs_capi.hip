@@ -1430,10 +1430,10 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
   {
     if (xl)
       hipLaunchKernelGGL((grs::grs_msd_plan2<XL::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
-                         totals, exact, chunk, tab, rec2, hdr2);
+                         totals, exact, chunk, tab, rec2, hdr2, shift == 0 ? 1u : 0u);
     else
       hipLaunchKernelGGL((grs::grs_msd_plan2<Big::TILE>), dim3(1), dim3(1024), 0, stream, samp, mult, pad,
-                         totals, exact, chunk, tab, rec2, hdr2);
+                         totals, exact, chunk, tab, rec2, hdr2, shift == 0 ? 1u : 0u);
     GRS_HIP(hipGetLastError());
     hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
                        shift ? mb + L.h2s : h2x, st[1], static_cast<uint32_t>(words2), tab, chunk, shift,
@@ -1473,8 +1473,8 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
         GRS_DIAG_CHECK("P2region");
         GRS_DIAG_SET(n, region_len);
         // the redo: exact counts, then the exact pass in place (persistent, gated by the flag)
-        hipLaunchKernelGGL((grs::grs_msd_hist2<K>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt, h2x,
-                           st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2, top);
+        hipLaunchKernelGGL((grs::grs_msd_hist2<K, T::TILE>), dim3(n / chunk + 257), dim3(1024), 0, stream, alt,
+                           h2x, st[0], static_cast<uint32_t>(words2), tab, chunk, 0u, spill2, top, 8u, rec2, hdr2);
         GRS_HIP(hipGetLastError());
         hipLaunchKernelGGL((grs::grs_onesweep_seg<K, PAIRS, 8, T::BLOCK, T::ITEMS, T::MINW, T::OPT, true>),
                            dim3(s->cus), dim3(T::BLOCK), 0, stream, alt, keys, valt, vals, d2, rec2, hdr2, h2x,

@@ -301,10 +301,18 @@ __global__ __launch_bounds__(256) void grs_msd_sample(const K* __restrict__ keys
     g[u] = i < n ? keys[pos] : K(0);
   }
   const uint32_t gs = gridDim.x * 256;
-  for (uint32_t i = blockIdx.x * 256 + t; i < clear_words; i += gs) clear[i] = 0;
-  for (uint32_t i = blockIdx.x * 256 + t; i < clear2_words; i += gs) clear2[i] = 0;
+  // the clears in 16-B stores (22 MB of P1's look-back words at 2^30: a dword a lane took most
+  // of this kernel's 20 us); the buffers are 16-B aligned, the tails word by word
+  auto zero16 = [&](uint32_t* p, uint32_t words) {
+    uint4* const q = reinterpret_cast<uint4*>(p);
+    const uint32_t nv = words / 4;
+    for (uint32_t i = blockIdx.x * 256 + t; i < nv; i += gs) q[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = nv * 4 + blockIdx.x * 256 + t; i < words; i += gs) p[i] = 0;
+  };
+  zero16(clear, clear_words);
+  zero16(clear2, clear2_words);
   constexpr uint32_t H = GRS_CTRL_HIST_WORDS, TK = GRS_MAX_PASSES * GRS_XCDS;
-  for (uint32_t i = blockIdx.x * 256 + t; i < H + TK; i += gs) clear_ctrl[i] = 0;
+  zero16(clear_ctrl, H + TK);
   K o = 0, no = 0;
 #pragma unroll
   for (uint32_t u = 0; u < GK; ++u)
@@ -435,7 +443,7 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ exact,
                                                       uint32_t chunk, uint32_t* __restrict__ tab,
                                                       SegTile* __restrict__ rec2,
-                                                      uint32_t* __restrict__ hdr2) {
+                                                      uint32_t* __restrict__ hdr2, uint32_t with_records = 1) {
   __shared__ uint32_t lds[GRS_PLAN_LDS_WORDS + 4 * 257 + 64];
   uint32_t* const in = lds + GRS_PLAN_LDS_WORDS;
   uint32_t* const len = in + 257;
@@ -444,7 +452,9 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
   uint32_t* const wsum = cpre + 257;
   msd_bucket_table(samp, mult, pad, totals, exact, chunk, in, len, out, cpre, wsum);
   for (uint32_t i = threadIdx.x; i < 4 * 257; i += 1024) tab[i] = in[i];
-  seg_plan_block<TILE2, 1024, kSegMoved>(in, len, out, 256u, nullptr, rec2, hdr2, lds);
+  // (with_records 0, a sampled P2: its exact tiles are planned by the gated exact H2 only when
+  // a region overflows -- the record loop was most of this kernel's 21 us at 2^30)
+  if (with_records != 0u) seg_plan_block<TILE2, 1024, kSegMoved>(in, len, out, 256u, nullptr, rec2, hdr2, lds);
 }
 
 // H2: h2[(top byte) * 256 + byte 2] over P1's output, one chunk of one bucket per block (grid
@@ -453,8 +463,8 @@ __global__ __launch_bounds__(1024) void grs_msd_plan2(const uint32_t* __restrict
 // `zero` (P2's status).  Two 1024-thread blocks per CU (8 waves per SIMD).  (P1 writing the
 // sample itself, the byte below its digit at one output position in 16 or in whole 1024-position
 // windows, cost P1 230 us at 2^30 for the 110 us it saved here: round 6)
-template <typename K>
-__global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ keys,
+template <typename K, uint32_t TILE2 = 0>
+__global__ __launch_bounds__(1024, TILE2 != 0 ? 4 : 8) void grs_msd_hist2(const K* __restrict__ keys,
                                                          uint32_t* __restrict__ h2,
                                                          uint32_t* __restrict__ zero,
                                                          uint32_t zero_words,
@@ -462,7 +472,9 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
                                                          uint32_t sample_shift = 0,
                                                          const uint32_t* __restrict__ gate = nullptr,
                                                          const uint32_t* __restrict__ top_shift = nullptr,
-                                                         uint32_t piece_log = 8) {
+                                                         uint32_t piece_log = 8,
+                                                         SegTile* __restrict__ rec2 = nullptr,
+                                                         uint32_t* __restrict__ hdr2 = nullptr) {
   constexpr uint32_t B = 1024;
   constexpr uint32_t LW = 256 * GRS_H2_COPIES;
   __shared__ __attribute__((aligned(16))) uint32_t h[LW];
@@ -470,6 +482,16 @@ __global__ __launch_bounds__(1024, 8) void grs_msd_hist2(const K* __restrict__ k
   const uint32_t t = threadIdx.x;
   if (gate != nullptr && __builtin_amdgcn_readfirstlane(*gate) == 0u) return;   // (the exact redo)
   for (uint32_t i = blockIdx.x * B + t; i < zero_words; i += gridDim.x * B) zero[i] = 0;
+  if constexpr (TILE2 != 0) {
+    // the exact redo after a sampled P2: the last block (never one of the chunks: the grid has
+    // 256 more blocks than n / chunk) plans the exact pass's tiles from tab's in / len / out,
+    // which grs_msd_plan2 skipped
+    __shared__ uint32_t plan_lds[GRS_PLAN_LDS_WORDS];
+    if (blockIdx.x == gridDim.x - 1) {
+      seg_plan_block<TILE2, 1024, kSegMoved>(tab, tab + 257, tab + 2 * 257, 256u, nullptr, rec2, hdr2, plan_lds);
+      return;
+    }
+  }
   for (uint32_t i = t; i < LW; i += B) h[i] = 0;
   if (t < 257) cpre[t] = tab[3 * 257 + t];
   __syncthreads();
