@@ -68,7 +68,7 @@ OPTIONS = {
     "seg_route": (12, {"shape": 0, "passes": 1, "composite": 2}),
     "h2_chunk": (13, {"size": 0}),
     "h2_piece": (14, {"default": 0}),
-    "p3": (15, {"per_segment": 0, "persistent": 1}),
+    "p3": (15, {"per_segment": 0, "persistent": 1, "whole_keys": 2}),
     "x_chunks": (16, {"default": 0}),
 }
 

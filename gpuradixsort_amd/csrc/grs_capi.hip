@@ -318,7 +318,8 @@ struct grs_sorter {
   uint32_t h2_chunk = 0;           // GRS_OPT_H2_CHUNK: 0 by size, else H2's chunk (keys per block)
   uint32_t h2_piece = 0;           // GRS_OPT_H2_PIECE: 0 default, else H2's sample piece (keys)
   int p3_mode = 0;                 // GRS_OPT_P3: 0 a workgroup per segment, 1 persistent with
-                                   // prefetch (u32 keys / pairs; measured slower, round 6)
+                                   // prefetch (u32 keys / pairs; measured slower, round 6), 2 as 0
+                                   // without the low-halves kernel for C4's size
   int seg_route = 0;               // GRS_OPT_SEG_ROUTE: 0 by shape, 1 segmented passes, 2 one
                                    // composite-key sort (grs_sort_segmented's longer segments)
   int msd_mode = -1;               // GRS_OPT_MSD: -1 by size, 0 never, 1 whenever it applies,
@@ -772,7 +773,7 @@ grs_status grs_set_option(grs_sorter* s, grs_option opt, int value) {
       s->h2_piece = static_cast<uint32_t>(value);
       break;
     case GRS_OPT_P3:
-      if (value < 0 || value > 1) return bad();
+      if (value < 0 || value > 2) return bad();
       s->p3_mode = value;
       break;
 
@@ -1522,6 +1523,13 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
                          dim3(per_cu * std::max(1, s->cus)), dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2,
                          mb + L.len2, mb + L.in2, mb + L.out2, mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart,
                          mb + L.blen, mb + L.brow, rows, top, bigc + 16);
+    } else if (!PAIRS && P3C::SMAX == MsdLocalC2::SMAX && s->p3_mode == 0) {
+      // C4's 2^30 keys: the low halves in LDS, three workgroups a CU (grs_msd_local16; tools/lab8.py
+      // round 6: 1.90 vs 1.96 ms uniform, 1.83 vs 1.99 on the reference's input).  Segments past
+      // its 17408 keys (8 sigma above the mean at 2^30) take the mid list
+      hipLaunchKernelGGL((grs::grs_msd_local16<512, 34, 6, FT::TILE>), dim3(65536), dim3(512), 0, stream,
+                         (uint32_t*)keys, vals, (const uint32_t*)rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
+                         mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows, top);
     } else {
       hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
                          dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2,

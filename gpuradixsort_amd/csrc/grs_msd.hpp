@@ -988,6 +988,145 @@ struct LocalSort {
   }
 };
 
+// P3 for u32 keys without payload: the keys of a 16-bit segment agree in bits 16..31 (the
+// prefix and the bits above the top digit; the bits sorted are below 16 whatever the top shift),
+// so LDS holds their low halves only and the registers two of them a VGPR -- half LocalSort's
+// LDS and registers, so that four 17K-key workgroups share a CU (LocalSort<u32>'s 72-KB shape:
+// two), and one segment's HBM loads and stores overlap three others' LDS rounds.  The rounds are
+// LocalSort's (lane-ordered returning LDS adds on 16-bit wave counters, stable); copy_out widens
+// each 8-B group of low halves to a 16-B store of whole keys.  rounds 1..2 (msd_p3_rounds).
+#ifndef GRS_P3H_GROUP
+#define GRS_P3H_GROUP 8
+#endif
+template <int BLOCK, int I>
+struct LocalSort16 {
+  static_assert(I % 2 == 0, "two keys a register");
+  static constexpr uint32_t W = BLOCK / GRS_WAVE, SMAX = BLOCK * I, IP = I / 2;
+  // LDS operations a wave keeps in flight in the rank and scatter loops (the scheduler would
+  // issue all I of them at once and spill at eight waves a SIMD)
+  static constexpr uint32_t G = GRS_P3H_GROUP;
+  static_assert(W <= 16 && BLOCK >= 256 && SMAX < 65536, "digit threads: waves 0..3; 16-bit counters");
+  // LocalSort::swz_t for 4-element groups: XOR of the group index inside each 64-element block
+  // with bits 8.. of x (runs 256 long would otherwise send a wave's 64 scatter targets to one bank)
+  __device__ __forceinline__ static uint32_t swz(uint32_t x) { return x ^ (((x >> 8) & 15u) << 2); }
+  // swz(base + lane) for a wave-uniform base that is a multiple of 64 (lane < 64)
+  __device__ __forceinline__ static uint32_t swz_row(uint32_t base, uint32_t lane) {
+    return base + (lane ^ (((base >> 8) & 15u) << 2));
+  }
+  static constexpr uint32_t SK = (SMAX + 4 + 63) / 64 * 64;   // SMAX slots + an alignment shift < 4
+  struct Smem {
+    alignas(16) uint16_t sk[SK];
+    uint32_t cnt[W * 128];   // 16-bit counters, two a word
+    uint32_t spare[GRS_WAVE];   // the ranking's adds for slots past the keys
+    uint32_t wtot[4];
+    uint32_t slot;
+  };
+  __device__ __forceinline__ static uint32_t half(const uint32_t (&p)[IP], uint32_t j) {
+    return (p[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+  }
+  // kin[0, len) -> kout[0, len) sorted by bits 0 .. 8 * rounds (rounds 0: the load + store
+  // skeleton of the lab, LDS left unwritten).  The slots past len skip the ranking (lanes of one
+  // digit would serialise on its counter) and scatter to their own index, past the keys
+  __device__ __forceinline__ static void run(Smem& sm, const uint32_t* kin, uint32_t* kout, uint32_t len,
+                                             int rounds) {
+    const uint32_t t = threadIdx.x, lane = t & (GRS_WAVE - 1), w = t >> 6;
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(kin[0]) & 0xFFFF0000u;
+    // the low halves only (2-B buffer loads of the same lines: unpredicated, the descriptor's
+    // range check drops the slots past len, one offset register for all I), packed two a register
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(kin), 0, static_cast<int>(4u * len),
+                                                        0x00020000);
+    // (wave-uniform bases: the per-item parts of offsets and bounds stay scalar)
+    const uint32_t ws = __builtin_amdgcn_readfirstlane(w), wbase = ws * GRS_WAVE * I;
+    const uint32_t wlen = len > wbase ? len - wbase : 0u;   // this wave's slots holding keys
+    uint32_t kp[IP];
+#pragma unroll
+    for (uint32_t j = 0; j < IP; ++j) {
+      const uint32_t a = __builtin_amdgcn_raw_buffer_load_b16(rsrc, 4u * lane, 4u * (wbase + 2u * j * GRS_WAVE), 0);
+      const uint32_t b = __builtin_amdgcn_raw_buffer_load_b16(rsrc, 4u * lane, 4u * (wbase + (2u * j + 1u) * GRS_WAVE), 0);
+      kp[j] = (a & 0xFFFFu) | (b << 16);
+    }
+    const uint32_t ak = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(kout) / 4u) % 4u;
+    uint16_t* const c16 = reinterpret_cast<uint16_t*>(sm.cnt);
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass >= rounds) break;   // (uniform)
+      const uint32_t shift = 8u * static_cast<uint32_t>(pass);
+      for (uint32_t c = t; c < W * 128; c += BLOCK) sm.cnt[c] = 0;
+      __syncthreads();
+      uint32_t rp[IP];
+#pragma unroll
+      for (uint32_t j = 0; j < I; ++j) {
+        const uint32_t d = (half(kp, j) >> shift) & 255u, sh = (d & 1u) << 4;
+        // a slot past the keys adds to its lane's own spare word (no predicate, no serialising
+        // lanes on one counter)
+        const bool ok = lane + j * GRS_WAVE < wlen;
+        const uint32_t r = (atomicAdd(ok ? &sm.cnt[(w * 256 + d) >> 1] : &sm.spare[lane], 1u << sh) >> sh) & 0xFFFFu;
+        if (j & 1) rp[j >> 1] |= r << 16;
+        else rp[j >> 1] = r;
+        if (j % G == G - 1) __builtin_amdgcn_sched_barrier(0);   // G returning adds in flight
+      }
+      // opaque: the scatter recomputes each half and digit from the packed registers (the
+      // compiler would keep I unpacked halves and I digits live across the scan and spill them)
+#pragma unroll
+      for (uint32_t j = 0; j < IP; ++j) asm volatile("" : "+v"(kp[j]), "+v"(rp[j]));
+      __syncthreads();
+      uint32_t c[W], tot = 0, incl = 0;
+      if (t < 256) {
+#pragma unroll
+        for (uint32_t ww = 0; ww < W; ++ww) {
+          c[ww] = c16[ww * 256 + t];
+          tot += c[ww];
+        }
+        incl = wave_scan_dpp(tot);
+        if (lane == GRS_WAVE - 1) sm.wtot[w] = incl;
+      }
+      __syncthreads();
+      if (t < 256) {
+        uint32_t b = incl - tot;
+#pragma unroll
+        for (uint32_t ww = 0; ww < 4; ++ww) b += ww < w ? sm.wtot[ww] : 0u;
+#pragma unroll
+        for (uint32_t ww = 0; ww < W; ++ww) {
+          c16[ww * 256 + t] = static_cast<uint16_t>(b);
+          b += c[ww];
+        }
+      }
+      __syncthreads();
+      const uint32_t off = pass + 1 >= rounds ? ak : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < I; ++j) {
+        const uint32_t x = half(kp, j);
+        const uint32_t dst = lane + j * GRS_WAVE < wlen ? c16[w * 256 + ((x >> shift) & 255u)] + half(rp, j)
+                                                        : wbase + j * GRS_WAVE + lane;
+        sm.sk[swz(dst + off)] = static_cast<uint16_t>(x);
+        if (j % G == G - 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();
+      if (pass + 1 < rounds) {
+#pragma unroll
+        for (uint32_t j = 0; j < IP; ++j) {
+          const uint32_t b0 = wbase + 2u * j * GRS_WAVE, b1 = b0 + GRS_WAVE;
+          kp[j] = static_cast<uint32_t>(sm.sk[swz_row(b0, lane)]) | (static_cast<uint32_t>(sm.sk[swz_row(b1, lane)]) << 16);
+        }
+      }
+    }
+    // sm.sk[ak + p] -> kout[p] in 16-B stores (head / tail peeled to kout's 16-B alignment), the
+    // workgroup's vectors rotated as LocalSort::copy_out's
+    const uint32_t head = min(len, (4u - ak) % 4u), nv = (len - head) / 4u;
+    if (t < head) kout[t] = hi | sm.sk[swz(ak + t)];
+    uint4* const dst = reinterpret_cast<uint4*>(kout + head);
+    const uint32_t rot = nv != 0u ? ((blockIdx.x * 97u & 255u) * 16u) % nv : 0u;
+    for (uint32_t c = t; c < nv; c += BLOCK) {
+      uint32_t r = c + rot;
+      if (r >= nv) r -= nv;
+      const uint2 g = *reinterpret_cast<const uint2*>(sm.sk + swz(ak + head + r * 4u));
+      dst[r] = make_uint4(hi | (g.x & 0xFFFFu), hi | (g.x >> 16), hi | (g.y & 0xFFFFu), hi | (g.y >> 16));
+    }
+    const uint32_t r = head + nv * 4u + t;
+    if (r < len) kout[r] = hi | sm.sk[swz(ak + r)];
+  }
+};
+
 // P3: one workgroup per 16-bit prefix b (grid 65536): its len2[b] keys (and payload), read at
 // in2[b] of the region buffer (rk / rv) -- or, after a P2 spill, of the caller's arrays, in
 // place -- sorted in LDS (LocalSort) and written to out2[b] of the caller's arrays
@@ -1081,6 +1220,33 @@ __global__ __launch_bounds__(BLOCK) void grs_msd_local(K* __restrict__ keys, uin
   const int rounds = msd_p3_rounds<LS::ROUNDS>(__builtin_amdgcn_readfirstlane(*top_shift));
   LS::template run_vec<>(sm, kin + lo, PAIRS ? vin + lo : nullptr, keys + o, PAIRS ? vals + o : nullptr, len,
                          rounds);
+}
+
+// P3 of u32 keys without payload on LocalSort16 (the low halves in LDS; three 512 x 34
+// workgroups a CU at 2^30 keys instead of LocalSort's two 768 x 23): grs_msd_local's tables,
+// lists and results.
+template <int BLOCK, int I, int MINW, uint32_t TILEF>
+__global__ __launch_bounds__(BLOCK, MINW) void grs_msd_local16(
+    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, const uint32_t* __restrict__ rk,
+    const uint32_t* __restrict__ rv, const uint32_t* __restrict__ spill, const uint32_t* __restrict__ len2,
+    const uint32_t* __restrict__ in2, const uint32_t* __restrict__ out2, uint32_t mid_max, uint32_t* __restrict__ mid,
+    uint32_t* __restrict__ big, uint32_t* __restrict__ big_in, uint32_t* __restrict__ big_start,
+    uint32_t* __restrict__ big_len, uint32_t* __restrict__ big_row, uint32_t* __restrict__ rows,
+    const uint32_t* __restrict__ top_shift) {
+  using LS = LocalSort16<BLOCK, I>;
+  __shared__ typename LS::Smem sm;
+  const uint32_t len = len2[blockIdx.x];
+  if (len == 0u) return;
+  const bool inplace = __builtin_amdgcn_readfirstlane(*spill) != 0u;
+  const uint32_t lo = in2[blockIdx.x], o = out2[blockIdx.x];
+  const uint32_t* const kin = inplace ? keys : rk;
+  if (len == 1u || len > LS::SMAX) {
+    msd_local_other<uint32_t, false, BLOCK, LS::SMAX, 2, TILEF>(len, lo, o, inplace, kin, nullptr, keys, vals, mid_max,
+                                                                mid, big, big_in, big_start, big_len, big_row, rows,
+                                                                sm.slot);
+    return;
+  }
+  LS::run(sm, kin + lo, keys + o, len, msd_p3_rounds<2>(__builtin_amdgcn_readfirstlane(*top_shift)));
 }
 
 // P3 persistent (keys sorted in at most two LDS rounds: u32 keys, u32 pairs): grid = resident

@@ -201,8 +201,10 @@ typedef enum grs_option {
   GRS_OPT_H2_PIECE = 14,     /* the same histogram's sample: 0 (default) pieces of 256 keys, else
                                 the keys of a piece (a power of two, 64..4096; A/B runs) */
   GRS_OPT_P3 = 15,           /* the MSD sort's LDS segment sort, u32 keys and u32 pairs: 0
-                                (default) one workgroup per segment, 1 persistent workgroups that
-                                load the next segment while storing this one (slower; A/B runs) */
+                                (default) one workgroup per segment (u32 keys at ~2^30: the low
+                                halves in LDS, three workgroups a CU), 1 persistent workgroups that
+                                load the next segment while storing this one (slower; A/B runs),
+                                2 one workgroup per segment, whole keys in LDS (A/B runs) */
   GRS_OPT_X_CHUNKS = 16      /* chunks of the chunked exchange (GRS_OPT_EXCHANGE = 3): 0 (default)
                                 4, else 1..16; the same on every rank */
 } grs_option;

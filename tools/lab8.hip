@@ -46,7 +46,35 @@ __global__ __launch_bounds__(BLOCK) void lab_p3w(const uint64_t* __restrict__ in
   else LS::template run_vec<>(sm, kin, nullptr, kout, nullptr, len, rounds);
 }
 
+// u32 keys, low halves in LDS (grs::LocalSort16, round 7 of the lab): MINW waves a SIMD
+template <int BLOCK, int I, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void lab_p3h(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       const uint32_t* __restrict__ inoff,
+                                                       const uint32_t* __restrict__ outoff,
+                                                       const uint32_t* __restrict__ lens, int rounds) {
+  using LS = grs::LocalSort16<BLOCK, I>;
+  __shared__ typename LS::Smem sm;
+  const uint32_t len = lens[blockIdx.x];
+  if (len == 0) return;
+  LS::run(sm, in + inoff[blockIdx.x], out + outoff[blockIdx.x], len, rounds);
+}
+
 }  // namespace
+
+extern "C" int lab8_p3h(int block, int items, int minw, int rounds, const uint32_t* in, uint32_t* out,
+                        const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens, uint32_t nseg,
+                        void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define P3H(B, I, M)                                                                                          \
+  if (block == B && items == I && minw == M) {                                                              \
+    hipLaunchKernelGGL((lab_p3h<B, I, M>), dim3(nseg), dim3(B), 0, s, in, out, inoff, outoff, lens, rounds);   \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                        \
+  }
+  P3H(512, 34, 8) P3H(512, 36, 6) P3H(256, 68, 4) P3H(768, 24, 6) P3H(512, 34, 6) P3H(256, 68, 5)
+  P3H(256, 20, 8) P3H(256, 16, 8) P3H(512, 10, 8)
+#undef P3H
+  return -1;
+}
 
 extern "C" int lab8_p3w(int block, int items, int mode, int rounds, const uint64_t* in, uint64_t* out,
                         const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens, uint32_t nseg,

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--shapes", default="768:24:1")
     ap.add_argument("--modes", default="0,1,3")
     ap.add_argument("--u64-shapes", default="256:20,512:10,1024:5")
+    ap.add_argument("--half-shapes", default="",
+                    help="grs::LocalSort16 (low halves in LDS) shapes block:items:minw, e.g. 512:36:6")
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--exact", action="store_true",
                     help="segments of exactly n / 65536 keys, no gaps (every run 16-B... 64-KB aligned, as the "
@@ -80,7 +82,9 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     print(f"n {n}, segments {nseg} of {m} +- {sd}, regions at gaps 0..256 (+3); exact={a.exact} "
           f"perm_keys={a.perm_keys}", flush=True)
-    for spec in a.shapes.split(","):
+    if a.half_shapes:
+        run_half(a, keys, out, d_in, d_out, d_len, nseg, n, m, sd, want, stream, e0, e1)
+    for spec in filter(None, a.shapes.split(",")):
         b, it, c16 = (int(x) for x in spec.split(":"))
         if b * it < m + sd:
             print(f"{spec}: segments too long for the shape", flush=True)
@@ -103,6 +107,28 @@ def main():
                     ok = f" sorted={bool(torch.equal(out[:n].to(torch.int64) & 0xFFFFFFFF, want))}"
                 print(f"p3 {spec} mode {mode} ({NAMES[mode]:22s}) rounds={rounds}: {ms * 1e3:8.1f} us "
                       f"{n * 8 / ms / 1e6:7.1f} GB/s ({n * 8 / ms / 1e6 / 8000:.3f} of 8 TB/s){ok}", flush=True)
+
+
+def run_half(a, keys, out, d_in, d_out, d_len, nseg, n, m, sd, want, stream, e0, e1):
+    for spec in filter(None, a.half_shapes.split(",")):
+        b, it, minw = (int(x) for x in spec.split(":"))
+        if b * it < m + sd:
+            print(f"half {spec}: segments too long for the shape", flush=True)
+            continue
+        for rounds in (0, 2):
+            ts = []
+            for _ in range(a.reps):
+                e0.record()
+                rc = L.lab8_p3h(b, it, minw, rounds, vp(keys.data_ptr()), vp(out.data_ptr()), vp(d_in.data_ptr()),
+                                vp(d_out.data_ptr()), vp(d_len.data_ptr()), nseg, stream)
+                e1.record()
+                torch.cuda.synchronize()
+                assert rc == 0, (spec, rc)
+                ts.append(e0.elapsed_time(e1))
+            ms = statistics.median(ts)
+            ok = f" sorted={bool(torch.equal(out[:n].to(torch.int64) & 0xFFFFFFFF, want))}" if rounds else ""
+            print(f"p3 half {spec} (LocalSort16) rounds={rounds}: {ms * 1e3:8.1f} us "
+                  f"{n * 8 / ms / 1e6:7.1f} GB/s ({n * 8 / ms / 1e6 / 8000:.3f} of 8 TB/s){ok}", flush=True)
 
 
 def run_u64(a, dev, nseg, m, sd, lens, inoff, outoff, total_in, n):
