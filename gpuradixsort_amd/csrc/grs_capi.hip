@@ -1222,9 +1222,13 @@ grs_status run_sort(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, int begi
 // The P3 shape for n elements of E bytes: a uniform 16-bit segment holds m = n / 65536, +-
 // sqrt(m); the shape must take m + 8 sqrt(m) + 64 (longer segments take the segmented
 // fallback).  0: none fits (the LSD sort).
-int msd_local_shape(size_t n, size_t elem) {
+double msd_segment_need(size_t n) {
   const double m = static_cast<double>(n) / 65536.0;
-  const double need = m + 8.0 * std::sqrt(m) + 64.0;
+  return m + 8.0 * std::sqrt(m) + 64.0;
+}
+
+int msd_local_shape(size_t n, size_t elem) {
+  const double need = msd_segment_need(n);
   if (need <= MsdLocalS::SMAX) return 4;
   if (need <= MsdLocalM::SMAX) return 5;
   if (need <= MsdLocalA::SMAX) return 1;
@@ -1530,6 +1534,13 @@ grs_status run_msd(grs_sorter* s, K* keys, uint32_t* vals, uint32_t n, hipStream
       hipLaunchKernelGGL((grs::grs_msd_local16<512, 34, 6, FT::TILE>), dim3(65536), dim3(512), 0, stream,
                          (uint32_t*)keys, vals, (const uint32_t*)rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
                          mid_max, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows, top);
+    } else if (!PAIRS && P3C::SMAX == MsdLocalD::SMAX && s->p3_mode == 0 && msd_segment_need(n) <= 1024 * 34) {
+      // past 1.13G keys up to ~2.18G: 1024 x 34 low halves, two workgroups a CU where LocalSort's
+      // 1024 x 36 fits one (lab at 2^31: 4.81 vs ~5.3 ms).  No mid list in this shape's sort: a
+      // segment past 34816 keys takes the fallback
+      hipLaunchKernelGGL((grs::grs_msd_local16<1024, 34, 8, FT::TILE>), dim3(65536), dim3(1024), 0, stream,
+                         (uint32_t*)keys, vals, (const uint32_t*)rk, rv, spill2, mb + L.len2, mb + L.in2, mb + L.out2,
+                         1024u * 34u, mb + L.mid, bigc, mb + L.bin, mb + L.bstart, mb + L.blen, mb + L.brow, rows, top);
     } else {
       hipLaunchKernelGGL((grs::grs_msd_local<K, PAIRS, P3C::BLOCK, P3C::I, P3C::C16, FT::TILE>), dim3(65536),
                          dim3(P3C::BLOCK), 0, stream, keys, vals, rk, rv, spill2, mb + L.len2, mb + L.in2,

@@ -71,7 +71,8 @@ extern "C" int lab8_p3h(int block, int items, int minw, int rounds, const uint32
     return hipGetLastError() == hipSuccess ? 0 : -2;                                                        \
   }
   P3H(512, 34, 8) P3H(512, 36, 6) P3H(256, 68, 4) P3H(768, 24, 6) P3H(512, 34, 6) P3H(256, 68, 5)
-  P3H(256, 20, 8) P3H(256, 16, 8) P3H(512, 10, 8)
+  P3H(256, 20, 8) P3H(256, 16, 8) P3H(512, 10, 8) P3H(768, 46, 6) P3H(1024, 34, 8) P3H(512, 68, 4)
+  P3H(1024, 36, 4)
 #undef P3H
   return -1;
 }
