@@ -317,3 +317,37 @@ def test_c4_size_distributions(gpu, name):
     assert grs.count_inversions(k) == 0
     assert checks(k) == before
     s.close()
+
+
+def test_p3_low_halves_lists(gpu):
+    """P3 on the low 16 bits in LDS (grs_msd_local16, the u32 P3 from ~0.6G keys, 512 x 34 slots)
+    against the whole-key kernel (option p3 = whole_keys) on the same 700M keys, with one 16-bit
+    segment pushed past 17408 keys into the mid list (~18K keys) and one into the fallback (~41K):
+    identical output, sorted, the same multiset, no guard word touched."""
+    import gpuradixsort_amd as grs
+
+    n = 700_000_000
+    src = torch.empty(n, dtype=torch.uint32, device=gpu)
+    grs.fill_splitmix(src, 0x3C6EF372FE94F82B)
+    v = src.view(torch.int32)
+    v[:7300] = (v[:7300] & 0xFFFF) | (0x1234 << 16)
+    v[7300:37300] = (v[7300:37300] & 0xFFFF) | (0x4321 << 16)
+    before = _checksums(src)
+    outs = []
+    for mode in ("per_segment", "whole_keys"):
+        k = src.clone()
+        s = grs.RadixSorter(n, key_bits=32)
+        s.set_option("p3", mode)
+        s.sort(k)
+        s.check_error()
+        assert s.check_guards() == 0, mode
+        s.close()
+        outs.append(k)
+    del src
+    assert torch.equal(outs[0], outs[1])
+    assert grs.count_inversions(outs[0]) == 0
+    assert _checksums(outs[0]) == before
+    hi = (outs[0].view(torch.int32) >> 16) & 0xFFFF
+    assert int((hi == 0x1234).sum().item()) > 17408 and int((hi == 0x4321).sum().item()) > 36864
+    del outs, hi
+    torch.cuda.empty_cache()
