@@ -9,6 +9,8 @@
 // against 1829 for MODE 3; skeleton 1634 vs 1670)
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../gpuradixsort_amd/csrc/grs_msd.hpp"
 
 namespace {
@@ -59,7 +61,54 @@ __global__ __launch_bounds__(BLOCK, MINW) void lab_p3h(const uint32_t* __restric
   LS::run(sm, in + inoff[blockIdx.x], out + outoff[blockIdx.x], len, rounds);
 }
 
+// persistent P3 with a static segment stride (no ticket): the next segment's table entries are
+// read while this one sorts, and its key loads follow this one's stores at once (HALF: LocalSort16)
+template <int BLOCK, int I, int MINW, bool HALF>
+__global__ __launch_bounds__(BLOCK, MINW) void lab_p3s(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       const uint32_t* __restrict__ inoff,
+                                                       const uint32_t* __restrict__ outoff,
+                                                       const uint32_t* __restrict__ lens, uint32_t nseg, int rounds) {
+  using LS = grs::LocalSort<uint32_t, false, BLOCK, I, (BLOCK > 256), 2>;
+  using LH = grs::LocalSort16<BLOCK, (I + 1) / 2 * 2>;
+  __shared__ std::conditional_t<HALF, typename LH::Smem, typename LS::Smem> sm;
+  uint32_t b = blockIdx.x;
+  uint32_t len = lens[b], io = inoff[b], oo = outoff[b];
+  for (; b < nseg; b += gridDim.x) {
+    const uint32_t nb = b + gridDim.x;
+    uint32_t nlen = 0, nio = 0, noo = 0;
+    if (nb < nseg) {
+      nlen = lens[nb];
+      nio = inoff[nb];
+      noo = outoff[nb];
+    }
+    if (len != 0) {
+      if constexpr (HALF) LH::run(sm, in + io, out + oo, len, rounds);
+      else LS::template run_vec<>(sm, in + io, nullptr, out + oo, nullptr, len, rounds);
+    }
+    __syncthreads();   // (LDS reuse by the next segment)
+    len = nlen;
+    io = nio;
+    oo = noo;
+  }
+}
+
 }  // namespace
+
+extern "C" int lab8_p3s(int block, int items, int minw, int half, int grid, int rounds, const uint32_t* in,
+                        uint32_t* out, const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens,
+                        uint32_t nseg, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (grid <= 0 || static_cast<uint32_t>(grid) > nseg) return -3;
+#define P3S(B, I, M, H)                                                                                   \
+  if (block == B && items == I && minw == M && half == H) {                                               \
+    hipLaunchKernelGGL((lab_p3s<B, I, M, H != 0>), dim3(grid), dim3(B), 0, s, in, out, inoff, outoff, lens, \
+                       nseg, rounds);                                                                     \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                      \
+  }
+  P3S(256, 20, 6, 0) P3S(256, 20, 8, 0) P3S(768, 23, 6, 0) P3S(512, 34, 6, 1) P3S(256, 20, 8, 1)
+#undef P3S
+  return -1;
+}
 
 extern "C" int lab8_p3h(int block, int items, int minw, int rounds, const uint32_t* in, uint32_t* out,
                         const uint32_t* inoff, const uint32_t* outoff, const uint32_t* lens, uint32_t nseg,

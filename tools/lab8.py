@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--u64-shapes", default="256:20,512:10,1024:5")
     ap.add_argument("--half-shapes", default="",
                     help="grs::LocalSort16 (low halves in LDS) shapes block:items:minw, e.g. 512:36:6")
+    ap.add_argument("--persistent", default="",
+                    help="persistent static-stride P3 block:items:minw:half:grid_per_cu, e.g. 256:20:6:0:6")
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--exact", action="store_true",
                     help="segments of exactly n / 65536 keys, no gaps (every run 16-B... 64-KB aligned, as the "
@@ -84,6 +86,8 @@ def main():
           f"perm_keys={a.perm_keys}", flush=True)
     if a.half_shapes:
         run_half(a, keys, out, d_in, d_out, d_len, nseg, n, m, sd, want, stream, e0, e1)
+    if a.persistent:
+        run_persistent(a, keys, out, d_in, d_out, d_len, nseg, n, m, sd, want, stream, e0, e1)
     for spec in filter(None, a.shapes.split(",")):
         b, it, c16 = (int(x) for x in spec.split(":"))
         if b * it < m + sd:
@@ -128,6 +132,29 @@ def run_half(a, keys, out, d_in, d_out, d_len, nseg, n, m, sd, want, stream, e0,
             ms = statistics.median(ts)
             ok = f" sorted={bool(torch.equal(out[:n].to(torch.int64) & 0xFFFFFFFF, want))}" if rounds else ""
             print(f"p3 half {spec} (LocalSort16) rounds={rounds}: {ms * 1e3:8.1f} us "
+                  f"{n * 8 / ms / 1e6:7.1f} GB/s ({n * 8 / ms / 1e6 / 8000:.3f} of 8 TB/s){ok}", flush=True)
+
+
+def run_persistent(a, keys, out, d_in, d_out, d_len, nseg, n, m, sd, want, stream, e0, e1):
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for spec in filter(None, a.persistent.split(",")):
+        b, it, minw, half, per_cu = (int(x) for x in spec.split(":"))
+        if b * it < m + sd:
+            print(f"persistent {spec}: segments too long for the shape", flush=True)
+            continue
+        for rounds in (2,):
+            ts = []
+            for _ in range(a.reps):
+                e0.record()
+                rc = L.lab8_p3s(b, it, minw, half, per_cu * cus, rounds, vp(keys.data_ptr()), vp(out.data_ptr()),
+                                vp(d_in.data_ptr()), vp(d_out.data_ptr()), vp(d_len.data_ptr()), nseg, stream)
+                e1.record()
+                torch.cuda.synchronize()
+                assert rc == 0, (spec, rc)
+                ts.append(e0.elapsed_time(e1))
+            ms = statistics.median(ts)
+            ok = f" sorted={bool(torch.equal(out[:n].to(torch.int64) & 0xFFFFFFFF, want))}"
+            print(f"p3 persistent {spec} (grid {per_cu} x {cus}) rounds={rounds}: {ms * 1e3:8.1f} us "
                   f"{n * 8 / ms / 1e6:7.1f} GB/s ({n * 8 / ms / 1e6 / 8000:.3f} of 8 TB/s){ok}", flush=True)
 
 
