@@ -319,19 +319,28 @@ def test_c4_size_distributions(gpu, name):
     s.close()
 
 
-def test_p3_low_halves_lists(gpu):
+@pytest.mark.parametrize("dist", ["lists", "narrow28", "perm"])
+def test_p3_low_halves_lists(gpu, dist):
     """P3 on the low 16 bits in LDS (grs_msd_local16, the u32 P3 from ~0.6G keys, 512 x 34 slots)
-    against the whole-key kernel (option p3 = whole_keys) on the same 700M keys, with one 16-bit
-    segment pushed past 17408 keys into the mid list (~18K keys) and one into the fallback (~41K):
-    identical output, sorted, the same multiset, no guard word touched."""
+    against the whole-key kernel (option p3 = whole_keys) on the same 700M keys: identical
+    output, sorted, the same multiset, no guard word touched.  lists: uniform keys with one
+    16-bit segment pushed past 17408 keys into the mid list (~18K keys) and one into the fallback
+    (~41K); narrow28: keys below 2^28 (the top digit at bit 20, P3's bits 12..15 constant in a
+    segment); perm: the reference's 0..n-1 shuffled (top digit at bit 22)."""
     import gpuradixsort_amd as grs
 
     n = 700_000_000
     src = torch.empty(n, dtype=torch.uint32, device=gpu)
-    grs.fill_splitmix(src, 0x3C6EF372FE94F82B)
+    if dist == "perm":
+        grs.fill_permutation(src, 0x5EED7)
+    else:
+        grs.fill_splitmix(src, 0x3C6EF372FE94F82B)
     v = src.view(torch.int32)
-    v[:7300] = (v[:7300] & 0xFFFF) | (0x1234 << 16)
-    v[7300:37300] = (v[7300:37300] & 0xFFFF) | (0x4321 << 16)
+    if dist == "lists":
+        v[:7300] = (v[:7300] & 0xFFFF) | (0x1234 << 16)
+        v[7300:37300] = (v[7300:37300] & 0xFFFF) | (0x4321 << 16)
+    elif dist == "narrow28":
+        v &= (1 << 28) - 1
     before = _checksums(src)
     outs = []
     for mode in ("per_segment", "whole_keys"):
@@ -341,13 +350,20 @@ def test_p3_low_halves_lists(gpu):
         s.sort(k)
         s.check_error()
         assert s.check_guards() == 0, mode
+        f = s.msd_flags()
         s.close()
         outs.append(k)
     del src
     assert torch.equal(outs[0], outs[1])
     assert grs.count_inversions(outs[0]) == 0
     assert _checksums(outs[0]) == before
-    hi = (outs[0].view(torch.int32) >> 16) & 0xFFFF
-    assert int((hi == 0x1234).sum().item()) > 17408 and int((hi == 0x4321).sum().item()) > 36864
-    del outs, hi
+    if dist == "lists":
+        hi = (outs[0].view(torch.int32) >> 16) & 0xFFFF
+        assert int((hi == 0x1234).sum().item()) > 17408 and int((hi == 0x4321).sum().item()) > 36864
+        del hi
+    else:
+        assert f["top_shift"] == (20 if dist == "narrow28" else 22), f
+    if dist == "perm":
+        assert int(outs[0][:1].view(torch.int32).item()) == 0 and int(outs[0][-1:].view(torch.int32).item()) == n - 1
+    del outs
     torch.cuda.empty_cache()
